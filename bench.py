@@ -1,0 +1,301 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X sort path (BASELINE.json metric: sorted keys/sec, int32, 2^30 keys).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--keys N_TOTAL] [--dtype i32|i64]
+                    [--dist uniform|zipf] [--no-cpu-baseline]
+
+One step = one full sort of the synthetic batch with the input already resident in HBM:
+  N = 1: dsort_sort_dev_copy (tile sort + merge-path passes) of all keys on one GPU.
+  N > 1: launched by torch.distributed.run, one process per GPU; every rank holds an equal
+         contiguous chunk (server.c:185-216 partitioning) and the step is the sample sort
+         (local sort + splitters + RCCL all-to-all over xGMI + merge of the received runs).
+         The total key count stays fixed (strong scaling), as the metric is quoted on 2^30 keys.
+The sorted output is verified outside the timed region (ascending + multiset fingerprint).
+
+Prints ONE JSON line on rank 0 (contract in the task statement) with two extra objects:
+  roofline      live HIP-event timing of the dominant kernel (the merge-path merge kernel) and
+                its algorithmic bytes (2*w bytes per key per launch) against 8 TB/s;
+  cpu_baseline  the reference's own algorithm (client.c merge_sort on 4 threads + server.c
+                merge_chunks, compiled from the reference sources into oracle/_ref) on a bounded
+                sample, timed on this host's cores.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import tempfile
+import threading
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "distributed-sorting-with-fault-tolerance_amd")
+sys.path.insert(0, PKG)
+
+import torch  # noqa: E402  (before dsort: one HIP runtime)
+import dsort  # noqa: E402
+
+SEED = 0x5EED2026
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--keys", type=lambda s: int(eval(s, {}, {})), default=1 << 30,
+                    help="total keys (e.g. 2**30)")
+    ap.add_argument("--dtype", choices=["i32", "i64"], default="i32")
+    ap.add_argument("--dist", choices=["uniform", "zipf"], default="uniform")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-keys", type=lambda s: int(eval(s, {}, {})), default=1 << 25)
+    return ap.parse_args()
+
+
+# ------------------------------------------------------------------------- CPU baseline
+def cpu_baseline(sample_keys):
+    """The reference algorithm on the host: 4 worker threads each run the reference's
+    merge_sort (client.c:166) on an equal contiguous chunk (server.c:185-216), then the
+    reference's merge_chunks (server.c:481, linear argmin 4-way merge + output.txt text write).
+    Uses oracle/_ref (reference compiled from its sources); falls back to the oracle restatement
+    (kind "port") when that build is absent."""
+    ref_dir = os.path.join(REPO, "oracle", "_ref")
+    workers = 4
+    keys = np.empty(sample_keys, np.int32)
+    orc_path = os.path.join(REPO, "oracle", "liboracle.so")
+    orc = ctypes.CDLL(orc_path)
+    orc.oracle_gen_uniform_i32.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_void_p]
+    orc.oracle_gen_uniform_i32(SEED, 0, sample_keys, keys.ctypes.data)
+    sz = [sample_keys // workers + (1 if i < sample_keys % workers else 0) for i in range(workers)]
+    offs = np.concatenate([[0], np.cumsum(sz)[:-1]]).astype(np.int64)
+    chunks = [keys[o:o + s].copy() for o, s in zip(offs, sz)]
+    kind = "reference"
+    try:
+        cl = ctypes.CDLL(os.path.join(ref_dir, "libref_client.so"))
+        sv = ctypes.CDLL(os.path.join(ref_dir, "libref_server.so"))
+        cl.merge_sort.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        sv.merge_chunks.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        sort_fn = lambda c: cl.merge_sort(c.ctypes.data, 0, c.size - 1)  # noqa: E731
+
+        def merge_fn(cs, total):
+            ptrs = (ctypes.c_void_p * workers)(*[c.ctypes.data for c in cs])
+            lens = (ctypes.c_int * workers)(*[c.size for c in cs])
+            sv.merge_chunks(workers, ptrs, lens, total)
+    except OSError:
+        kind = "port"
+        orc.oracle_merge_sort_i32.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+        orc.oracle_merge_chunks_i32.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        orc.oracle_format_i32.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]
+        orc.oracle_format_i32.restype = ctypes.c_long
+        sort_fn = lambda c: orc.oracle_merge_sort_i32(c.ctypes.data, c.size)  # noqa: E731
+
+        def merge_fn(cs, total):
+            ptrs = (ctypes.c_void_p * workers)(*[c.ctypes.data for c in cs])
+            lens = (ctypes.c_size_t * workers)(*[c.size for c in cs])
+            out = np.zeros(total, np.int32)
+            orc.oracle_merge_chunks_i32(workers, ptrs, lens, out.ctypes.data)
+            buf = ctypes.create_string_buffer(12 * total + 1)
+            n = orc.oracle_format_i32(out.ctypes.data, total, buf, len(buf))
+            with open("output.txt", "wb") as f:
+                f.write(buf.raw[:n])
+
+    cwd = os.getcwd()
+    with tempfile.TemporaryDirectory() as d:
+        os.chdir(d)
+        try:
+            t0 = time.perf_counter()
+            th = [threading.Thread(target=sort_fn, args=(c,)) for c in chunks]  # ctypes drops the GIL
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            t1 = time.perf_counter()
+            merge_fn(chunks, sample_keys)
+            t2 = time.perf_counter()
+        finally:
+            os.chdir(cwd)
+    ok = all(np.all(c[:-1] <= c[1:]) for c in chunks)
+    return {
+        "value": sample_keys / (t2 - t0), "unit": "sorted keys/s", "cores": workers, "kind": kind,
+        "sample": (f"{sample_keys} uniform int32 keys (seed {SEED:#x}); 4 threads x reference merge_sort "
+                   f"on equal chunks ({t1 - t0:.2f} s) + reference merge_chunks incl. output.txt "
+                   f"text write ({t2 - t1:.2f} s); host nproc={os.cpu_count()}; chunks sorted={ok}"),
+    }
+
+
+# ------------------------------------------------------------------------- GPU runs
+def make_input(ctx, n, first, dtype, dist):
+    tdt = torch.int32 if dtype == "i32" else torch.int64
+    t = torch.empty(max(n, 1), dtype=tdt, device="cuda")[:n]
+    if dist == "zipf":
+        if dtype != "i64":
+            raise SystemExit("zipf is defined for int64 keys (BASELINE config 4)")
+        ctx.gen_zipf_i64(t, SEED, first)
+    else:
+        ctx.gen_uniform(t, SEED, first)
+    torch.cuda.synchronize()
+    return t
+
+
+def run_single(args):
+    ctx = dsort.Context(0)
+    n = args.keys
+    w = 4 if args.dtype == "i32" else 8
+    t_in = make_input(ctx, n, 0, args.dtype, args.dist)
+    out = torch.empty_like(t_in)
+    fp_in = ctx.fingerprint(t_in)
+    for _ in range(args.warmup):
+        ctx.sort_dev(t_in, out)
+    torch.cuda.synchronize()
+    if args.warmup == 0:  # still verify once, outside the timed region
+        ctx.sort_dev(t_in, out)
+        torch.cuda.synchronize()
+    ok = ctx.descents(out) == 0 and ctx.fingerprint(out) == fp_in
+    if not ok:
+        raise SystemExit("bench: sorted output failed verification")
+    torch.cuda.synchronize()
+    kms, klaunch, bms, tot = 0.0, 0, 0.0, 0.0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.sort_dev(t_in, out)
+        st = ctx.stats()  # reads the HIP events of this step (syncs the stream)
+        kms += st["merge_kernel_ms"]
+        klaunch += st["merge_kernel_launches"]
+        bms += st["block_sort_ms"]
+        tot += st["total_ms"]
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    stats = ctx.stats()
+    ctx.close()
+    return elapsed, {"kernel_ms": kms, "launches": klaunch, "block_ms": bms, "device_ms": tot,
+                     "passes": stats["merge_passes"], "tile": stats["tile_keys"], "w": w, "n_gpu": n}
+
+
+def run_multi(args):
+    import torch.distributed as dist
+    rank = int(os.environ["RANK"])
+    world = int(os.environ["WORLD_SIZE"])
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    torch.cuda.set_device(local)
+    dist.init_process_group("gloo")
+    ctx = dsort.Context(local)
+    uid = [dsort.Context.unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(uid, src=0)
+    ctx.comm_init(world, rank, uid[0])
+    n = args.keys
+    sz = n // world + (1 if rank < n % world else 0)
+    first = rank * (n // world) + min(rank, n % world)
+    t_in = make_input(ctx, sz, first, args.dtype, args.dist)
+    w = 4 if args.dtype == "i32" else 8
+    for _ in range(max(args.warmup, 1)):
+        ptr, nout = ctx.sample_sort_dev(t_in)
+    torch.cuda.synchronize()
+    # verification outside the timed region: local order, global multiset, rank boundaries
+    out_view = torch.empty(max(nout, 1), dtype=t_in.dtype, device="cuda")
+    ctx.lib.dsort_copy_d2h  # noqa: B018  (binding loaded)
+    import ctypes as _c
+    _c.memmove  # noqa: B018
+    desc = ctx.lib.dsort_count_descents_i32 if args.dtype == "i32" else ctx.lib.dsort_count_descents_i64
+    c = dsort.U64()
+    ctx.check(desc(ctx.h, ptr, nout, _c.byref(c)))
+    fs, fx = dsort.U64(), dsort.U64()
+    fpf = ctx.lib.dsort_fingerprint_i32 if args.dtype == "i32" else ctx.lib.dsort_fingerprint_i64
+    ctx.check(fpf(ctx.h, ptr, nout, _c.byref(fs), _c.byref(fx)))
+    in_fp = ctx.fingerprint(t_in)
+    ends = np.zeros(2, np.int64)
+    if nout:
+        hb = np.zeros(1, np.int64 if args.dtype == "i64" else np.int32)
+        ctx.copy_d2h(hb, ptr, hb.itemsize)
+        ends[0] = hb[0]
+        ctx.copy_d2h(hb, ptr + (nout - 1) * hb.itemsize, hb.itemsize)
+        ends[1] = hb[0]
+    info = torch.tensor([c.value, fs.value & 0x7FFFFFFFFFFFFFFF, nout, in_fp[0] & 0x7FFFFFFFFFFFFFFF,
+                         ends[0], ends[1]], dtype=torch.int64)
+    allinfo = [torch.zeros_like(info) for _ in range(world)]
+    dist.all_gather(allinfo, info)
+    del out_view
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    ex, fm = 0.0, 0.0
+    for _ in range(args.steps):
+        ptr, nout = ctx.sample_sort_dev(t_in)
+        st = ctx.stats()
+        ex += st["exchange_ms"]
+        fm += st["final_merge_ms"]
+    torch.cuda.synchronize()
+    dist.barrier()
+    t1 = time.perf_counter()
+    el = torch.tensor([t1 - t0], dtype=torch.float64)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    A = torch.stack(allinfo)
+    ok = bool((A[:, 0] == 0).all())
+    ok &= int(A[:, 2].sum()) == n
+    ok &= (int(A[:, 1].sum()) & 0x7FFFFFFFFFFFFFFF) == (int(A[:, 3].sum()) & 0x7FFFFFFFFFFFFFFF)
+    for r in range(world - 1):
+        if A[r, 2] > 0 and A[r + 1, 2] > 0:
+            ok &= bool(A[r, 5] <= A[r + 1, 4])
+    ctx.comm_destroy()
+    ctx.close()
+    return rank, world, float(el.item()), ok, {"exchange_ms": ex, "final_merge_ms": fm, "w": w,
+                                                "n_gpu": sz}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world and world != 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    metric = "sorted keys/sec (int32, 2^30 keys)" if args.dtype == "i32" else "sorted keys/sec (int64)"
+    result = {"metric": metric, "unit": "keys/s", "n_gpus": args.gpus, "steps": args.steps,
+              "warmup": args.warmup, "higher_is_better": True, "scaling": "strong",
+              "vs_baseline": None, "dtype": "int32" if args.dtype == "i32" else "int64",
+              "data": f"synthetic {args.dist} keys, splitmix64(seed={SEED:#x} + global index)"}
+    if world == 1 and args.gpus == 1:
+        elapsed, k = run_single(args)
+        n = args.keys
+        step_ms = 1000.0 * elapsed / args.steps
+        result.update({"value": n * args.steps / elapsed, "ms_per_step": step_ms})
+        avg_launch_ms = k["kernel_ms"] / max(k["launches"], 1)
+        bytes_per_launch = 2 * k["w"] * n
+        achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if k["launches"] else 0.0
+        result["config"] = {"workload": f"C2-style single-GPU sort of {n} {args.dist} {result['dtype']} keys "
+                                        f"(BASELINE metric size); tile {k['tile']} keys, {k['passes']} merge passes",
+                            "keys": n, "parallelism": "1 GPU"}
+        result["roofline"] = {
+            "bound": "hbm", "kernel": "merge2_kernel (merge-path pass)", "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None, "avg_launch_ms": round(avg_launch_ms, 4),
+            "algorithmic_bytes_per_launch": bytes_per_launch,
+            "block_sort_ms": round(k["block_ms"] / args.steps, 3),
+            "whole_sort_single_pass_bound_frac": round(2 * k["w"] * n / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        }
+        if not args.no_cpu_baseline and args.dtype == "i32":
+            result["cpu_baseline"] = cpu_baseline(args.cpu_sample_keys)
+        print(json.dumps(result), flush=True)
+    else:
+        rank, world, elapsed, ok, k = run_multi(args)
+        if rank == 0:
+            if not ok:
+                raise SystemExit("bench: distributed output failed verification")
+            n = args.keys
+            step_ms = 1000.0 * elapsed / args.steps
+            result.update({"value": n * args.steps / elapsed, "ms_per_step": step_ms})
+            result["config"] = {"workload": f"sample sort of {n} {args.dist} {result['dtype']} keys over {world} GPUs "
+                                            "(equal chunks, RCCL all-to-all)", "keys": n,
+                                "parallelism": f"sample-sort x{world}"}
+            result["roofline"] = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
+                                  "frac": None, "traffic": None,
+                                  "rank0_exchange_ms": round(k["exchange_ms"] / args.steps, 3),
+                                  "rank0_final_merge_ms": round(k["final_merge_ms"] / args.steps, 3),
+                                  "whole_sort_single_pass_bound_frac": round(
+                                      2 * k["w"] * n / (step_ms * 1e-3) / 1e9 / (HBM_PEAK_GBS * world), 4)}
+            print(json.dumps(result), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,760 @@
+// dsort_api.hip -- the C ABI of libdsort (include/dsort.h): contexts, host-buffer entry points,
+// device utilities (generators, parity checks), sample-sort planning and the multi-GPU sample
+// sort over RCCL.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cmath>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "dsort_internal.h"
+
+#define DSORT_VERSION_STRING "libdsort 0.1 (gfx950, HIP " DSORT_STR(HIP_VERSION_MAJOR) "." DSORT_STR(HIP_VERSION_MINOR) ")"
+#define DSORT_STR2(x) #x
+#define DSORT_STR(x) DSORT_STR2(x)
+
+namespace dsort {
+
+int set_err(dsort_ctx *ctx, int code, const std::string &msg) {
+    if (ctx) ctx->err = msg;
+    return code;
+}
+
+int hip_err(dsort_ctx *ctx, hipError_t e, const char *what) {
+    std::string m = std::string(what) + ": " + hipGetErrorString(e);
+    int code = (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) ? DSORT_ENOMEM : DSORT_EHIP;
+    return set_err(ctx, code, m);
+}
+
+int ensure(dsort_ctx *ctx, void **buf, size_t *have, size_t need, const char *what) {
+    if (need <= *have && *buf) return DSORT_OK;
+    if (*buf) {
+        // the old arena may still be used by queued work on any stream of this device
+        hipError_t e = hipDeviceSynchronize();
+        if (e != hipSuccess) return hip_err(ctx, e, "hipDeviceSynchronize (arena grow)");
+        hipFree(*buf);
+        *buf = nullptr;
+        *have = 0;
+    }
+    size_t sz = need < 256 ? 256 : need;
+    hipError_t e = hipMalloc(buf, sz);
+    if (e != hipSuccess) {
+        *buf = nullptr;
+        return set_err(ctx, DSORT_ENOMEM, std::string("hipMalloc failed for ") + what + " (" +
+                                              std::to_string(sz) + " bytes): " + hipGetErrorString(e));
+    }
+    *have = sz;
+    return DSORT_OK;
+}
+
+static hipStream_t pick(dsort_ctx *ctx, void *stream) {
+    if (stream == DSORT_NULL_STREAM) return static_cast<hipStream_t>(nullptr);
+    return stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+}
+
+// ------------------------------------------------------------------ utility kernels ------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+__global__ void gen_uniform_i32_kernel(int32_t *out, uint64_t n, uint64_t seed) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        out[i] = (int32_t)(uint32_t)(splitmix64(seed + i) >> 32);
+}
+
+__global__ void gen_uniform_i64_kernel(int64_t *out, uint64_t n, uint64_t seed) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        out[i] = (int64_t)splitmix64(seed + i);
+}
+
+// Truncated continuous power law over ranks [1, 2^24], exponent s = 1.2:
+// rank = floor((1 + u*((2^24+1)^(1-s) - 1))^(1/(1-s))).  Heavy head (rank 1 ~ 13% of keys).
+__global__ void gen_zipf_i64_kernel(int64_t *out, uint64_t n, uint64_t seed) {
+    const double s = 1.2, nr = 16777216.0;
+    const double e = 1.0 - s;
+    const double top = pow(nr + 1.0, e) - 1.0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const double u = (double)(splitmix64(seed + i) >> 11) * 0x1.0p-53;
+        double r = floor(pow(1.0 + u * top, 1.0 / e));
+        if (r < 1.0) r = 1.0;
+        if (r > nr) r = nr;
+        out[i] = (int64_t)((uint64_t)r * 0x9E3779B97F4A7C15ull);
+    }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) fingerprint_kernel(const T *keys, uint64_t n,
+                                                          unsigned long long *acc) {
+    uint64_t s = 0, x = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t k = sizeof(T) == 4 ? (uint64_t)(uint32_t)keys[i] : (uint64_t)keys[i];
+        s += splitmix64(k);
+        x ^= splitmix64(k ^ 0xD1B54A32D192ED03ull);
+    }
+    __shared__ uint64_t ss[256], sx[256];
+    ss[threadIdx.x] = s;
+    sx[threadIdx.x] = x;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+            ss[threadIdx.x] += ss[threadIdx.x + w];
+            sx[threadIdx.x] ^= sx[threadIdx.x + w];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        atomicAdd(&acc[0], (unsigned long long)ss[0]);
+        atomicXor(&acc[1], (unsigned long long)sx[0]);
+    }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) descents_kernel(const T *keys, uint64_t n,
+                                                       unsigned long long *acc) {
+    unsigned long long c = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x + 1; i < n; i += stride)
+        c += keys[i - 1] > keys[i] ? 1 : 0;
+    __shared__ unsigned long long sc[256];
+    sc[threadIdx.x] = c;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) sc[threadIdx.x] += sc[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) atomicAdd(&acc[2], sc[0]);
+}
+
+// Regular samples of a sorted local run: sample j = keys[(j+1)*n/(s+1)].
+template <typename T>
+__global__ void sample_kernel(const T *keys, uint64_t n, int s, T *out) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= s) return;
+    if (n == 0) {
+        out[j] = sizeof(T) == 4 ? (T)INT32_MAX : (T)INT64_MAX;
+        return;
+    }
+    uint64_t idx = (uint64_t)(j + 1) * n / (uint64_t)(s + 1);
+    if (idx >= n) idx = n - 1;
+    out[j] = keys[idx];
+}
+
+// Composite-splitter cut positions in a sorted local run (same rule as dsort_plan_cuts_*):
+// keys of this rank below splitter (v, r, i) in (value, rank, index) order.
+template <typename T>
+__global__ void cuts_kernel(const T *keys, uint64_t n, int my_rank, int nsplit, const T *sv,
+                            const int32_t *sr, const uint64_t *si, uint64_t *cuts) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j > nsplit) return;
+    if (j == 0) {
+        cuts[0] = 0;
+        cuts[nsplit + 1] = n;
+    }
+    if (j == nsplit) return;
+    const T v = sv[j];
+    const int r = sr[j];
+    uint64_t pos;
+    if (r == my_rank) {
+        pos = si[j] < n ? si[j] : n;
+    } else {
+        const bool upper = my_rank < r;  // equal keys of lower ranks go left
+        uint64_t lo = 0, hi = n;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            const bool left = upper ? (keys[mid] <= v) : (keys[mid] < v);
+            if (left) lo = mid + 1;
+            else hi = mid;
+        }
+        pos = lo;
+    }
+    cuts[j + 1] = pos;
+}
+
+static unsigned grid_for(uint64_t n, int per_block) {
+    uint64_t g = (n + per_block - 1) / per_block;
+    if (g > 4096) g = 4096;
+    if (g == 0) g = 1;
+    return (unsigned)g;
+}
+
+template <typename T>
+static int fingerprint_t(dsort_ctx *ctx, const T *d, size_t n, uint64_t *sum, uint64_t *xr,
+                         uint64_t *desc, bool want_desc) {
+    if (!ctx) return DSORT_EINVAL;
+    hipStream_t s = ctx->stream;
+    DSORT_HIP(ctx, hipMemsetAsync(ctx->red, 0, 64, s));
+    if (n) {
+        if (!want_desc)
+            hipLaunchKernelGGL((fingerprint_kernel<T>), dim3(grid_for(n, 256 * 8)), dim3(256), 0, s,
+                               d, (uint64_t)n, static_cast<unsigned long long *>(ctx->red));
+        else
+            hipLaunchKernelGGL((descents_kernel<T>), dim3(grid_for(n, 256 * 8)), dim3(256), 0, s, d,
+                               (uint64_t)n, static_cast<unsigned long long *>(ctx->red));
+        DSORT_HIP(ctx, hipGetLastError());
+    }
+    DSORT_HIP(ctx, hipMemcpyAsync(ctx->red_host, ctx->red, 64, hipMemcpyDeviceToHost, s));
+    DSORT_HIP(ctx, hipStreamSynchronize(s));
+    if (sum) *sum = ctx->red_host[0];
+    if (xr) *xr = ctx->red_host[1];
+    if (desc) *desc = ctx->red_host[2];
+    return DSORT_OK;
+}
+
+// ------------------------------------------------------------------ host entry points ---
+template <typename T>
+static int sort_host(dsort_ctx *ctx, T *host, size_t n) {
+    if (!ctx || (!host && n)) return set_err(ctx, DSORT_EINVAL, "null argument");
+    if (n < 2) return DSORT_OK;
+    int rc = ensure(ctx, &ctx->io, &ctx->io_bytes, n * sizeof(T), "staging");
+    if (rc) return rc;
+    hipStream_t s = ctx->stream;
+    T *d = static_cast<T *>(ctx->io);
+    DSORT_HIP(ctx, hipMemcpyAsync(d, host, n * sizeof(T), hipMemcpyHostToDevice, s));
+    rc = sort_device<T>(ctx, d, d, n, s, true);
+    if (rc) return rc;
+    DSORT_HIP(ctx, hipMemcpyAsync(host, d, n * sizeof(T), hipMemcpyDeviceToHost, s));
+    DSORT_HIP(ctx, hipStreamSynchronize(s));
+    return DSORT_OK;
+}
+
+template <typename T>
+static int merge_host(dsort_ctx *ctx, const T *const runs[], const size_t lens[], int k, T *out) {
+    if (!ctx || k < 0 || (k > 0 && (!runs || !lens))) return set_err(ctx, DSORT_EINVAL, "bad argument");
+    size_t n = 0;
+    for (int j = 0; j < k; ++j) {
+        if (lens[j] && !runs[j]) return set_err(ctx, DSORT_EINVAL, "null run");
+        n += lens[j];
+    }
+    if (n == 0) return DSORT_OK;
+    if (!out) return set_err(ctx, DSORT_EINVAL, "null output");
+    int rc = ensure(ctx, &ctx->io, &ctx->io_bytes, n * sizeof(T), "staging");
+    if (rc) return rc;
+    rc = ensure(ctx, &ctx->io2, &ctx->io2_bytes, n * sizeof(T), "staging 2");
+    if (rc) return rc;
+    hipStream_t s = ctx->stream;
+    T *din = static_cast<T *>(ctx->io), *dout = static_cast<T *>(ctx->io2);
+    size_t off = 0;
+    for (int j = 0; j < k; ++j) {
+        if (lens[j])
+            DSORT_HIP(ctx, hipMemcpyAsync(din + off, runs[j], lens[j] * sizeof(T),
+                                          hipMemcpyHostToDevice, s));
+        off += lens[j];
+    }
+    rc = merge_device<T>(ctx, din, lens, k, dout, s);
+    if (rc) return rc;
+    DSORT_HIP(ctx, hipMemcpyAsync(out, dout, n * sizeof(T), hipMemcpyDeviceToHost, s));
+    DSORT_HIP(ctx, hipStreamSynchronize(s));
+    return DSORT_OK;
+}
+
+// ------------------------------------------------------------------ planning (host) -----
+template <typename T>
+static int plan_splitters(int nranks, int s, const T *samples, const uint64_t *idx, T *sv,
+                          int32_t *sr, uint64_t *si) {
+    if (nranks < 1 || s < 1 || !samples || !idx) return DSORT_EINVAL;
+    if (nranks == 1) return DSORT_OK;
+    if (!sv || !sr || !si) return DSORT_EINVAL;
+    struct S {
+        T v;
+        int32_t r;
+        uint64_t i;
+    };
+    std::vector<S> all((size_t)nranks * s);
+    for (int r = 0; r < nranks; ++r)
+        for (int j = 0; j < s; ++j) all[(size_t)r * s + j] = S{samples[(size_t)r * s + j], r, idx[(size_t)r * s + j]};
+    std::sort(all.begin(), all.end(), [](const S &a, const S &b) {
+        if (a.v != b.v) return a.v < b.v;
+        if (a.r != b.r) return a.r < b.r;
+        return a.i < b.i;
+    });
+    // splitter q sits at the q-th P-quantile of the merged sample (PSRS with oversampling s)
+    const size_t m = all.size();
+    for (int q = 1; q < nranks; ++q) {
+        size_t pos = (size_t)q * m / (size_t)nranks;
+        if (pos >= m) pos = m - 1;
+        sv[q - 1] = all[pos].v;
+        sr[q - 1] = all[pos].r;
+        si[q - 1] = all[pos].i;
+    }
+    return DSORT_OK;
+}
+
+template <typename T>
+static int plan_cuts(const T *sorted, size_t n, int my_rank, int nranks, const T *sv,
+                     const int32_t *sr, const uint64_t *si, uint64_t *cuts) {
+    if (nranks < 1 || !cuts || (n && !sorted)) return DSORT_EINVAL;
+    cuts[0] = 0;
+    cuts[nranks] = n;
+    for (int q = 0; q + 1 < nranks; ++q) {
+        uint64_t pos;
+        if (sr[q] == my_rank) {
+            pos = si[q] < n ? si[q] : n;
+        } else {
+            const bool upper = my_rank < sr[q];
+            const T *p = upper ? std::upper_bound(sorted, sorted + n, sv[q])
+                               : std::lower_bound(sorted, sorted + n, sv[q]);
+            pos = (uint64_t)(p - sorted);
+        }
+        cuts[q + 1] = pos;
+    }
+    return DSORT_OK;
+}
+
+// ------------------------------------------------------------------ sample sort ---------
+static const int kSamplesPerRank = 512;
+
+template <typename T> static ncclDataType_t nccl_type();
+template <> ncclDataType_t nccl_type<int32_t>() { return ncclInt32; }
+template <> ncclDataType_t nccl_type<int64_t>() { return ncclInt64; }
+
+#define DSORT_NCCL(ctx, call)                                                             \
+    do {                                                                                  \
+        ncclResult_t r_ = (call);                                                         \
+        if (r_ != ncclSuccess)                                                            \
+            return dsort::set_err((ctx), DSORT_ECOMM,                                     \
+                                  std::string(#call) + ": " + ncclGetErrorString(r_));    \
+    } while (0)
+
+template <typename T>
+static int sample_sort(dsort_ctx *ctx, const T *d_in, size_t n_local, T **d_out, size_t *n_out,
+                       void *stream) {
+    if (!ctx || !d_out || !n_out || (n_local && !d_in)) return set_err(ctx, DSORT_EINVAL, "null argument");
+    if (!ctx->comm) return set_err(ctx, DSORT_ECOMM, "communicator not initialised (dsort_comm_init)");
+    hipStream_t s = pick(ctx, stream);
+    const int P = ctx->nranks, me = ctx->rank, S = kSamplesPerRank;
+    // 1. local sort (the worker's merge_sort) into the context's local arena
+    int rc = ensure(ctx, &ctx->local, &ctx->local_bytes, (n_local ? n_local : 1) * sizeof(T), "local run");
+    if (rc) return rc;
+    T *d_keys = static_cast<T *>(ctx->local);
+    rc = sort_device<T>(ctx, d_in, d_keys, n_local, s, true);
+    if (rc) return rc;
+    dsort_stats st = ctx->stats;
+    // device small-area layout
+    const size_t off_samp = 0;                                   // S keys
+    const size_t off_all = off_samp + (size_t)S * sizeof(T);      // P*S keys
+    const size_t off_n = off_all + (size_t)P * S * sizeof(T);     // P uint64 (n_local of all)
+    const size_t off_sv = off_n + (size_t)P * 8;                  // P keys (splitter values)
+    const size_t off_sr = off_sv + (size_t)P * sizeof(T);         // P int32
+    const size_t off_si = off_sr + (size_t)P * 8;                 // P uint64
+    const size_t off_cut = off_si + (size_t)P * 8;                // P+1 uint64
+    const size_t off_cnt = off_cut + (size_t)(P + 1) * 8;         // P uint64 (send counts)
+    const size_t off_mat = off_cnt + (size_t)P * 8;               // P*P uint64
+    const size_t total_small = off_mat + (size_t)P * P * 8 + 64;
+    rc = ensure(ctx, &ctx->small, &ctx->small_bytes, total_small, "sample-sort small buffers");
+    if (rc) return rc;
+    if (ctx->small_host_bytes < total_small) {
+        if (ctx->small_host) hipHostFree(ctx->small_host);
+        ctx->small_host = nullptr;
+        ctx->small_host_bytes = 0;
+        DSORT_HIP(ctx, hipHostMalloc(&ctx->small_host, total_small, hipHostMallocDefault));
+        ctx->small_host_bytes = total_small;
+    }
+    char *dsm = static_cast<char *>(ctx->small);
+    char *hsm = static_cast<char *>(ctx->small_host);
+    // 2. regular samples + local size
+    hipLaunchKernelGGL((sample_kernel<T>), dim3((S + 255) / 256), dim3(256), 0, s, d_keys,
+                       (uint64_t)n_local, S, reinterpret_cast<T *>(dsm + off_samp));
+    DSORT_HIP(ctx, hipGetLastError());
+    uint64_t nl = n_local;
+    DSORT_HIP(ctx, hipMemcpyAsync(dsm + off_cnt, &nl, 8, hipMemcpyHostToDevice, s));
+    // 3. all-gather samples and sizes
+    DSORT_NCCL(ctx, ncclGroupStart());
+    DSORT_NCCL(ctx, ncclAllGather(dsm + off_samp, dsm + off_all, (size_t)S, nccl_type<T>(), ctx->comm, s));
+    DSORT_NCCL(ctx, ncclAllGather(dsm + off_cnt, dsm + off_n, 1, ncclUint64, ctx->comm, s));
+    DSORT_NCCL(ctx, ncclGroupEnd());
+    DSORT_HIP(ctx, hipMemcpyAsync(hsm + off_all, dsm + off_all, (size_t)P * S * sizeof(T) + (size_t)P * 8,
+                                  hipMemcpyDeviceToHost, s));
+    DSORT_HIP(ctx, hipStreamSynchronize(s));
+    // 4. splitters on the host (tiny: P*S composites)
+    {
+        const T *hs = reinterpret_cast<const T *>(hsm + off_all);
+        const uint64_t *hn = reinterpret_cast<const uint64_t *>(hsm + off_n);
+        std::vector<uint64_t> idx((size_t)P * S);
+        for (int r = 0; r < P; ++r) dsort_plan_sample_positions(hn[r], S, &idx[(size_t)r * S]);
+        T *sv = reinterpret_cast<T *>(hsm + off_sv);
+        int32_t *sr = reinterpret_cast<int32_t *>(hsm + off_sr);
+        uint64_t *si = reinterpret_cast<uint64_t *>(hsm + off_si);
+        rc = plan_splitters<T>(P, S, hs, idx.data(), sv, sr, si);
+        if (rc) return set_err(ctx, rc, "splitter planning failed");
+        DSORT_HIP(ctx, hipMemcpyAsync(dsm + off_sv, hsm + off_sv, off_cut - off_sv, hipMemcpyHostToDevice, s));
+    }
+    // 5. cuts and send counts
+    hipLaunchKernelGGL((cuts_kernel<T>), dim3(1), dim3(((P + 63) / 64) * 64), 0, s, d_keys,
+                       (uint64_t)n_local, me, P - 1, reinterpret_cast<const T *>(dsm + off_sv),
+                       reinterpret_cast<const int32_t *>(dsm + off_sr),
+                       reinterpret_cast<const uint64_t *>(dsm + off_si),
+                       reinterpret_cast<uint64_t *>(dsm + off_cut));
+    DSORT_HIP(ctx, hipGetLastError());
+    DSORT_HIP(ctx, hipMemcpyAsync(hsm + off_cut, dsm + off_cut, (size_t)(P + 1) * 8, hipMemcpyDeviceToHost, s));
+    DSORT_HIP(ctx, hipStreamSynchronize(s));
+    const uint64_t *hcut = reinterpret_cast<const uint64_t *>(hsm + off_cut);
+    uint64_t *hcnt = reinterpret_cast<uint64_t *>(hsm + off_cnt);
+    for (int r = 0; r < P; ++r) hcnt[r] = hcut[r + 1] - hcut[r];
+    DSORT_HIP(ctx, hipMemcpyAsync(dsm + off_cnt, hcnt, (size_t)P * 8, hipMemcpyHostToDevice, s));
+    // 6. count matrix
+    DSORT_NCCL(ctx, ncclAllGather(dsm + off_cnt, dsm + off_mat, (size_t)P, ncclUint64, ctx->comm, s));
+    DSORT_HIP(ctx, hipMemcpyAsync(hsm + off_mat, dsm + off_mat, (size_t)P * P * 8, hipMemcpyDeviceToHost, s));
+    DSORT_HIP(ctx, hipStreamSynchronize(s));
+    const uint64_t *mat = reinterpret_cast<const uint64_t *>(hsm + off_mat);  // mat[src*P + dst]
+    std::vector<size_t> rlen(P);
+    std::vector<uint64_t> roff(P + 1, 0);
+    for (int r = 0; r < P; ++r) {
+        rlen[r] = mat[(size_t)r * P + me];
+        roff[r + 1] = roff[r] + rlen[r];
+    }
+    const uint64_t nrecv = roff[P];
+    rc = ensure(ctx, &ctx->recv, &ctx->recv_bytes, (nrecv ? nrecv : 1) * sizeof(T), "receive buffer");
+    if (rc) return rc;
+    rc = ensure(ctx, &ctx->recv2, &ctx->recv2_bytes, (nrecv ? nrecv : 1) * sizeof(T), "merge output");
+    if (rc) return rc;
+    T *rb = static_cast<T *>(ctx->recv);
+    // 7. key exchange: one send and one receive per peer link, grouped (RCCL all-to-all-v)
+    DSORT_NCCL(ctx, ncclGroupStart());
+    for (int r = 0; r < P; ++r) {
+        if (r == me) continue;
+        if (hcnt[r]) DSORT_NCCL(ctx, ncclSend(d_keys + hcut[r], hcnt[r], nccl_type<T>(), r, ctx->comm, s));
+        if (rlen[r]) DSORT_NCCL(ctx, ncclRecv(rb + roff[r], rlen[r], nccl_type<T>(), r, ctx->comm, s));
+    }
+    DSORT_NCCL(ctx, ncclGroupEnd());
+    if (hcnt[me])
+        DSORT_HIP(ctx, hipMemcpyAsync(rb + roff[me], d_keys + hcut[me], hcnt[me] * sizeof(T),
+                                      hipMemcpyDeviceToDevice, s));
+    if (ctx->ev_ok) {
+        DSORT_HIP(ctx, hipEventRecord(ctx->ev[3], s));
+        ctx->ev_mask |= 8u;
+    }
+    // 8. merge the P received runs (source-rank order keeps the merge deterministic)
+    T *outp = static_cast<T *>(ctx->recv2);
+    rc = merge_device<T>(ctx, rb, rlen.data(), P, outp, s);
+    if (rc) return rc;
+    if (ctx->ev_ok) {
+        DSORT_HIP(ctx, hipEventRecord(ctx->ev[4], s));
+        ctx->ev_mask |= 16u;
+    }
+    ctx->last_stream = s;
+    st.keys_out = nrecv;
+    ctx->stats = st;
+    ctx->stats.merge_passes = st.merge_passes;
+    *d_out = outp;
+    *n_out = nrecv;
+    return DSORT_OK;
+}
+
+}  // namespace dsort
+
+using namespace dsort;
+
+// ======================================================================== C ABI =========
+extern "C" {
+
+const char *dsort_version(void) { return DSORT_VERSION_STRING; }
+
+int dsort_init(dsort_ctx **out, int device) {
+    if (!out) return DSORT_EINVAL;
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return DSORT_ENODEV;
+    if (device < 0 || device >= count) return DSORT_ENODEV;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return DSORT_ENODEV;
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return DSORT_ENODEV;
+    dsort_ctx *ctx = new (std::nothrow) dsort_ctx();
+    if (!ctx) return DSORT_ENOMEM;
+    ctx->device = device;
+    if (hipSetDevice(device) != hipSuccess ||
+        hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return DSORT_EHIP;
+    }
+    if (hipMalloc(&ctx->red, 64) != hipSuccess ||
+        hipHostMalloc((void **)&ctx->red_host, 64, hipHostMallocDefault) != hipSuccess) {
+        dsort_finalize(ctx);
+        return DSORT_ENOMEM;
+    }
+    ctx->ev_ok = true;
+    for (auto &e : ctx->ev)
+        if (hipEventCreate(&e) != hipSuccess) ctx->ev_ok = false;
+    for (auto &e : ctx->kev)
+        if (hipEventCreate(&e) != hipSuccess) ctx->ev_ok = false;
+    *out = ctx;
+    return DSORT_OK;
+}
+
+int dsort_finalize(dsort_ctx *ctx) {
+    if (!ctx) return DSORT_EINVAL;
+    hipSetDevice(ctx->device);
+    if (ctx->stream) hipStreamSynchronize(ctx->stream);
+    if (ctx->comm) {
+        ncclCommDestroy(ctx->comm);
+        ctx->comm = nullptr;
+    }
+    void *bufs[] = {ctx->scratch, ctx->buckets, ctx->pairs, ctx->io, ctx->io2, ctx->red,
+                    ctx->local, ctx->recv, ctx->recv2, ctx->small};
+    for (void *b : bufs)
+        if (b) hipFree(b);
+    if (ctx->red_host) hipHostFree(ctx->red_host);
+    if (ctx->small_host) hipHostFree(ctx->small_host);
+    for (auto &e : ctx->ev)
+        if (e) (void)hipEventDestroy(e);
+    for (auto &e : ctx->kev)
+        if (e) (void)hipEventDestroy(e);
+    if (ctx->stream) hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return DSORT_OK;
+}
+
+const char *dsort_last_error(const dsort_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int dsort_get_stats(const dsort_ctx *cctx, dsort_stats *out) {
+    if (!cctx || !out) return DSORT_EINVAL;
+    dsort_ctx *ctx = const_cast<dsort_ctx *>(cctx);
+    *out = ctx->stats;
+    if (!ctx->ev_ok) return DSORT_OK;
+    if (hipStreamSynchronize(ctx->last_stream) != hipSuccess) return DSORT_EHIP;
+    float ms = 0;
+    auto el = [&](int a, int b) -> double {
+        if (!(ctx->ev_mask & (1u << a)) || !(ctx->ev_mask & (1u << b))) return 0.0;
+        return hipEventElapsedTime(&ms, ctx->ev[a], ctx->ev[b]) == hipSuccess ? (double)ms : 0.0;
+    };
+    out->merge_kernel_ms = 0;
+    out->merge_kernel_launches = 0;
+    for (int i = 0; i + 1 < ctx->kev_used; i += 2) {
+        if (hipEventQuery(ctx->kev[i + 1]) != hipSuccess) break;
+        if (hipEventElapsedTime(&ms, ctx->kev[i], ctx->kev[i + 1]) == hipSuccess) {
+            out->merge_kernel_ms += ms;
+            out->merge_kernel_launches += 1;
+        }
+    }
+    out->block_sort_ms = el(0, 1);
+    out->merge_ms = el(1, 2);
+    if (ctx->ev_mask & 16u) {
+        out->exchange_ms = el(2, 3);
+        out->final_merge_ms = el(3, 4);
+        out->total_ms = el(0, 4);
+    } else {
+        out->total_ms = el(0, 2);
+    }
+    return DSORT_OK;
+}
+
+int dsort_synchronize(dsort_ctx *ctx) {
+    if (!ctx) return DSORT_EINVAL;
+    DSORT_HIP(ctx, hipStreamSynchronize(ctx->last_stream));
+    DSORT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return DSORT_OK;
+}
+
+int dsort_sort_i32(dsort_ctx *ctx, int32_t *keys, size_t n) { return sort_host<int32_t>(ctx, keys, n); }
+int dsort_sort_i64(dsort_ctx *ctx, int64_t *keys, size_t n) { return sort_host<int64_t>(ctx, keys, n); }
+
+int dsort_sort_dev_i32(dsort_ctx *ctx, int32_t *d, size_t n, void *stream) {
+    if (!ctx || (n && !d)) return set_err(ctx, DSORT_EINVAL, "null argument");
+    return sort_device<int32_t>(ctx, d, d, n, pick(ctx, stream), true);
+}
+int dsort_sort_dev_i64(dsort_ctx *ctx, int64_t *d, size_t n, void *stream) {
+    if (!ctx || (n && !d)) return set_err(ctx, DSORT_EINVAL, "null argument");
+    return sort_device<int64_t>(ctx, d, d, n, pick(ctx, stream), true);
+}
+int dsort_sort_dev_copy_i32(dsort_ctx *ctx, const int32_t *in, int32_t *out, size_t n, void *stream) {
+    if (!ctx || (n && (!in || !out))) return set_err(ctx, DSORT_EINVAL, "null argument");
+    return sort_device<int32_t>(ctx, in, out, n, pick(ctx, stream), true);
+}
+int dsort_sort_dev_copy_i64(dsort_ctx *ctx, const int64_t *in, int64_t *out, size_t n, void *stream) {
+    if (!ctx || (n && (!in || !out))) return set_err(ctx, DSORT_EINVAL, "null argument");
+    return sort_device<int64_t>(ctx, in, out, n, pick(ctx, stream), true);
+}
+
+int dsort_merge_i32(dsort_ctx *ctx, const int32_t *const runs[], const size_t lens[], int k, int32_t *out) {
+    return merge_host<int32_t>(ctx, runs, lens, k, out);
+}
+int dsort_merge_i64(dsort_ctx *ctx, const int64_t *const runs[], const size_t lens[], int k, int64_t *out) {
+    return merge_host<int64_t>(ctx, runs, lens, k, out);
+}
+int dsort_merge_dev_i32(dsort_ctx *ctx, const int32_t *d_in, const size_t lens[], int k, int32_t *d_out,
+                        void *stream) {
+    if (!ctx || k < 0 || (k && !lens)) return set_err(ctx, DSORT_EINVAL, "bad argument");
+    return merge_device<int32_t>(ctx, d_in, lens, k, d_out, pick(ctx, stream));
+}
+int dsort_merge_dev_i64(dsort_ctx *ctx, const int64_t *d_in, const size_t lens[], int k, int64_t *d_out,
+                        void *stream) {
+    if (!ctx || k < 0 || (k && !lens)) return set_err(ctx, DSORT_EINVAL, "bad argument");
+    return merge_device<int64_t>(ctx, d_in, lens, k, d_out, pick(ctx, stream));
+}
+
+int dsort_comm_unique_id(char id[DSORT_UNIQUE_ID_BYTES]) {
+    static_assert(sizeof(ncclUniqueId) == DSORT_UNIQUE_ID_BYTES, "ncclUniqueId size");
+    if (!id) return DSORT_EINVAL;
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return DSORT_ECOMM;
+    memcpy(id, &u, sizeof(u));
+    return DSORT_OK;
+}
+
+int dsort_comm_init(dsort_ctx *ctx, int nranks, int rank, const char id[DSORT_UNIQUE_ID_BYTES]) {
+    if (!ctx || !id || nranks < 1 || rank < 0 || rank >= nranks) return set_err(ctx, DSORT_EINVAL, "bad argument");
+    if (ctx->comm) return set_err(ctx, DSORT_EINVAL, "communicator already initialised");
+    DSORT_HIP(ctx, hipSetDevice(ctx->device));
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof(u));
+    ncclComm_t c = nullptr;
+    DSORT_NCCL(ctx, ncclCommInitRank(&c, nranks, u, rank));
+    ctx->comm = c;
+    ctx->nranks = nranks;
+    ctx->rank = rank;
+    return DSORT_OK;
+}
+
+int dsort_comm_abort(dsort_ctx *ctx) {
+    if (!ctx) return DSORT_EINVAL;
+    if (ctx->comm) ncclCommAbort(ctx->comm);
+    ctx->comm = nullptr;
+    ctx->nranks = 1;
+    ctx->rank = 0;
+    return DSORT_OK;
+}
+
+int dsort_comm_destroy(dsort_ctx *ctx) {
+    if (!ctx) return DSORT_EINVAL;
+    if (ctx->comm) {
+        hipStreamSynchronize(ctx->stream);
+        ncclCommDestroy(ctx->comm);
+    }
+    ctx->comm = nullptr;
+    ctx->nranks = 1;
+    ctx->rank = 0;
+    return DSORT_OK;
+}
+
+int dsort_sample_sort_dev_i32(dsort_ctx *ctx, const int32_t *d, size_t n, int32_t **o, size_t *no, void *st) {
+    return sample_sort<int32_t>(ctx, d, n, o, no, st);
+}
+int dsort_sample_sort_dev_i64(dsort_ctx *ctx, const int64_t *d, size_t n, int64_t **o, size_t *no, void *st) {
+    return sample_sort<int64_t>(ctx, d, n, o, no, st);
+}
+
+int dsort_plan_sample_positions(size_t n, int s, uint64_t *idx) {
+    if (s < 1 || !idx) return DSORT_EINVAL;
+    for (int j = 0; j < s; ++j) {
+        uint64_t p = n ? (uint64_t)(j + 1) * (uint64_t)n / (uint64_t)(s + 1) : 0;
+        if (n && p >= n) p = n - 1;
+        idx[j] = p;
+    }
+    return DSORT_OK;
+}
+
+int dsort_plan_splitters_i32(int nranks, int s, const int32_t *samples, const uint64_t *idx,
+                             int32_t *sv, int32_t *sr, uint64_t *si) {
+    return plan_splitters<int32_t>(nranks, s, samples, idx, sv, sr, si);
+}
+int dsort_plan_splitters_i64(int nranks, int s, const int64_t *samples, const uint64_t *idx,
+                             int64_t *sv, int32_t *sr, uint64_t *si) {
+    return plan_splitters<int64_t>(nranks, s, samples, idx, sv, sr, si);
+}
+int dsort_plan_cuts_i32(const int32_t *sorted, size_t n, int my_rank, int nranks, const int32_t *sv,
+                        const int32_t *sr, const uint64_t *si, uint64_t *cuts) {
+    return plan_cuts<int32_t>(sorted, n, my_rank, nranks, sv, sr, si, cuts);
+}
+int dsort_plan_cuts_i64(const int64_t *sorted, size_t n, int my_rank, int nranks, const int64_t *sv,
+                        const int32_t *sr, const uint64_t *si, uint64_t *cuts) {
+    return plan_cuts<int64_t>(sorted, n, my_rank, nranks, sv, sr, si, cuts);
+}
+
+int dsort_gen_uniform_i32(dsort_ctx *ctx, int32_t *d, size_t n, uint64_t seed, uint64_t first, void *stream) {
+    if (!ctx || (n && !d)) return set_err(ctx, DSORT_EINVAL, "null argument");
+    if (!n) return DSORT_OK;
+    hipLaunchKernelGGL(gen_uniform_i32_kernel, dim3(grid_for(n, 256 * 4)), dim3(256), 0, pick(ctx, stream), d,
+                       (uint64_t)n, seed + first);
+    DSORT_HIP(ctx, hipGetLastError());
+    return DSORT_OK;
+}
+int dsort_gen_uniform_i64(dsort_ctx *ctx, int64_t *d, size_t n, uint64_t seed, uint64_t first, void *stream) {
+    if (!ctx || (n && !d)) return set_err(ctx, DSORT_EINVAL, "null argument");
+    if (!n) return DSORT_OK;
+    hipLaunchKernelGGL(gen_uniform_i64_kernel, dim3(grid_for(n, 256 * 4)), dim3(256), 0, pick(ctx, stream), d,
+                       (uint64_t)n, seed + first);
+    DSORT_HIP(ctx, hipGetLastError());
+    return DSORT_OK;
+}
+int dsort_gen_zipf_i64(dsort_ctx *ctx, int64_t *d, size_t n, uint64_t seed, uint64_t first, void *stream) {
+    if (!ctx || (n && !d)) return set_err(ctx, DSORT_EINVAL, "null argument");
+    if (!n) return DSORT_OK;
+    hipLaunchKernelGGL(gen_zipf_i64_kernel, dim3(grid_for(n, 256 * 4)), dim3(256), 0, pick(ctx, stream), d,
+                       (uint64_t)n, seed + first);
+    DSORT_HIP(ctx, hipGetLastError());
+    return DSORT_OK;
+}
+
+int dsort_fingerprint_i32(dsort_ctx *ctx, const int32_t *d, size_t n, uint64_t *sum, uint64_t *xr) {
+    return fingerprint_t<int32_t>(ctx, d, n, sum, xr, nullptr, false);
+}
+int dsort_fingerprint_i64(dsort_ctx *ctx, const int64_t *d, size_t n, uint64_t *sum, uint64_t *xr) {
+    return fingerprint_t<int64_t>(ctx, d, n, sum, xr, nullptr, false);
+}
+int dsort_count_descents_i32(dsort_ctx *ctx, const int32_t *d, size_t n, uint64_t *count) {
+    return fingerprint_t<int32_t>(ctx, d, n, nullptr, nullptr, count, true);
+}
+int dsort_count_descents_i64(dsort_ctx *ctx, const int64_t *d, size_t n, uint64_t *count) {
+    return fingerprint_t<int64_t>(ctx, d, n, nullptr, nullptr, count, true);
+}
+
+int dsort_dev_alloc(dsort_ctx *ctx, void **p, size_t bytes) {
+    if (!ctx || !p) return DSORT_EINVAL;
+    DSORT_HIP(ctx, hipMalloc(p, bytes ? bytes : 1));
+    return DSORT_OK;
+}
+int dsort_dev_free(dsort_ctx *ctx, void *p) {
+    if (!ctx) return DSORT_EINVAL;
+    if (p) DSORT_HIP(ctx, hipFree(p));
+    return DSORT_OK;
+}
+int dsort_copy_h2d(dsort_ctx *ctx, void *d, const void *h, size_t bytes) {
+    if (!ctx) return DSORT_EINVAL;
+    if (bytes) DSORT_HIP(ctx, hipMemcpy(d, h, bytes, hipMemcpyHostToDevice));
+    return DSORT_OK;
+}
+int dsort_copy_d2h(dsort_ctx *ctx, void *h, const void *d, size_t bytes) {
+    if (!ctx) return DSORT_EINVAL;
+    if (bytes) DSORT_HIP(ctx, hipMemcpy(h, d, bytes, hipMemcpyDeviceToHost));
+    return DSORT_OK;
+}
+
+int dsort_write_text_i32(const char *path, const int32_t *keys, size_t n) {
+    if (!path || (n && !keys)) return DSORT_EINVAL;
+    FILE *f = fopen(path, "w");
+    if (!f) return DSORT_EINVAL;
+    std::vector<char> buf(1 << 20);
+    size_t o = 0;
+    char tmp[16];
+    for (size_t i = 0; i < n; ++i) {
+        if (o + 13 > buf.size()) {
+            if (fwrite(buf.data(), 1, o, f) != o) { fclose(f); return DSORT_EINVAL; }
+            o = 0;
+        }
+        int64_t v = keys[i];
+        const bool neg = v < 0;
+        uint64_t u = neg ? (uint64_t)(-v) : (uint64_t)v;
+        int t = 0;
+        do { tmp[t++] = (char)('0' + u % 10); u /= 10; } while (u);
+        if (neg) buf[o++] = '-';
+        while (t) buf[o++] = tmp[--t];
+        buf[o++] = '\n';
+    }
+    if (o && fwrite(buf.data(), 1, o, f) != o) { fclose(f); return DSORT_EINVAL; }
+    return fclose(f) == 0 ? DSORT_OK : DSORT_EINVAL;
+}
+
+}  // extern "C"

@@ -1,0 +1,191 @@
+/*
+ * dsort.h -- C ABI of libdsort, the MI355X (gfx950) sort path of the distributed sort.
+ *
+ * Drop-in boundary for khimansusinha/Distributed-sorting-with-fault-tolerance
+ * (reference snapshot 2025-10-24).  The reference has two in-process calls on its hot path:
+ *
+ *   client.c:117   merge_sort(chunk, 0, num_integers - 1);            (worker, L3)
+ *   server.c:266   merge_chunks(MAX_WORKERS, received_chunks,
+ *                               chunk_sizes, total_integers);        (master, L4)
+ *
+ * dsort_sort_i32() replaces the first and dsort_merge_i32() replaces the merge half of the
+ * second (the text write of output.txt, server.c:517-519, stays in host C: dsort_write_text()).
+ * The multi-GPU entry points replace the single-master gather (server.c:414-415) by a sample
+ * sort whose key exchange is an RCCL all-to-all over xGMI.
+ *
+ * Conventions (differences from the reference are deliberate and listed in DESIGN.md):
+ *   - plain C types only: no HIP, RCCL or torch types cross this boundary; streams are passed
+ *     as `void *` holding a hipStream_t (NULL = the context's own stream,
+ *     DSORT_NULL_STREAM = HIP's legacy default stream, i.e. hipStream_t 0);
+ *   - all sizes are size_t (the reference uses int, client.c:166, server.c:481);
+ *   - every call returns 0 on success or a negative DSORT_E* code; dsort_last_error(ctx)
+ *     gives the message.  Nothing inside the library calls exit() (server.c:485-498 does);
+ *   - keys are signed, compared as signed integers, sorted ascending; the full range is valid
+ *     (the reference cannot take -1 or INT_MAX);
+ *   - one context per thread; one context drives one GPU.
+ */
+#ifndef DSORT_H
+#define DSORT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DSORT_ABI_VERSION 1
+
+#define DSORT_OK 0
+#define DSORT_EINVAL (-1)   /* bad argument */
+#define DSORT_ENOMEM (-2)   /* device or host allocation failed */
+#define DSORT_EHIP (-3)     /* HIP runtime error (kernel launch, copy, ...) */
+#define DSORT_ECOMM (-4)    /* RCCL error or communicator not initialised */
+#define DSORT_ENODEV (-5)   /* no gfx950 device / device index out of range */
+#define DSORT_ETIMEOUT (-6) /* a peer did not answer in time (fault path) */
+
+typedef struct dsort_ctx dsort_ctx;
+
+/* Stream argument meaning "the HIP null stream" (a NULL argument selects the context's own
+ * non-blocking stream instead). */
+#define DSORT_NULL_STREAM ((void *)1)
+
+/* Per-call stage timings of the last sort/merge on this context (device time, ms). */
+typedef struct dsort_stats {
+    double block_sort_ms;   /* LDS tile sort (the worker's merge_sort leaves)            */
+    double merge_ms;        /* global merge-path passes                                   */
+    double exchange_ms;     /* multi-GPU: sampling + splitters + RCCL all-to-all          */
+    double final_merge_ms;  /* multi-GPU: merge of the runs received from every rank      */
+    double total_ms;
+    double merge_kernel_ms; /* sum of the merge kernel's own launch durations (HIP events) */
+    int merge_kernel_launches;
+    int merge_passes;       /* number of global merge passes executed                     */
+    int tile_keys;          /* keys per block-sort tile                                   */
+    size_t keys_in;         /* keys handed to the call                                    */
+    size_t keys_out;        /* keys produced (multi-GPU: this rank's key range)           */
+} dsort_stats;
+
+/* ---------------------------------------------------------------- lifecycle ---------- */
+/* Creates a context bound to HIP device `device` (its own stream, scratch arenas). */
+int dsort_init(dsort_ctx **ctx, int device);
+int dsort_finalize(dsort_ctx *ctx);
+const char *dsort_last_error(const dsort_ctx *ctx);
+const char *dsort_version(void);
+int dsort_get_stats(const dsort_ctx *ctx, dsort_stats *out);
+/* Blocks until all work queued by this context has finished. */
+int dsort_synchronize(dsort_ctx *ctx);
+
+/* ---------------------------------------------------------------- worker sort -------- */
+/* Drop-in for `merge_sort(chunk, 0, n-1)` (client.c:117 -> client.c:166-173): sorts the
+ * caller-owned HOST buffer in place, ascending.  Copies to HBM, sorts on the GPU, copies
+ * back; returns when `host_keys` holds the result. */
+int dsort_sort_i32(dsort_ctx *ctx, int32_t *host_keys, size_t n);
+int dsort_sort_i64(dsort_ctx *ctx, int64_t *host_keys, size_t n);
+
+/* Device-resident variants: `d_keys` is device memory of this context's GPU, sorted in
+ * place, asynchronously on `stream` (NULL = context stream).  Scratch of n keys is taken
+ * from the context's arena (allocated on first use, reused afterwards). */
+int dsort_sort_dev_i32(dsort_ctx *ctx, int32_t *d_keys, size_t n, void *stream);
+int dsort_sort_dev_i64(dsort_ctx *ctx, int64_t *d_keys, size_t n, void *stream);
+/* Out-of-place: sorts d_in[0..n) into d_out (d_in is not modified; d_in == d_out allowed). */
+int dsort_sort_dev_copy_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_out, size_t n,
+                            void *stream);
+int dsort_sort_dev_copy_i64(dsort_ctx *ctx, const int64_t *d_in, int64_t *d_out, size_t n,
+                            void *stream);
+
+/* ---------------------------------------------------------------- master merge ------- */
+/* Drop-in for the merge half of merge_chunks (server.c:481-515): merges k sorted host runs
+ * into `out` (sum(lens) keys).  Ties take the lowest run index first, like the reference's
+ * strict `<` argmin scan (server.c:504), which for keys-only data is the sorted multiset.
+ * Unlike the reference, INT_MAX keys are kept. */
+int dsort_merge_i32(dsort_ctx *ctx, const int32_t *const runs[], const size_t lens[], int k,
+                    int32_t *out);
+int dsort_merge_i64(dsort_ctx *ctx, const int64_t *const runs[], const size_t lens[], int k,
+                    int64_t *out);
+/* Device-resident: the k runs lie back to back in d_in (run j has lens[j] keys, host array);
+ * the merged result goes to d_out (no overlap with d_in). */
+int dsort_merge_dev_i32(dsort_ctx *ctx, const int32_t *d_in, const size_t lens[], int k,
+                        int32_t *d_out, void *stream);
+int dsort_merge_dev_i64(dsort_ctx *ctx, const int64_t *d_in, const size_t lens[], int k,
+                        int64_t *d_out, void *stream);
+
+/* ---------------------------------------------------------------- multi-GPU ---------- */
+/* One process per GPU.  Rank 0 creates the 128-byte RCCL unique id and ships it to the other
+ * ranks by any side channel (the bench uses torch.distributed's store; the C master uses its
+ * TCP control socket); every rank then calls dsort_comm_init. */
+#define DSORT_UNIQUE_ID_BYTES 128
+int dsort_comm_unique_id(char id[DSORT_UNIQUE_ID_BYTES]);
+int dsort_comm_init(dsort_ctx *ctx, int nranks, int rank, const char id[DSORT_UNIQUE_ID_BYTES]);
+/* Abort in-flight collectives (fault path: a peer died) and drop the communicator. */
+int dsort_comm_abort(dsort_ctx *ctx);
+int dsort_comm_destroy(dsort_ctx *ctx);
+
+/* Sample sort over the communicator: every rank holds an equal contiguous
+ * chunk (server.c:185-216 partitioning); local sort, regular samples, all-gathered splitters
+ * with (value, rank, index) tie-splitting, RCCL all-to-all of key ranges, merge of the
+ * received runs.  On return *d_out points to this rank's slice of the global sorted order
+ * (owned by the context, valid until the next sample sort or dsort_finalize) and *n_out is its
+ * length; concatenating the slices of ranks 0..nranks-1 gives the sorted input.  `d_keys` is
+ * not modified (the local run is sorted into a context arena). */
+int dsort_sample_sort_dev_i32(dsort_ctx *ctx, const int32_t *d_keys, size_t n_local,
+                              int32_t **d_out, size_t *n_out, void *stream);
+int dsort_sample_sort_dev_i64(dsort_ctx *ctx, const int64_t *d_keys, size_t n_local,
+                              int64_t **d_out, size_t *n_out, void *stream);
+
+/* ---------------------------------------------------------------- sample-sort planning  */
+/* Host-side planning rules of the sample sort, exported so that the CPU tests (gloo, no GPU)
+ * exercise the exact code the GPU path runs.
+ *
+ * dsort_plan_splitters_*: `samples` holds nranks*s keys, s per rank, each rank's block sorted,
+ * sample j of rank r having local index idx[r*s+j].  Writes nranks-1 splitters as
+ * (value, rank, index) triples: the composite order (value, rank, index) is total, so ranks
+ * holding a heavy duplicate split it between them instead of one rank receiving it all. */
+int dsort_plan_splitters_i32(int nranks, int s, const int32_t *samples, const uint64_t *idx,
+                             int32_t *split_val, int32_t *split_rank, uint64_t *split_idx);
+int dsort_plan_splitters_i64(int nranks, int s, const int64_t *samples, const uint64_t *idx,
+                             int64_t *split_val, int32_t *split_rank, uint64_t *split_idx);
+/* dsort_plan_cuts_*: for a sorted local run of rank `my_rank`, cuts[0..nranks] (cuts[0]=0,
+ * cuts[nranks]=n) such that keys [cuts[r], cuts[r+1]) go to rank r. */
+int dsort_plan_cuts_i32(const int32_t *sorted, size_t n, int my_rank, int nranks,
+                        const int32_t *split_val, const int32_t *split_rank,
+                        const uint64_t *split_idx, uint64_t *cuts);
+int dsort_plan_cuts_i64(const int64_t *sorted, size_t n, int my_rank, int nranks,
+                        const int64_t *split_val, const int32_t *split_rank,
+                        const uint64_t *split_idx, uint64_t *cuts);
+/* Regular sample positions of a local run of n keys: s indices (j+1)*n/(s+1), j<s. */
+int dsort_plan_sample_positions(size_t n, int s, uint64_t *idx);
+
+/* ---------------------------------------------------------------- utilities ---------- */
+/* Synthetic workload generators on the GPU: key i = f(splitmix64(seed+first+i)).
+ * uniform i32 = high 32 bits, uniform i64 = all 64 bits; zipf i64 = s=1.2 over 2^24 ranks,
+ * key = rank * 0x9E3779B97F4A7C15 (an odd multiplier, so ranks map to distinct keys). */
+int dsort_gen_uniform_i32(dsort_ctx *ctx, int32_t *d_keys, size_t n, uint64_t seed,
+                          uint64_t first, void *stream);
+int dsort_gen_uniform_i64(dsort_ctx *ctx, int64_t *d_keys, size_t n, uint64_t seed,
+                          uint64_t first, void *stream);
+int dsort_gen_zipf_i64(dsort_ctx *ctx, int64_t *d_keys, size_t n, uint64_t seed, uint64_t first,
+                       void *stream);
+/* Size-independent parity checks on device data: order-independent multiset fingerprint
+ * (sum and xor of splitmix64 of each key) and the number of adjacent descents (0 = sorted).
+ * Blocking: results are on the host when the call returns. */
+int dsort_fingerprint_i32(dsort_ctx *ctx, const int32_t *d_keys, size_t n, uint64_t *sum,
+                          uint64_t *xr);
+int dsort_fingerprint_i64(dsort_ctx *ctx, const int64_t *d_keys, size_t n, uint64_t *sum,
+                          uint64_t *xr);
+int dsort_count_descents_i32(dsort_ctx *ctx, const int32_t *d_keys, size_t n, uint64_t *count);
+int dsort_count_descents_i64(dsort_ctx *ctx, const int64_t *d_keys, size_t n, uint64_t *count);
+
+/* Device memory helpers for hosts without another allocator (C master/worker, ctypes). */
+int dsort_dev_alloc(dsort_ctx *ctx, void **d_ptr, size_t bytes);
+int dsort_dev_free(dsort_ctx *ctx, void *d_ptr);
+int dsort_copy_h2d(dsort_ctx *ctx, void *d_dst, const void *h_src, size_t bytes);
+int dsort_copy_d2h(dsort_ctx *ctx, void *h_dst, const void *d_src, size_t bytes);
+
+/* Text output of the reference (server.c:517-519): one "%d\n" per key into `path`.
+ * Host-only helper; returns DSORT_EINVAL if the file cannot be written. */
+int dsort_write_text_i32(const char *path, const int32_t *keys, size_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DSORT_H */

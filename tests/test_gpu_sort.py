@@ -1,0 +1,195 @@
+"""GPU parity of the worker sort and the master merge against the oracle and the reference's
+golden vectors.  Runs on the MI355X box only (pytest -m gpu).  Every call goes through the C ABI
+(libdsort.so); the oracle is only the checker."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+CASES = json.load(open(os.path.join(GOLDEN, "cases.json")))
+INT_MIN, INT_MAX = -(2**31), 2**31 - 1
+I64_MIN, I64_MAX = -(2**63), 2**63 - 1
+TILE32, TILE64 = 8192, 4096
+
+
+def sha(b):
+    return hashlib.sha256(b).hexdigest()
+
+
+def test_reference_kat_output_txt(gpu_ctx, oracle):
+    """input.txt -> 4 equal chunks -> GPU worker sort each -> GPU merge -> output.txt bytes."""
+    raw = open(os.path.join(GOLDEN, "ref_input.txt"), "rb").read()
+    exp = open(os.path.join(GOLDEN, "ref_output.txt"), "rb").read()
+    keys = oracle.parse(raw)
+    sz, of = oracle.partition(keys.size, 4)
+    chunks = [keys[int(o):int(o) + int(s)].copy() for s, o in zip(sz, of)]
+    for c in chunks:
+        gpu_ctx.sort(c)
+    merged = gpu_ctx.merge(chunks)
+    assert oracle.format(merged) == exp
+    assert sha(oracle.format(merged)) == CASES["ref_output_sha256"]
+
+
+@pytest.mark.parametrize("case", CASES["e2e"], ids=lambda c: c["name"])
+def test_golden_e2e_whole_and_chunked(gpu_ctx, oracle, case):
+    keys = np.load(os.path.join(GOLDEN, case["name"] + ".in.npy"))
+    exp = np.load(os.path.join(GOLDEN, case["name"] + ".out.npy"))
+    whole = gpu_ctx.sort(keys.copy())
+    assert np.array_equal(whole, exp)
+    sz, of = oracle.partition(keys.size, 4)
+    chunks = [gpu_ctx.sort(keys[int(o):int(o) + int(s)].copy()) for s, o in zip(sz, of)]
+    merged = gpu_ctx.merge(chunks)
+    assert np.array_equal(merged, exp)
+    assert sha(oracle.format(merged)) == case["output_sha256"]
+
+
+@pytest.mark.parametrize("case", [c for c in CASES["merge_chunks"] if c["written_prefix"] == c["total"]],
+                         ids=lambda c: c["name"])
+def test_golden_merge_chunks(gpu_ctx, case):
+    z = np.load(os.path.join(GOLDEN, case["name"] + ".npz"))
+    runs = [z[f"arr_{i}"] for i in range(case["k"])]
+    assert gpu_ctx.merge(runs).tolist() == case["reference_output_prefix"]
+
+
+def test_merge_keeps_intmax(gpu_ctx, oracle):
+    """Documented divergence from the reference: INT_MAX keys are kept."""
+    runs = [np.array([1, INT_MAX, INT_MAX], np.int32), np.array([-5, 2], np.int32),
+            np.array([0], np.int32), np.array([INT_MAX], np.int32)]
+    assert gpu_ctx.merge(runs).tolist() == oracle.merge_runs(runs).tolist()
+
+
+@pytest.mark.parametrize("case", CASES["merge_sort"], ids=lambda c: c["name"])
+def test_golden_merge_sort(gpu_ctx, case):
+    a = np.load(os.path.join(GOLDEN, case["name"] + ".in.npy"))
+    exp = np.load(os.path.join(GOLDEN, case["name"] + ".out.npy"))
+    assert np.array_equal(gpu_ctx.sort(a.copy()), exp)
+
+
+SIZES = [0, 1, 2, 3, 15, 16, 17, 511, 4096, TILE32 - 1, TILE32, TILE32 + 1, 2 * TILE32,
+         3 * TILE32 + 5, 5 * TILE32 - 7, 17 * TILE32 + 123, 100003, 1 << 20, (1 << 20) + 3333]
+
+
+def _dist(rng, kind, n, dt):
+    info = np.iinfo(dt)
+    if kind == "uniform":
+        return rng.integers(info.min, info.max, n, dtype=dt, endpoint=True)
+    if kind == "equal":
+        return np.full(n, -1, dt)
+    if kind == "sorted":
+        return np.sort(rng.integers(info.min, info.max, n, dtype=dt, endpoint=True))
+    if kind == "reverse":
+        return np.sort(rng.integers(info.min, info.max, n, dtype=dt, endpoint=True))[::-1].copy()
+    if kind == "few":
+        return rng.choice(np.array([info.min, -1, 0, 1, info.max], dt), n)
+    if kind == "extremes":
+        a = rng.integers(-3, 3, n).astype(dt)
+        a[::3] = info.max
+        a[1::5] = info.min
+        return a
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("n", SIZES)
+@pytest.mark.parametrize("kind", ["uniform", "equal", "sorted", "reverse", "few", "extremes"])
+def test_sort_i32_vs_oracle(gpu_ctx, oracle, n, kind):
+    rng = np.random.default_rng(n * 7 + len(kind))
+    a = _dist(rng, kind, n, np.int32)
+    exp = oracle.merge_sort(a) if n <= 200000 else np.sort(a, kind="stable")
+    got = gpu_ctx.sort(a.copy())
+    assert np.array_equal(got, exp)
+
+
+@pytest.mark.parametrize("n", [0, 1, 5, TILE64 - 1, TILE64, TILE64 + 1, 9 * TILE64 + 77, 300001])
+@pytest.mark.parametrize("kind", ["uniform", "few", "extremes", "reverse"])
+def test_sort_i64_vs_oracle(gpu_ctx, oracle, n, kind):
+    rng = np.random.default_rng(n * 13 + len(kind))
+    a = _dist(rng, kind, n, np.int64)
+    exp = oracle.merge_sort(a) if n <= 200000 else np.sort(a, kind="stable")
+    assert np.array_equal(gpu_ctx.sort(a.copy()), exp)
+
+
+@pytest.mark.parametrize("k", [1, 2, 3, 4, 5, 8, 9, 16, 33])
+def test_merge_k_runs_vs_oracle(gpu_ctx, oracle, k):
+    rng = np.random.default_rng(k)
+    lens = rng.integers(0, 3 * TILE32, k)
+    lens[0] = 0 if k > 2 else lens[0]
+    runs = [np.sort(rng.integers(-1000, 1000, int(m))).astype(np.int32) for m in lens]
+    exp = oracle.merge_runs(runs)
+    assert np.array_equal(gpu_ctx.merge(runs), exp)
+    runs64 = [np.sort(rng.integers(I64_MIN, I64_MAX, int(m), endpoint=True)) for m in lens]
+    assert np.array_equal(gpu_ctx.merge(runs64), oracle.merge_runs(runs64, np.int64))
+
+
+def test_merge_all_empty(gpu_ctx):
+    assert gpu_ctx.merge([np.zeros(0, np.int32)] * 3).size == 0
+
+
+def test_device_sort_inplace_and_copy(gpu_ctx, oracle):
+    import torch
+    n = 3 * TILE32 * 64 + 99
+    a = oracle.gen_uniform(0x5EED2026, 0, n)
+    t = torch.from_numpy(a).cuda()
+    out = torch.empty_like(t)
+    gpu_ctx.sort_dev(t, out)
+    assert np.array_equal(t.cpu().numpy(), a)  # input untouched
+    assert np.array_equal(out.cpu().numpy(), np.sort(a))
+    gpu_ctx.sort_dev(t)
+    assert np.array_equal(t.cpu().numpy(), np.sort(a))
+
+
+def test_gpu_generator_matches_oracle(gpu_ctx, oracle):
+    import torch
+    t = torch.empty(100000, dtype=torch.int32, device="cuda")
+    gpu_ctx.gen_uniform(t, 0x5EED2026, 12345)
+    assert np.array_equal(t.cpu().numpy(), oracle.gen_uniform(0x5EED2026, 12345, 100000))
+    t64 = torch.empty(50000, dtype=torch.int64, device="cuda")
+    gpu_ctx.gen_uniform(t64, 7, 3)
+    assert np.array_equal(t64.cpu().numpy(), oracle.gen_uniform(7, 3, 50000, np.int64))
+
+
+def test_gpu_fingerprint_matches_oracle(gpu_ctx, oracle):
+    import torch
+    a = oracle.gen_uniform(11, 0, 1 << 20)
+    t = torch.from_numpy(a).cuda()
+    assert gpu_ctx.fingerprint(t) == oracle.fingerprint(a)
+    b = np.random.default_rng(2).integers(I64_MIN, I64_MAX, 70001, dtype=np.int64)
+    assert gpu_ctx.fingerprint(torch.from_numpy(b).cuda()) == oracle.fingerprint(b)
+    s = torch.from_numpy(np.sort(a)).cuda()
+    assert gpu_ctx.descents(s) == 0
+    assert gpu_ctx.descents(t) == int((a[1:] < a[:-1]).sum())
+
+
+@pytest.mark.parametrize("n,dt", [(1 << 28, "i32"), ((1 << 26) + 12345, "i64")])
+def test_full_size_properties(gpu_ctx, n, dt):
+    """At BASELINE sizes the oracle is too slow: check size-independent properties on the GPU --
+    the output is ascending and is the same multiset as the input (fingerprint)."""
+    import torch
+    tdt = torch.int32 if dt == "i32" else torch.int64
+    t = torch.empty(n, dtype=tdt, device="cuda")
+    gpu_ctx.gen_uniform(t, 0x5EED2026, 0)
+    fp_in = gpu_ctx.fingerprint(t)
+    out = torch.empty_like(t)
+    gpu_ctx.sort_dev(t, out)
+    assert gpu_ctx.descents(out) == 0
+    assert gpu_ctx.fingerprint(out) == fp_in
+    del t, out
+    torch.cuda.empty_cache()
+
+
+def test_zipf_i64_sort(gpu_ctx):
+    import torch
+    n = (1 << 24) + 17
+    t = torch.empty(n, dtype=torch.int64, device="cuda")
+    gpu_ctx.gen_zipf_i64(t, 0x5EED2026)
+    host = t.cpu().numpy()
+    top = np.unique(host[: 1 << 20], return_counts=True)[1].max() / (1 << 20)
+    assert top > 0.05  # heavy hitter present
+    out = torch.empty_like(t)
+    gpu_ctx.sort_dev(t, out)
+    assert np.array_equal(out.cpu().numpy(), np.sort(host))
