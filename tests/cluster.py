@@ -33,6 +33,23 @@ def free_port():
     return p
 
 
+def established(port):
+    """Number of accepted-or-pending TCP connections whose local port is `port` (the master's
+    side), in any state but LISTEN: a worker that already died still counts (CLOSE_WAIT)."""
+    n = 0
+    for path in ("/proc/net/tcp", "/proc/net/tcp6"):
+        try:
+            with open(path) as f:
+                next(f)
+                for line in f:
+                    parts = line.split()
+                    if parts[3] != "0A" and int(parts[1].split(":")[1], 16) == port:
+                        n += 1
+        except OSError:
+            pass
+    return n
+
+
 def listening(port):
     """True once some socket LISTENs on `port` (read from /proc, without connecting: a probe
     connection would take one of the master's accept() slots)."""
@@ -84,9 +101,13 @@ class Session:
                 wc = [os.path.join(BIN, "dsort_worker"), "--proto", proto, *wargs[i], "client.conf"]
             else:
                 wc = [os.path.join(REF_BUILD, "client"), "client.conf"]
-            self.workers.append(subprocess.Popen(wc, cwd=self.dir, stdout=log, stderr=subprocess.STDOUT,
-                                                 env=self.env))
-            time.sleep(0.05)  # accept order = worker identity (server.c:148)
+            p = subprocess.Popen(wc, cwd=self.dir, stdout=log, stderr=subprocess.STDOUT, env=self.env)
+            self.workers.append(p)
+            # accept order = worker identity (server.c:148): wait for this worker's connection
+            # before starting the next (a GPU worker connects only after its context is up)
+            t0 = time.time()
+            while established(self.port) < i + 1 and p.poll() is None and time.time() - t0 < 60:
+                time.sleep(0.01)
 
     def sort_files(self, names, timeout=120):
         self.master.stdin.write(("\n".join(names) + "\nexit\n").encode())
