@@ -502,12 +502,14 @@ int dsort_finalize(dsort_ctx *ctx) {
         ncclCommDestroy(ctx->comm);
         ctx->comm = nullptr;
     }
-    void *bufs[] = {ctx->scratch, ctx->buckets, ctx->pairs, ctx->io, ctx->io2, ctx->red,
+    void *bufs[] = {ctx->scratch, ctx->scratch2, ctx->splits, ctx->groups, ctx->io, ctx->io2, ctx->red,
                     ctx->local, ctx->recv, ctx->recv2, ctx->small};
     for (void *b : bufs)
         if (b) hipFree(b);
     if (ctx->red_host) hipHostFree(ctx->red_host);
     if (ctx->small_host) hipHostFree(ctx->small_host);
+    if (ctx->groups_host) (void)hipHostFree(ctx->groups_host);
+    if (ctx->groups_ev) (void)hipEventDestroy(ctx->groups_ev);
     for (auto &e : ctx->ev)
         if (e) (void)hipEventDestroy(e);
     for (auto &e : ctx->kev)

@@ -31,22 +31,31 @@ template <> struct Geom<int64_t> {
     static constexpr int TILE = THREADS * K;
 };
 
-// One output tile of a 2-way merge pass: merge in[a_start, a_start+a_len) with
-// in[b_start, b_start+b_len) into out[out_off, out_off + a_len + b_len).
-struct Bucket2 {
-    uint64_t out_off;
-    uint64_t a_start;
-    uint64_t b_start;
-    uint32_t a_len;
-    uint32_t b_len;
+// ----------------------------------------------------------------------------------------
+// k-way merge passes.  A pass merges GROUPS of up to F sorted runs (F a power of two <= kMaxF)
+// that lie back to back; every group's output is cut into TILE-key output tiles, one workgroup
+// per tile.  Regular passes (the sort): runs of length R, groups of F runs, so every group is
+// a multiple of TILE long and tile j covers output [j*TILE, (j+1)*TILE).  Irregular passes (the
+// master merge, the multi-GPU receive merge): a table of groups with arbitrary run lengths.
+// ----------------------------------------------------------------------------------------
+constexpr int kMaxLogF = 6;
+constexpr int kMaxF = 1 << kMaxLogF;
+
+struct GroupK {
+    uint64_t base;        // first key of the group (input and output index)
+    uint64_t first_tile;  // global index of the group's first output tile
+    uint64_t total;       // keys in the group
+    uint32_t nruns;       // runs in the group (<= F of the pass)
+    uint32_t pad;
+    uint64_t roff[kMaxF + 1];  // run i = [base + roff[i], base + roff[i+1])
 };
 
-// A pair of adjacent runs to merge (irregular passes: user runs of arbitrary length).
-struct Pair {
-    uint64_t a_off;         // run A starts here; run B follows at a_off + a_len
-    uint64_t a_len;
-    uint64_t b_len;
-    uint64_t first_bucket;  // global index of the pair's first output tile
+struct PassDesc {
+    uint64_t n;              // keys in the whole array
+    uint64_t R;              // regular: run length (a multiple of TILE)
+    int F;                   // runs per group, power of two
+    int ngroups;             // irregular: entries in `groups`
+    const GroupK *groups;    // irregular: group table (device memory)
 };
 
 }  // namespace dsort
@@ -59,10 +68,16 @@ struct dsort_ctx {
     // grow-only device arenas
     void *scratch = nullptr;
     size_t scratch_bytes = 0;
-    void *buckets = nullptr;
-    size_t buckets_bytes = 0;
-    void *pairs = nullptr;
-    size_t pairs_bytes = 0;
+    void *splits = nullptr;   // per-tile split vectors of a k-way pass (uint32 x F per tile)
+    size_t splits_bytes = 0;
+    void *groups = nullptr;   // irregular group tables (device)
+    size_t groups_bytes = 0;
+    void *groups_host = nullptr;  // pinned staging of the group tables
+    size_t groups_host_bytes = 0;
+    hipEvent_t groups_ev = nullptr;  // last H2D copy out of groups_host
+    bool groups_ev_pending = false;
+    void *scratch2 = nullptr; // second scratch for multi-level irregular merges
+    size_t scratch2_bytes = 0;
     void *io = nullptr;        // staging for the host-buffer entry points
     size_t io_bytes = 0;
     void *io2 = nullptr;
