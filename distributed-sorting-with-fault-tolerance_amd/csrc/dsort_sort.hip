@@ -78,25 +78,71 @@ __device__ __forceinline__ void sort_regs(T (&v)[K]) {
     }
 }
 
-// LDS layout: key position p lives at word p + p/32 (one pad word per 32).  Merge levels make
-// lane t touch positions ~K/2*t + i (windows) and K*t + i (outputs); unpadded, those strides
-// fold onto a few of the 32 banks (up to 16-way conflicts); the pad rotates every 32-key row
-// by one bank.
-__device__ __forceinline__ int swz(int p) { return p + (p >> 5); }
-__host__ __device__ constexpr int padded(int n) { return n + n / 32; }
+// LDS layout.  Keys are grouped in 16-byte chunks (4 int32 / 2 int64); chunk c is stored at
+// slot c ^ ((c >> 3) & 3).  Within a 128-byte row of 8 chunks this XOR gives the 8 lanes of a
+// ds_write_b128 lane group distinct slots when each lane writes its own K keys (chunks 4t..),
+// and keeps every chunk 16-byte contiguous, so windows and outputs move as ds_read_b128 /
+// ds_write_b128 (CDNA4 LDS: 256 B/clk for b128 vs 128 B/clk for b32).
+template <typename T> struct Chunk;
+template <> struct Chunk<int32_t> { using V = int4; static constexpr int KPC = 4, SH = 2; };
+template <> struct Chunk<int64_t> { using V = longlong2; static constexpr int KPC = 2, SH = 1; };
+
+__device__ __forceinline__ int cslot(int c) { return c ^ ((c >> 3) & 3); }
+template <typename T>
+__device__ __forceinline__ int kpos(int p) {  // LDS word (key) index of key position p
+    constexpr int SH = Chunk<T>::SH;
+    return (cslot(p >> SH) << SH) | (p & ((1 << SH) - 1));
+}
+// LDS keys to allocate for a tile of n keys: window reads run up to 6 chunks past the end.
+template <typename T> __host__ __device__ constexpr int lds_keys(int n) { return n + 8 * Chunk<T>::KPC; }
 
 // Merge-path split on LDS: number of A keys among the first `diag` outputs of merge(A, B),
-// A first on ties.  A = s[A0 .. A0+na), B = s[B0 .. B0+nb) in key positions.
+// A first on ties.  A = positions [A0, A0+na), B = [B0, B0+nb).
 template <typename T>
 __device__ __forceinline__ int lds_merge_path(const T *s, int A0, int na, int B0, int nb, int diag) {
     int lo = diag > nb ? diag - nb : 0;
     int hi = diag < na ? diag : na;
     while (lo < hi) {
         const int mid = (lo + hi) >> 1;
-        if (s[swz(A0 + mid)] <= s[swz(B0 + diag - 1 - mid)]) lo = mid + 1;
+        if (s[kpos<T>(A0 + mid)] <= s[kpos<T>(B0 + diag - 1 - mid)]) lo = mid + 1;
         else hi = mid;
     }
     return lo;
+}
+
+// K keys from position `start` (keys at offset >= lim read as key_max): the K/KPC+1 chunks that
+// cover the window are read as 16-byte LDS vectors, then shifted by start % KPC in registers.
+template <typename T, int K>
+__device__ __forceinline__ void load_window(const T *s, int start, int lim, T (&x)[K]) {
+    using V = typename Chunk<T>::V;
+    constexpr int KPC = Chunk<T>::KPC, SH = Chunk<T>::SH, NCH = K / KPC + 1;
+    const V *sv = reinterpret_cast<const V *>(s);
+    const int c0 = start >> SH, off = start & (KPC - 1);
+    T w[NCH * KPC];
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+        const V v = sv[cslot(c0 + j)];
+        const T *pv = reinterpret_cast<const T *>(&v);
+#pragma unroll
+        for (int q = 0; q < KPC; ++q) w[j * KPC + q] = pv[q];
+    }
+    // The shift is a bitwise blend on purpose: written as `(off & 1) ? w[i+1] : w[i]` hipcc
+    // folds it into w[i + off], a dynamically indexed array, i.e. scratch memory.
+    using U = typename Unsigned<T>::type;
+    const U m1 = (U)0 - (U)(off & 1);
+    if (KPC == 4) {
+        const U m2 = (U)0 - (U)((off >> 1) & 1);
+        T u[NCH * KPC - 1];
+#pragma unroll
+        for (int i = 0; i < NCH * KPC - 1; ++i) u[i] = (T)(((U)w[i] & ~m1) | ((U)w[i + 1] & m1));
+#pragma unroll
+        for (int i = 0; i < K; ++i) x[i] = (T)(((U)u[i] & ~m2) | ((U)u[i + 2] & m2));
+    } else {
+#pragma unroll
+        for (int i = 0; i < K; ++i) x[i] = (T)(((U)w[i] & ~m1) | ((U)w[i + 1] & m1));
+    }
+#pragma unroll
+    for (int i = 0; i < K; ++i) x[i] = i < lim ? x[i] : key_max<T>();
 }
 
 // The K smallest keys of A[a..na) u B[b..nb): the two ascending K-windows form the bitonic
@@ -106,44 +152,55 @@ template <typename T, int K>
 __device__ __forceinline__ void kmerge(const T *s, int A0, int na, int B0, int nb, int a, int b,
                                        T (&m)[K]) {
     T x[K], y[K];
-#pragma unroll
-    for (int i = 0; i < K; ++i) x[i] = (a + i < na) ? s[swz(A0 + a + i)] : key_max<T>();
-#pragma unroll
-    for (int i = 0; i < K; ++i) y[i] = (b + i < nb) ? s[swz(B0 + b + i)] : key_max<T>();
+    load_window<T, K>(s, A0 + a, na - a, x);
+    load_window<T, K>(s, B0 + b, nb - b, y);
 #pragma unroll
     for (int i = 0; i < K; ++i) m[i] = x[i] < y[K - 1 - i] ? x[i] : y[K - 1 - i];
 #pragma unroll
-    for (int s = K / 2; s >= 1; s >>= 1) {
+    for (int st = K / 2; st >= 1; st >>= 1) {
 #pragma unroll
         for (int i = 0; i < K; ++i)
-            if ((i & s) == 0) cex(m[i], m[i + s]);
+            if ((i & st) == 0) cex(m[i], m[i + st]);
     }
 }
 
-// Coalesced store of the first `valid` keys of a padded LDS tile: full tiles leave as 16-byte
-// vectors (lane t writes vectors t, t+THREADS, ...), assembled from conflict-free 4-byte reads.
+// K keys of one lane to positions [pos, pos+K), pos a multiple of K: whole chunks.
+template <typename T, int K>
+__device__ __forceinline__ void store_lane(T *s, int pos, const T (&v)[K]) {
+    using V = typename Chunk<T>::V;
+    constexpr int KPC = Chunk<T>::KPC, SH = Chunk<T>::SH;
+    V *sv = reinterpret_cast<V *>(s);
+#pragma unroll
+    for (int j = 0; j < K / KPC; ++j) {
+        V x;
+        T *px = reinterpret_cast<T *>(&x);
+#pragma unroll
+        for (int q = 0; q < KPC; ++q) px[q] = v[j * KPC + q];
+        sv[cslot((pos >> SH) + j)] = x;
+    }
+}
+
+// Coalesced store of the first `valid` keys of an LDS tile: full tiles leave as 16-byte vectors
+// (lane t moves chunks t, t+THREADS, ...: one ds_read_b128 and one global_store_dwordx4 each).
 template <typename T, int THREADS, int K>
 __device__ __forceinline__ void store_tile(const T *s, T *out, int valid) {
     constexpr int TILE = THREADS * K;
-    using V = typename Vec16<T>::type;
-    constexpr int VN = Vec16<T>::N;
+    using V = typename Chunk<T>::V;
+    constexpr int KPC = Chunk<T>::KPC;
     const int t = threadIdx.x;
     if (valid == TILE && (reinterpret_cast<uintptr_t>(out) % 16) == 0) {
         V *dst = reinterpret_cast<V *>(out);
+        const V *sv = reinterpret_cast<const V *>(s);
 #pragma unroll
-        for (int i = 0; i < K / VN; ++i) {
+        for (int i = 0; i < K / KPC; ++i) {
             const int q = i * THREADS + t;
-            V x;
-            T *px = reinterpret_cast<T *>(&x);
-#pragma unroll
-            for (int j = 0; j < VN; ++j) px[j] = s[swz(q * VN + j)];
-            dst[q] = x;
+            dst[q] = sv[cslot(q)];
         }
     } else {
 #pragma unroll
         for (int i = 0; i < K; ++i) {
             const int e = i * THREADS + t;
-            if (e < valid) out[e] = s[swz(e)];
+            if (e < valid) out[e] = s[kpos<T>(e)];
         }
     }
 }
@@ -157,7 +214,7 @@ __global__ void __launch_bounds__(THREADS) block_sort_kernel(const T *in, T *out
     constexpr int TILE = THREADS * K;
     using V = typename Vec16<T>::type;
     constexpr int VN = Vec16<T>::N;
-    __shared__ __attribute__((aligned(16))) T s[padded(TILE)];
+    __shared__ __attribute__((aligned(16))) T s[lds_keys<T>(TILE)];
 
     const int t = threadIdx.x;
     const uint64_t base = (uint64_t)blockIdx.x * TILE;
@@ -184,8 +241,7 @@ __global__ void __launch_bounds__(THREADS) block_sort_kernel(const T *in, T *out
 
     sort_regs<T, K>(v);
     const int pos = t * K;
-#pragma unroll
-    for (int i = 0; i < K; ++i) s[swz(pos + i)] = v[i];
+    store_lane<T, K>(s, pos, v);
     __syncthreads();
 
 #pragma unroll 1
@@ -195,32 +251,35 @@ __global__ void __launch_bounds__(THREADS) block_sort_kernel(const T *in, T *out
         const int a = lds_merge_path(s, pb, r, pb + r, r, diag);
         kmerge<T, K>(s, pb, r, pb + r, r, a, diag - a, v);
         __syncthreads();
-#pragma unroll
-        for (int i = 0; i < K; ++i) s[swz(pos + i)] = v[i];
+        store_lane<T, K>(s, pos, v);
         __syncthreads();
     }
     store_tile<T, THREADS, K>(s, out + base, valid);
 }
 
 // ---------------------------------------------------------------------------------------
-// Tile / group geometry of a k-way pass.
+// Tile / group geometry of a k-way pass.  A group's output is cut into tiles of NOMINAL size
+// tnom = TILE - 2*slack; the actual cut of boundary jr lies within +-slack of jr*tnom, so every
+// tile holds at most TILE keys.
 // ---------------------------------------------------------------------------------------
 struct TileInfo {
     uint64_t base;    // group start
     uint64_t gtotal;  // keys in the group
-    uint64_t d0, d1;  // the tile's output ranks [d0, d1) within the group
+    uint64_t jr;      // tile index within the group
+    uint64_t ntg;     // tiles in the group
 };
 
 template <bool REG>
-__device__ __forceinline__ const GroupK *tile_info(const PassDesc &pd, uint64_t j, int tile,
+__device__ __forceinline__ const GroupK *tile_info(const PassDesc &pd, uint64_t j, int tnom,
                                                    TileInfo &ti) {
     const GroupK *g = nullptr;
     if (REG) {
         const uint64_t gsize = (uint64_t)pd.F * pd.R;
-        const uint64_t start = j * (uint64_t)tile;
-        ti.base = start - start % gsize;
+        const uint64_t tpg = (gsize + tnom - 1) / tnom;
+        const uint64_t gi = j / tpg;
+        ti.base = gi * gsize;
         ti.gtotal = pd.n - ti.base < gsize ? pd.n - ti.base : gsize;
-        ti.d0 = start - ti.base;
+        ti.jr = j - gi * tpg;
     } else {
         int lo = 0, hi = pd.ngroups - 1;  // last group with first_tile <= j
         while (lo < hi) {
@@ -231,9 +290,9 @@ __device__ __forceinline__ const GroupK *tile_info(const PassDesc &pd, uint64_t 
         g = pd.groups + lo;
         ti.base = g->base;
         ti.gtotal = g->total;
-        ti.d0 = (j - g->first_tile) * (uint64_t)tile;
+        ti.jr = j - g->first_tile;
     }
-    ti.d1 = ti.d0 + tile < ti.gtotal ? ti.d0 + tile : ti.gtotal;
+    ti.ntg = (ti.gtotal + tnom - 1) / tnom;
     return g;
 }
 
@@ -274,29 +333,67 @@ __device__ __forceinline__ T wave_max(T v) {
     return v;
 }
 
-// Candidate key c of C strictly inside [lo, hi): lo + floor((hi-lo) * (c+1) / (C+1)), computed
-// without overflow in the unsigned type of T.
+// lo + round(frac * (hi - lo)) clamped to [lo, hi - 1]; frac in [0, 1].  Doubles carry the
+// estimate only: the result is always a valid key strictly below hi.
 template <typename T>
-__device__ __forceinline__ T candidate(T lo, T hi, int c, int C) {
+__device__ __forceinline__ T key_at(T lo, T hi, double frac) {
     using U = typename Unsigned<T>::type;
-    const U range = (U)hi - (U)lo;
-    const U q = range / (U)(C + 1), r = range % (U)(C + 1);
-    return (T)((U)lo + q * (U)(c + 1) + (r * (U)(c + 1)) / (U)(C + 1));
+    const U range = (U)hi - (U)lo;  // > 0
+    frac = frac < 0.0 ? 0.0 : (frac > 1.0 ? 1.0 : frac);
+    double off = frac * (double)range;
+    U o = off >= (double)range ? range - 1 : (U)off;
+    if (o >= range) o = range - 1;
+    return (T)((U)lo + o);
+}
+
+// #keys <= v in A[u, h), knowing A[u..h) lies within [klo, khi]: interpolation probes while the
+// window is large, then binary search.  Each probe is one dependent load.
+template <typename T>
+__device__ __forceinline__ uint64_t upper_bound_interp(const T *A, uint64_t u, uint64_t h, T v,
+                                                       T klo, T khi) {
+    using U = typename Unsigned<T>::type;
+#pragma unroll 1
+    for (int it = 0; it < 4 && h - u > 32; ++it) {
+        if (v < klo) return u;
+        if (v >= khi) return h;
+        const double frac = (double)((U)v - (U)klo) / ((double)((U)khi - (U)klo) + 1.0);
+        uint64_t m = u + (uint64_t)(frac * (double)(h - u));
+        m = m < u ? u : (m >= h ? h - 1 : m);
+        const T x = A[m];
+        if (x <= v) {
+            u = m + 1;
+            klo = x;
+        } else {
+            h = m;
+            khi = x;
+        }
+    }
+    while (u < h) {
+        const uint64_t m = (u + h) >> 1;
+        if (A[m] <= v) u = m + 1;
+        else h = m;
+    }
+    return u;
 }
 
 // ---------------------------------------------------------------------------------------
-// 2a. Exact split of output rank d0 of every tile over the F runs of its group.
-//     Writes splits[j*F + i] = number of keys of run i before rank d0 (relative to the run).
+// 2a. Cut of every tile boundary: for nominal rank d = jr*tnom find a VALID cut (all keys below
+//     a threshold in (key, run, position) order) whose rank lies in [d - slack, d + slack].
+//     One wave per tile; lane (c, i) evaluates candidate key c on run i (C = 64/F candidates
+//     per step).  Candidates bracket the interpolated key of rank d; a step that does not at
+//     least halve the bracket is followed by a plain C-section step.  A bracket collapsed to a
+//     single key (a heavy duplicate) is cut exactly at d, equal keys taken in run order.
+//     Writes splits[j*F + i] = keys of run i below the cut (relative to the run start).
 // ---------------------------------------------------------------------------------------
 template <typename T, bool REG>
-__global__ void __launch_bounds__(256) partk_kernel(const T *__restrict__ in, PassDesc pd, int tile,
-                                                    uint32_t *__restrict__ splits,
+__global__ void __launch_bounds__(256) partk_kernel(const T *__restrict__ in, PassDesc pd, int tnom,
+                                                    int slack, uint32_t *__restrict__ splits,
                                                     uint64_t ntiles) {
     const int lane = threadIdx.x & 63;
     const uint64_t j = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (j >= ntiles) return;  // wave-uniform
     TileInfo ti;
-    const GroupK *g = tile_info<REG>(pd, j, tile, ti);
+    const GroupK *g = tile_info<REG>(pd, j, tnom, ti);
     const int F = pd.F;
     const int C = 64 / F;
     const int i = lane & (F - 1);
@@ -305,53 +402,87 @@ __global__ void __launch_bounds__(256) partk_kernel(const T *__restrict__ in, Pa
     run_range<REG>(pd, ti, g, i, rs, rl);
     const T *A = in + rs;
     uint32_t *outp = splits + j * (uint64_t)F;
-    const uint64_t d = ti.d0;
+    const uint64_t d = ti.jr * (uint64_t)tnom;
     if (d == 0) {
         if (c == 0) outp[i] = 0;
         return;
     }
     T lo = wave_min(rl ? A[0] : key_max<T>());
     T hi = wave_max(rl ? A[rl - 1] : key_min<T>());
-    // invariant: ilo = #keys < lo, ihi = #keys <= hi in run i; sum(ilo) < d <= sum(ihi)
+    // bracket: ilo = #keys < lo, ihi = #keys <= hi in run i; nlo = sum(ilo) <= d <= sum(ihi) = nhi
     uint64_t ilo = 0, ihi = rl;
-    while (lo < hi) {
-        const T cand = candidate(lo, hi, c, C);
-        uint64_t u = ilo, h = ihi;
-        while (u < h) {
-            const uint64_t m = (u + h) >> 1;
-            if (A[m] <= cand) u = m + 1;
-            else h = m;
+    uint64_t nlo = 0, nhi = ti.gtotal;
+    bool interp = true;
+    uint64_t cut_i = 0;
+    bool done = false;
+#pragma unroll 1
+    for (int it = 0; it < 200 && !done; ++it) {
+        if (nhi - nlo <= (uint64_t)slack) {  // cut just below lo: rank nlo in [d - slack, d]
+            cut_i = ilo;
+            done = true;
+            break;
         }
+        if (lo == hi) break;  // a single key left: exact tie split below
+        T cand;
+        if (interp) {
+            const double n = (double)(nhi - nlo);
+            const double spread = fmax((double)slack * 0.5, 3.0 * sqrt(n));
+            const double r = C == 1 ? 0.0 : -spread + 2.0 * spread * (double)c / (double)(C - 1);
+            cand = key_at(lo, hi, ((double)d + r - (double)nlo) / n);
+        } else {
+            using U = typename Unsigned<T>::type;
+            const U range = (U)hi - (U)lo;
+            const U q = range / (U)(C + 1), rr = range % (U)(C + 1);
+            cand = (T)((U)lo + q * (U)(c + 1) + (rr * (U)(c + 1)) / (U)(C + 1));
+        }
+        const uint64_t u = upper_bound_interp(A, ilo, ihi, cand, lo, hi);
         uint64_t tot = u;
         for (int o = 1; o < F; o <<= 1) tot += __shfl_xor(tot, o);
+        // a candidate whose cut already lands within the slack ends the search
+        const bool ok = tot + (uint64_t)slack >= d && tot <= d + (uint64_t)slack;
+        const unsigned long long okm = __ballot(ok);
+        if (okm) {
+            const int cg = (int)((__ffsll((long long)okm) - 1) / F);
+            cut_i = __shfl(u, cg * F + i);
+            done = true;
+            break;
+        }
         const unsigned long long mask = __ballot(tot >= d);
         const int cs = mask ? (int)((__ffsll((long long)mask) - 1) / F) : C;  // first cand with U >= d
         const uint64_t ub_cs = __shfl(u, (cs < C ? cs : 0) * F + i);
         const uint64_t ub_pr = __shfl(u, (cs > 0 ? cs - 1 : 0) * F + i);
-        const T lo0 = lo, hi0 = hi;
+        const uint64_t tot_cs = __shfl(tot, (cs < C ? cs : 0) * F);
+        const uint64_t tot_pr = __shfl(tot, (cs > 0 ? cs - 1 : 0) * F);
+        const T cand_cs = __shfl(cand, (cs < C ? cs : 0) * F);
+        const T cand_pr = __shfl(cand, (cs > 0 ? cs - 1 : 0) * F);
+        const uint64_t before = nhi - nlo;
         if (cs < C) {
-            hi = candidate(lo0, hi0, cs, C);
+            hi = cand_cs;
             ihi = ub_cs;
+            nhi = tot_cs;
         }
         if (cs > 0) {
-            lo = candidate(lo0, hi0, cs - 1, C) + 1;
+            lo = cand_pr + 1;
             ilo = ub_pr;
+            nlo = tot_pr;
         }
+        // keep interpolating while it at least halves the bracket
+        interp = (nhi - nlo) * 2 <= before;
     }
-    // lo == hi == the key at rank d: ilo = #keys < key, ihi = #keys <= key.  The d - sum(ilo)
-    // remaining slots go to the equal keys in run order (lower runs first).
-    uint64_t below = ilo;
-    for (int o = 1; o < F; o <<= 1) below += __shfl_xor(below, o);
-    const uint64_t cnt = ihi - ilo;
-    uint64_t incl = cnt;  // inclusive scan of cnt over the F lanes of this candidate group
-    for (int o = 1; o < F; o <<= 1) {
-        const uint64_t v = __shfl_up(incl, o);
-        if (i >= o) incl += v;
+    if (!done) {
+        // lo == hi: ilo = #keys < key, ihi = #keys <= key; take d - sum(ilo) equal keys in run order
+        const uint64_t cnt = ihi - ilo;
+        uint64_t incl = cnt;
+        for (int o = 1; o < F; o <<= 1) {
+            const uint64_t v = __shfl_up(incl, o);
+            if (i >= o) incl += v;
+        }
+        const uint64_t excl = incl - cnt;
+        const uint64_t need = d - nlo;
+        const uint64_t take = need > excl ? (need - excl < cnt ? need - excl : cnt) : 0;
+        cut_i = ilo + take;
     }
-    const uint64_t excl = incl - cnt;
-    const uint64_t need = d - below;
-    const uint64_t take = need > excl ? (need - excl < cnt ? need - excl : cnt) : 0;
-    if (c == 0) outp[i] = (uint32_t)(ilo + take);
+    if (c == 0) outp[i] = (uint32_t)cut_i;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -360,42 +491,48 @@ __global__ void __launch_bounds__(256) partk_kernel(const T *__restrict__ in, Pa
 // ---------------------------------------------------------------------------------------
 template <typename T, int THREADS, int K, int LOGF, bool REG>
 __global__ void __launch_bounds__(THREADS) mergek_kernel(const T *__restrict__ in,
-                                                         T *__restrict__ out, PassDesc pd,
+                                                         T *__restrict__ out, PassDesc pd, int tnom,
                                                          const uint32_t *__restrict__ splits) {
     constexpr int TILE = THREADS * K;
     constexpr int F = 1 << LOGF;
     using V = typename Vec16<T>::type;
     constexpr int VN = Vec16<T>::N;
-    __shared__ __attribute__((aligned(16))) T buf[2 * padded(TILE)];
+    __shared__ __attribute__((aligned(16))) T buf[2 * lds_keys<T>(TILE)];
     __shared__ int soff[F + 1];
     __shared__ uint64_t sstart[F];
+    __shared__ uint64_t s_out;
 
     const int t = threadIdx.x;
     const uint64_t j = blockIdx.x;
     TileInfo ti;
-    const GroupK *g = tile_info<REG>(pd, j, TILE, ti);
+    const GroupK *g = tile_info<REG>(pd, j, tnom, ti);
     if (t < 64) {
         const int i = t & (F - 1);
         uint64_t rs, rl;
         run_range<REG>(pd, ti, g, i, rs, rl);
         const uint32_t s0 = splits[j * F + i];
-        const uint32_t s1 = ti.d1 == ti.gtotal ? (uint32_t)rl : splits[(j + 1) * F + i];
+        const uint32_t s1 = ti.jr + 1 == ti.ntg ? (uint32_t)rl : splits[(j + 1) * F + i];
         const int len = (int)(s1 - s0);
         int incl = len;
+        uint64_t before = s0;  // output offset of the tile = keys of the group below its cut
         for (int o = 1; o < F; o <<= 1) {
             const int v = __shfl_up(incl, o);
             if (i >= o) incl += v;
+            before += __shfl_xor(before, o);
         }
         if (t < F) {
             soff[i + 1] = incl;
             sstart[i] = rs + s0;
-            if (i == 0) soff[0] = 0;
+            if (i == 0) {
+                soff[0] = 0;
+                s_out = ti.base + before;
+            }
         }
     }
     __syncthreads();
     const int total = soff[F];
 
-    T *src = buf, *dst = buf + padded(TILE);
+    T *src = buf, *dst = buf + lds_keys<T>(TILE);
     {
         int seg = 0;
 #pragma unroll
@@ -403,7 +540,7 @@ __global__ void __launch_bounds__(THREADS) mergek_kernel(const T *__restrict__ i
             const int e = k * THREADS + t;
             if (e < total) {
                 while (e >= soff[seg + 1]) ++seg;
-                src[swz(e)] = in[sstart[seg] + (uint64_t)(e - soff[seg])];
+                src[kpos<T>(e)] = in[sstart[seg] + (uint64_t)(e - soff[seg])];
             }
         }
     }
@@ -431,11 +568,11 @@ __global__ void __launch_bounds__(THREADS) mergek_kernel(const T *__restrict__ i
             const int cnt = (end < pe ? end : pe) - pos;
             if (cnt == K) {
 #pragma unroll
-                for (int q = 0; q < K; ++q) dst[swz(pos + q)] = m[q];
+                for (int q = 0; q < 1; ++q) store_lane<T, K>(dst, pos, m);
             } else {
 #pragma unroll
                 for (int q = 0; q < K; ++q)
-                    if (q < cnt) dst[swz(pos + q)] = m[q];
+                    if (q < cnt) dst[kpos<T>(pos + q)] = m[q];
             }
             pos += cnt;
         }
@@ -445,13 +582,18 @@ __global__ void __launch_bounds__(THREADS) mergek_kernel(const T *__restrict__ i
         dst = tmp;
     }
 
-    store_tile<T, THREADS, K>(src, out + ti.base + ti.d0, total);
+    store_tile<T, THREADS, K>(src, out + s_out, total);
 }
 
 // ---------------------------------------------------------------------------------------
 // Host side
 // ---------------------------------------------------------------------------------------
 static inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
+
+// Merge tiles: nominal size TILE - 2*slack, so a cut off by at most `slack` on either side
+// still fits the TILE-key LDS buffer.
+template <typename T> static constexpr int slack_of() { return Geom<T>::TILE / 32; }
+template <typename T> static constexpr int tnom_of() { return Geom<T>::TILE - 2 * slack_of<T>(); }
 
 static int ceil_log2(uint64_t x) {
     int p = 0;
@@ -490,18 +632,18 @@ static int launch_pass(dsort_ctx *ctx, const T *src, T *dst, const PassDesc &pd,
     if (rc) return rc;
     uint32_t *sp = static_cast<uint32_t *>(ctx->splits);
     hipLaunchKernelGGL((partk_kernel<T, REG>), dim3((unsigned)ceil_div(ntiles, 4)), dim3(256), 0, s,
-                       src, pd, TILE, sp, ntiles);
+                       src, pd, tnom_of<T>(), slack_of<T>(), sp, ntiles);
     DSORT_HIP(ctx, hipGetLastError());
     const bool kt = timed && ctx->ev_ok && ctx->kev_used + 2 <= dsort_ctx::kMaxKev;
     if (kt) DSORT_HIP(ctx, hipEventRecord(ctx->kev[ctx->kev_used], s));
     const dim3 grid((unsigned)ntiles), block(THREADS);
     switch (logf) {
-        case 1: hipLaunchKernelGGL((mergek_kernel<T, THREADS, K, 1, REG>), grid, block, 0, s, src, dst, pd, sp); break;
-        case 2: hipLaunchKernelGGL((mergek_kernel<T, THREADS, K, 2, REG>), grid, block, 0, s, src, dst, pd, sp); break;
-        case 3: hipLaunchKernelGGL((mergek_kernel<T, THREADS, K, 3, REG>), grid, block, 0, s, src, dst, pd, sp); break;
-        case 4: hipLaunchKernelGGL((mergek_kernel<T, THREADS, K, 4, REG>), grid, block, 0, s, src, dst, pd, sp); break;
-        case 5: hipLaunchKernelGGL((mergek_kernel<T, THREADS, K, 5, REG>), grid, block, 0, s, src, dst, pd, sp); break;
-        case 6: hipLaunchKernelGGL((mergek_kernel<T, THREADS, K, 6, REG>), grid, block, 0, s, src, dst, pd, sp); break;
+        case 1: hipLaunchKernelGGL((mergek_kernel<T, THREADS, K, 1, REG>), grid, block, 0, s, src, dst, pd, tnom_of<T>(), sp); break;
+        case 2: hipLaunchKernelGGL((mergek_kernel<T, THREADS, K, 2, REG>), grid, block, 0, s, src, dst, pd, tnom_of<T>(), sp); break;
+        case 3: hipLaunchKernelGGL((mergek_kernel<T, THREADS, K, 3, REG>), grid, block, 0, s, src, dst, pd, tnom_of<T>(), sp); break;
+        case 4: hipLaunchKernelGGL((mergek_kernel<T, THREADS, K, 4, REG>), grid, block, 0, s, src, dst, pd, tnom_of<T>(), sp); break;
+        case 5: hipLaunchKernelGGL((mergek_kernel<T, THREADS, K, 5, REG>), grid, block, 0, s, src, dst, pd, tnom_of<T>(), sp); break;
+        case 6: hipLaunchKernelGGL((mergek_kernel<T, THREADS, K, 6, REG>), grid, block, 0, s, src, dst, pd, tnom_of<T>(), sp); break;
         default: return set_err(ctx, DSORT_EINVAL, "bad pass fan-in");
     }
     DSORT_HIP(ctx, hipGetLastError());
@@ -555,7 +697,11 @@ int sort_device(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipStream_t 
     uint64_t R = TILE;
     for (int p = 0; p < passes; ++p) {
         PassDesc pd{(uint64_t)n, R, 1 << plan[p], 0, nullptr};
-        int rc = launch_pass<T, THREADS, K, true>(ctx, bufs[cur], bufs[cur ^ 1], pd, plan[p], tiles, s,
+        const uint64_t gsize = R << plan[p];
+        const uint64_t ngroups = ceil_div(n, gsize);
+        const uint64_t tpg = ceil_div(gsize, tnom_of<T>());
+        const uint64_t mtiles = (ngroups - 1) * tpg + ceil_div(n - (ngroups - 1) * gsize, tnom_of<T>());
+        int rc = launch_pass<T, THREADS, K, true>(ctx, bufs[cur], bufs[cur ^ 1], pd, plan[p], mtiles, s,
                                                   timed);
         if (rc) return rc;
         R <<= plan[p];
@@ -636,7 +782,7 @@ int merge_device(dsort_ctx *ctx, const T *d_in, const size_t *lens, int k, T *d_
             }
             for (int r = (int)gk.nruns + 1; r <= kMaxF; ++r) gk.roff[r] = tot;
             gk.total = tot;
-            tiles += ceil_div(tot, TILE);
+            tiles += ceil_div(tot, tnom_of<T>());
             base += tot;
             next.push_back(tot);
         }
