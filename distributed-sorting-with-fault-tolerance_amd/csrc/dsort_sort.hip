@@ -33,6 +33,10 @@
 
 #include "dsort_internal.h"
 
+#ifndef DSORT_MERGEK_MINW
+#define DSORT_MERGEK_MINW 6  // waves per SIMD the merge kernel is compiled for (3 workgroups / CU)
+#endif
+
 namespace dsort {
 
 template <typename T> __host__ __device__ constexpr T key_max();
@@ -78,23 +82,26 @@ __device__ __forceinline__ void sort_regs(T (&v)[K]) {
     }
 }
 
-// LDS layout.  Keys are grouped in 16-byte chunks (4 int32 / 2 int64); chunk c is stored at
-// slot c ^ ((c >> 3) & 3).  Within a 128-byte row of 8 chunks this XOR gives the 8 lanes of a
-// ds_write_b128 lane group distinct slots when each lane writes its own K keys (chunks 4t..),
-// and keeps every chunk 16-byte contiguous, so windows and outputs move as ds_read_b128 /
-// ds_write_b128 (CDNA4 LDS: 256 B/clk for b128 vs 128 B/clk for b32).
+// LDS layout.  Keys are grouped in 16-byte chunks (4 int32 / 2 int64) and every 8th chunk slot
+// is left empty: chunk c lives at slot c + c/8.  A lane writing its K keys (chunks
+// K/KPC*t ...) then lands in a distinct 16-byte slot of its ds_write_b128 lane group, every
+// chunk stays 16-byte contiguous (windows and outputs move as ds_read_b128 / ds_write_b128),
+// and the address of a key costs three VALU ops.
 template <typename T> struct Chunk;
 template <> struct Chunk<int32_t> { using V = int4; static constexpr int KPC = 4, SH = 2; };
 template <> struct Chunk<int64_t> { using V = longlong2; static constexpr int KPC = 2, SH = 1; };
 
-__device__ __forceinline__ int cslot(int c) { return c ^ ((c >> 3) & 3); }
+__device__ __forceinline__ int cslot(int c) { return c + (c >> 3); }
 template <typename T>
 __device__ __forceinline__ int kpos(int p) {  // LDS word (key) index of key position p
     constexpr int SH = Chunk<T>::SH;
-    return (cslot(p >> SH) << SH) | (p & ((1 << SH) - 1));
+    return p + ((p >> (SH + 3)) << SH);
 }
-// LDS keys to allocate for a tile of n keys: window reads run up to 6 chunks past the end.
-template <typename T> __host__ __device__ constexpr int lds_keys(int n) { return n + 8 * Chunk<T>::KPC; }
+// LDS keys to allocate for a tile of n keys (n a multiple of 8 chunks): the pad slots plus the
+// window over-read (up to 2 chunks past the end).
+template <typename T> __host__ __device__ constexpr int lds_keys(int n) {
+    return n + n / 8 + 4 * Chunk<T>::KPC;
+}
 
 // Merge-path split on LDS: number of A keys among the first `diag` outputs of merge(A, B),
 // A first on ties.  A = positions [A0, A0+na), B = [B0, B0+nb).
@@ -486,21 +493,24 @@ __global__ void __launch_bounds__(256) partk_kernel(const T *__restrict__ in, Pa
 }
 
 // ---------------------------------------------------------------------------------------
-// 2b. Merge one output tile of a k-way pass: stage the F input windows in LDS, then log2(F)
-//     pairwise merge levels (double-buffered LDS), then coalesced stores.
+// 2b. Merge one output tile of a k-way pass.  The F input windows are staged in LDS, each padded
+//     with key_max up to a multiple of K (the last one up to TILE), so every pair boundary of
+//     every level is K-aligned: each lane's K outputs come from one pair, and a level is
+//     merge path + bitonic window merge in registers, barrier, in-place store, barrier (one
+//     TILE-key LDS buffer: 4 workgroups per CU).  Only the first `total` (real) keys leave.
 // ---------------------------------------------------------------------------------------
 template <typename T, int THREADS, int K, int LOGF, bool REG>
-__global__ void __launch_bounds__(THREADS) mergek_kernel(const T *__restrict__ in,
+__global__ void __launch_bounds__(THREADS, DSORT_MERGEK_MINW) mergek_kernel(const T *__restrict__ in,
                                                          T *__restrict__ out, PassDesc pd, int tnom,
                                                          const uint32_t *__restrict__ splits) {
     constexpr int TILE = THREADS * K;
     constexpr int F = 1 << LOGF;
-    using V = typename Vec16<T>::type;
-    constexpr int VN = Vec16<T>::N;
-    __shared__ __attribute__((aligned(16))) T buf[2 * lds_keys<T>(TILE)];
-    __shared__ int soff[F + 1];
+    __shared__ __attribute__((aligned(16))) T s[lds_keys<T>(TILE)];
+    __shared__ int soff[F + 1];  // padded segment offsets, soff[F] = TILE
+    __shared__ int slen[F];
     __shared__ uint64_t sstart[F];
     __shared__ uint64_t s_out;
+    __shared__ int s_total;
 
     const int t = threadIdx.x;
     const uint64_t j = blockIdx.x;
@@ -513,76 +523,67 @@ __global__ void __launch_bounds__(THREADS) mergek_kernel(const T *__restrict__ i
         const uint32_t s0 = splits[j * F + i];
         const uint32_t s1 = ti.jr + 1 == ti.ntg ? (uint32_t)rl : splits[(j + 1) * F + i];
         const int len = (int)(s1 - s0);
-        int incl = len;
+        const int plen = (len + K - 1) & ~(K - 1);
+        int incl = plen, real = len;
         uint64_t before = s0;  // output offset of the tile = keys of the group below its cut
         for (int o = 1; o < F; o <<= 1) {
             const int v = __shfl_up(incl, o);
             if (i >= o) incl += v;
+            real += __shfl_xor(real, o);
             before += __shfl_xor(before, o);
         }
         if (t < F) {
-            soff[i + 1] = incl;
+            soff[i + 1] = i == F - 1 ? TILE : incl;
+            slen[i] = len;
             sstart[i] = rs + s0;
             if (i == 0) {
                 soff[0] = 0;
                 s_out = ti.base + before;
+                s_total = real;
             }
         }
     }
     __syncthreads();
-    const int total = soff[F];
+    const int total = s_total;
 
-    T *src = buf, *dst = buf + lds_keys<T>(TILE);
     {
         int seg = 0;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const int e = k * THREADS + t;
-            if (e < total) {
-                while (e >= soff[seg + 1]) ++seg;
-                src[kpos<T>(e)] = in[sstart[seg] + (uint64_t)(e - soff[seg])];
-            }
+            while (seg < F - 1 && e >= soff[seg + 1]) ++seg;
+            const int r = e - soff[seg];
+            const bool real_key = r < slen[seg];
+            // padding slots load a key that surely exists (the group's first) and discard it
+            const T v = in[real_key ? sstart[seg] + (uint64_t)r : ti.base];
+            s[kpos<T>(e)] = real_key ? v : key_max<T>();
         }
     }
     __syncthreads();
 
+    const int pos = t * K;
 #pragma unroll 1
     for (int l = 0; l < LOGF; ++l) {
-        int pos = t * K;
-        const int end = pos + K < total ? pos + K : total;
         const int npairs = F >> (l + 1);
-        while (pos < end) {
-            int lo = 0, hi = npairs - 1;  // first pair whose end lies beyond pos
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (soff[(2 * mid + 2) << l] > pos) hi = mid;
-                else lo = mid + 1;
-            }
-            const int ps = soff[(2 * lo) << l];
-            const int pm = soff[(2 * lo + 1) << l];
-            const int pe = soff[(2 * lo + 2) << l];
-            const int na = pm - ps, nb = pe - pm, diag = pos - ps;
-            const int a = lds_merge_path(src, ps, na, pm, nb, diag);
-            T m[K];
-            kmerge<T, K>(src, ps, na, pm, nb, a, diag - a, m);
-            const int cnt = (end < pe ? end : pe) - pos;
-            if (cnt == K) {
-#pragma unroll
-                for (int q = 0; q < 1; ++q) store_lane<T, K>(dst, pos, m);
-            } else {
-#pragma unroll
-                for (int q = 0; q < K; ++q)
-                    if (q < cnt) dst[kpos<T>(pos + q)] = m[q];
-            }
-            pos += cnt;
+        int lo = 0, hi = npairs - 1;  // the pair holding pos
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (soff[(2 * mid + 2) << l] > pos) hi = mid;
+            else lo = mid + 1;
         }
+        const int ps = soff[(2 * lo) << l];
+        const int pm = soff[(2 * lo + 1) << l];
+        const int pe = soff[(2 * lo + 2) << l];
+        const int na = pm - ps, nb = pe - pm, diag = pos - ps;
+        const int a = lds_merge_path(s, ps, na, pm, nb, diag);
+        T m[K];
+        kmerge<T, K>(s, ps, na, pm, nb, a, diag - a, m);
         __syncthreads();
-        T *tmp = src;
-        src = dst;
-        dst = tmp;
+        store_lane<T, K>(s, pos, m);
+        __syncthreads();
     }
 
-    store_tile<T, THREADS, K>(src, out + s_out, total);
+    store_tile<T, THREADS, K>(s, out + s_out, total);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -590,10 +591,12 @@ __global__ void __launch_bounds__(THREADS) mergek_kernel(const T *__restrict__ i
 // ---------------------------------------------------------------------------------------
 static inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 
-// Merge tiles: nominal size TILE - 2*slack, so a cut off by at most `slack` on either side
-// still fits the TILE-key LDS buffer.
+// Merge tiles: nominal size TILE - 2*slack - F*(K-1), so a cut off by at most `slack` on either
+// side, with every staged run padded to a multiple of K, still fits the TILE-key LDS buffer.
 template <typename T> static constexpr int slack_of() { return Geom<T>::TILE / 32; }
-template <typename T> static constexpr int tnom_of() { return Geom<T>::TILE - 2 * slack_of<T>(); }
+template <typename T> static int tnom_of(int logf) {
+    return Geom<T>::TILE - 2 * slack_of<T>() - (1 << logf) * (Geom<T>::K - 1);
+}
 
 static int ceil_log2(uint64_t x) {
     int p = 0;
@@ -632,18 +635,18 @@ static int launch_pass(dsort_ctx *ctx, const T *src, T *dst, const PassDesc &pd,
     if (rc) return rc;
     uint32_t *sp = static_cast<uint32_t *>(ctx->splits);
     hipLaunchKernelGGL((partk_kernel<T, REG>), dim3((unsigned)ceil_div(ntiles, 4)), dim3(256), 0, s,
-                       src, pd, tnom_of<T>(), slack_of<T>(), sp, ntiles);
+                       src, pd, tnom_of<T>(logf), slack_of<T>(), sp, ntiles);
     DSORT_HIP(ctx, hipGetLastError());
     const bool kt = timed && ctx->ev_ok && ctx->kev_used + 2 <= dsort_ctx::kMaxKev;
     if (kt) DSORT_HIP(ctx, hipEventRecord(ctx->kev[ctx->kev_used], s));
     const dim3 grid((unsigned)ntiles), block(THREADS);
     switch (logf) {
-        case 1: hipLaunchKernelGGL((mergek_kernel<T, THREADS, K, 1, REG>), grid, block, 0, s, src, dst, pd, tnom_of<T>(), sp); break;
-        case 2: hipLaunchKernelGGL((mergek_kernel<T, THREADS, K, 2, REG>), grid, block, 0, s, src, dst, pd, tnom_of<T>(), sp); break;
-        case 3: hipLaunchKernelGGL((mergek_kernel<T, THREADS, K, 3, REG>), grid, block, 0, s, src, dst, pd, tnom_of<T>(), sp); break;
-        case 4: hipLaunchKernelGGL((mergek_kernel<T, THREADS, K, 4, REG>), grid, block, 0, s, src, dst, pd, tnom_of<T>(), sp); break;
-        case 5: hipLaunchKernelGGL((mergek_kernel<T, THREADS, K, 5, REG>), grid, block, 0, s, src, dst, pd, tnom_of<T>(), sp); break;
-        case 6: hipLaunchKernelGGL((mergek_kernel<T, THREADS, K, 6, REG>), grid, block, 0, s, src, dst, pd, tnom_of<T>(), sp); break;
+        case 1: hipLaunchKernelGGL((mergek_kernel<T, THREADS, K, 1, REG>), grid, block, 0, s, src, dst, pd, tnom_of<T>(logf), sp); break;
+        case 2: hipLaunchKernelGGL((mergek_kernel<T, THREADS, K, 2, REG>), grid, block, 0, s, src, dst, pd, tnom_of<T>(logf), sp); break;
+        case 3: hipLaunchKernelGGL((mergek_kernel<T, THREADS, K, 3, REG>), grid, block, 0, s, src, dst, pd, tnom_of<T>(logf), sp); break;
+        case 4: hipLaunchKernelGGL((mergek_kernel<T, THREADS, K, 4, REG>), grid, block, 0, s, src, dst, pd, tnom_of<T>(logf), sp); break;
+        case 5: hipLaunchKernelGGL((mergek_kernel<T, THREADS, K, 5, REG>), grid, block, 0, s, src, dst, pd, tnom_of<T>(logf), sp); break;
+        case 6: hipLaunchKernelGGL((mergek_kernel<T, THREADS, K, 6, REG>), grid, block, 0, s, src, dst, pd, tnom_of<T>(logf), sp); break;
         default: return set_err(ctx, DSORT_EINVAL, "bad pass fan-in");
     }
     DSORT_HIP(ctx, hipGetLastError());
@@ -699,8 +702,9 @@ int sort_device(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipStream_t 
         PassDesc pd{(uint64_t)n, R, 1 << plan[p], 0, nullptr};
         const uint64_t gsize = R << plan[p];
         const uint64_t ngroups = ceil_div(n, gsize);
-        const uint64_t tpg = ceil_div(gsize, tnom_of<T>());
-        const uint64_t mtiles = (ngroups - 1) * tpg + ceil_div(n - (ngroups - 1) * gsize, tnom_of<T>());
+        const uint64_t tn = (uint64_t)tnom_of<T>(plan[p]);
+        const uint64_t tpg = ceil_div(gsize, tn);
+        const uint64_t mtiles = (ngroups - 1) * tpg + ceil_div(n - (ngroups - 1) * gsize, tn);
         int rc = launch_pass<T, THREADS, K, true>(ctx, bufs[cur], bufs[cur ^ 1], pd, plan[p], mtiles, s,
                                                   timed);
         if (rc) return rc;
@@ -782,7 +786,7 @@ int merge_device(dsort_ctx *ctx, const T *d_in, const size_t *lens, int k, T *d_
             }
             for (int r = (int)gk.nruns + 1; r <= kMaxF; ++r) gk.roff[r] = tot;
             gk.total = tot;
-            tiles += ceil_div(tot, tnom_of<T>());
+            tiles += ceil_div(tot, (uint64_t)tnom_of<T>(logf));
             base += tot;
             next.push_back(tot);
         }
