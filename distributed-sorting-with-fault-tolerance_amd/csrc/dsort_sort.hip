@@ -511,6 +511,8 @@ __global__ void __launch_bounds__(THREADS, DSORT_MERGEK_MINW) mergek_kernel(cons
     __shared__ uint64_t sstart[F];
     __shared__ uint64_t s_out;
     __shared__ int s_total;
+    __shared__ uint64_t ubase[THREADS];  // per K-key unit: first source key, real keys in it
+    __shared__ int uvalid[THREADS];
 
     const int t = threadIdx.x;
     const uint64_t j = blockIdx.x;
@@ -546,18 +548,31 @@ __global__ void __launch_bounds__(THREADS, DSORT_MERGEK_MINW) mergek_kernel(cons
     __syncthreads();
     const int total = s_total;
 
+    // Staging.  Every K-key unit of the padded tile lies in one segment: thread t resolves unit t
+    // (its source address and how many of its K slots hold real keys) once; then all K loads of
+    // every thread are issued back to back, lane-consecutive (coalesced), with no branches.
     {
-        int seg = 0;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const int e = k * THREADS + t;
-            while (seg < F - 1 && e >= soff[seg + 1]) ++seg;
-            const int r = e - soff[seg];
-            const bool real_key = r < slen[seg];
-            // padding slots load a key that surely exists (the group's first) and discard it
-            const T v = in[real_key ? sstart[seg] + (uint64_t)r : ti.base];
-            s[kpos<T>(e)] = real_key ? v : key_max<T>();
+        const int pos = t * K;
+        int lo = 0, hi = F - 1;  // last segment starting at or before pos
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (soff[mid] <= pos) lo = mid;
+            else hi = mid - 1;
         }
+        const int r = pos - soff[lo];
+        int valid = slen[lo] - r;
+        valid = valid < 0 ? 0 : (valid > K ? K : valid);
+        ubase[t] = valid > 0 ? sstart[lo] + (uint64_t)r : ti.base;  // ti.base: a key that exists
+        uvalid[t] = valid;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int e = k * THREADS + t;
+        const int u = e / K, q = e & (K - 1);
+        const bool real_key = q < uvalid[u];
+        const T v = in[ubase[u] + (uint64_t)(real_key ? q : 0)];
+        s[kpos<T>(e)] = real_key ? v : key_max<T>();
     }
     __syncthreads();
 
