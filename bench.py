@@ -176,6 +176,8 @@ def run_single(args):
 
 
 def run_multi(args):
+    """One rank per GPU (torch.distributed.run): gloo for control, RCCL (inside libdsort) for
+    the key exchange.  Strong scaling: the 2^30 keys are split into equal contiguous chunks."""
     import torch.distributed as dist
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
@@ -187,44 +189,39 @@ def run_multi(args):
     dist.broadcast_object_list(uid, src=0)
     ctx.comm_init(world, rank, uid[0])
     n = args.keys
-    sz = n // world + (1 if rank < n % world else 0)
+    sz = n // world + (1 if rank < n % world else 0)          # server.c:185-216 partition rule
     first = rank * (n // world) + min(rank, n % world)
     t_in = make_input(ctx, sz, first, args.dtype, args.dist)
     w = 4 if args.dtype == "i32" else 8
+    in_fp = ctx.fingerprint(t_in)
     for _ in range(max(args.warmup, 1)):
         ptr, nout = ctx.sample_sort_dev(t_in)
-    torch.cuda.synchronize()
+    ctx.synchronize()
     # verification outside the timed region: local order, global multiset, rank boundaries
-    out_view = torch.empty(max(nout, 1), dtype=t_in.dtype, device="cuda")
-    ctx.lib.dsort_copy_d2h  # noqa: B018  (binding loaded)
-    import ctypes as _c
-    _c.memmove  # noqa: B018
-    desc = ctx.lib.dsort_count_descents_i32 if args.dtype == "i32" else ctx.lib.dsort_count_descents_i64
-    c = dsort.U64()
-    ctx.check(desc(ctx.h, ptr, nout, _c.byref(c)))
-    fs, fx = dsort.U64(), dsort.U64()
-    fpf = ctx.lib.dsort_fingerprint_i32 if args.dtype == "i32" else ctx.lib.dsort_fingerprint_i64
-    ctx.check(fpf(ctx.h, ptr, nout, _c.byref(fs), _c.byref(fx)))
-    in_fp = ctx.fingerprint(t_in)
+    sfx = args.dtype
+    c, fs, fx = dsort.U64(), dsort.U64(), dsort.U64()
+    ctx.check(getattr(ctx.lib, f"dsort_count_descents_{sfx}")(ctx.h, ptr, nout, ctypes.byref(c)))
+    ctx.check(getattr(ctx.lib, f"dsort_fingerprint_{sfx}")(ctx.h, ptr, nout, ctypes.byref(fs), ctypes.byref(fx)))
     ends = np.zeros(2, np.int64)
     if nout:
-        hb = np.zeros(1, np.int64 if args.dtype == "i64" else np.int32)
+        hb = np.zeros(1, np.int64 if sfx == "i64" else np.int32)
         ctx.copy_d2h(hb, ptr, hb.itemsize)
         ends[0] = hb[0]
         ctx.copy_d2h(hb, ptr + (nout - 1) * hb.itemsize, hb.itemsize)
         ends[1] = hb[0]
-    info = torch.tensor([c.value, fs.value & 0x7FFFFFFFFFFFFFFF, nout, in_fp[0] & 0x7FFFFFFFFFFFFFFF,
-                         ends[0], ends[1]], dtype=torch.int64)
+    M = 0xFFFFFFFFFFFFFFFF
+    info = torch.tensor([c.value, nout, ends[0], ends[1]], dtype=torch.int64)
     allinfo = [torch.zeros_like(info) for _ in range(world)]
     dist.all_gather(allinfo, info)
-    del out_view
+    fps = [None] * world
+    dist.all_gather_object(fps, (in_fp[0], in_fp[1], fs.value, fx.value))
     torch.cuda.synchronize()
     dist.barrier()
     t0 = time.perf_counter()
     ex, fm = 0.0, 0.0
     for _ in range(args.steps):
         ptr, nout = ctx.sample_sort_dev(t_in)
-        st = ctx.stats()
+        st = ctx.stats()  # synchronizes this rank's stream
         ex += st["exchange_ms"]
         fm += st["final_merge_ms"]
     torch.cuda.synchronize()
@@ -233,12 +230,16 @@ def run_multi(args):
     el = torch.tensor([t1 - t0], dtype=torch.float64)
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
     A = torch.stack(allinfo)
-    ok = bool((A[:, 0] == 0).all())
-    ok &= int(A[:, 2].sum()) == n
-    ok &= (int(A[:, 1].sum()) & 0x7FFFFFFFFFFFFFFF) == (int(A[:, 3].sum()) & 0x7FFFFFFFFFFFFFFF)
+    ok = bool((A[:, 0] == 0).all()) and int(A[:, 1].sum()) == n
+    ok &= sum(f[0] for f in fps) & M == sum(f[2] for f in fps) & M
+    x_in = x_out = 0
+    for f in fps:
+        x_in ^= f[1]
+        x_out ^= f[3]
+    ok &= x_in == x_out
     for r in range(world - 1):
-        if A[r, 2] > 0 and A[r + 1, 2] > 0:
-            ok &= bool(A[r, 5] <= A[r + 1, 4])
+        if A[r, 1] > 0 and A[r + 1, 1] > 0:
+            ok &= bool(A[r, 3] <= A[r + 1, 2])
     ctx.comm_destroy()
     ctx.close()
     return rank, world, float(el.item()), ok, {"exchange_ms": ex, "final_merge_ms": fm, "w": w,

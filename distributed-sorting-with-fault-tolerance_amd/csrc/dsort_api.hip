@@ -331,18 +331,35 @@ template <> ncclDataType_t nccl_type<int64_t>() { return ncclInt64; }
 
 template <typename T>
 static int sample_sort(dsort_ctx *ctx, const T *d_in, size_t n_local, T **d_out, size_t *n_out,
-                       void *stream) {
+                       void *stream, bool presorted) {
     if (!ctx || !d_out || !n_out || (n_local && !d_in)) return set_err(ctx, DSORT_EINVAL, "null argument");
     if (!ctx->comm) return set_err(ctx, DSORT_ECOMM, "communicator not initialised (dsort_comm_init)");
     hipStream_t s = pick(ctx, stream);
     const int P = ctx->nranks, me = ctx->rank, S = kSamplesPerRank;
-    // 1. local sort (the worker's merge_sort) into the context's local arena
-    int rc = ensure(ctx, &ctx->local, &ctx->local_bytes, (n_local ? n_local : 1) * sizeof(T), "local run");
-    if (rc) return rc;
-    T *d_keys = static_cast<T *>(ctx->local);
-    rc = sort_device<T>(ctx, d_in, d_keys, n_local, s, true);
-    if (rc) return rc;
-    dsort_stats st = ctx->stats;
+    int rc;
+    const T *d_keys;
+    dsort_stats st{};
+    if (presorted) {
+        // the caller already holds a sorted local run (fault recovery: a survivor merged the
+        // chunks it sorted)
+        d_keys = d_in;
+        ctx->ev_mask = 0;
+        ctx->last_stream = s;
+        if (ctx->ev_ok) {
+            for (int e = 0; e < 3; ++e) DSORT_HIP(ctx, hipEventRecord(ctx->ev[e], s));
+            ctx->ev_mask = 7u;
+        }
+        st.keys_in = n_local;
+    } else {
+        // 1. local sort (the worker's merge_sort) into the context's local arena
+        rc = ensure(ctx, &ctx->local, &ctx->local_bytes, (n_local ? n_local : 1) * sizeof(T), "local run");
+        if (rc) return rc;
+        T *dk = static_cast<T *>(ctx->local);
+        rc = sort_device<T>(ctx, d_in, dk, n_local, s, true);
+        if (rc) return rc;
+        d_keys = dk;
+        st = ctx->stats;
+    }
     // device small-area layout
     const size_t off_samp = 0;                                   // S keys
     const size_t off_all = off_samp + (size_t)S * sizeof(T);      // P*S keys
@@ -642,10 +659,16 @@ int dsort_comm_destroy(dsort_ctx *ctx) {
 }
 
 int dsort_sample_sort_dev_i32(dsort_ctx *ctx, const int32_t *d, size_t n, int32_t **o, size_t *no, void *st) {
-    return sample_sort<int32_t>(ctx, d, n, o, no, st);
+    return sample_sort<int32_t>(ctx, d, n, o, no, st, false);
 }
 int dsort_sample_sort_dev_i64(dsort_ctx *ctx, const int64_t *d, size_t n, int64_t **o, size_t *no, void *st) {
-    return sample_sort<int64_t>(ctx, d, n, o, no, st);
+    return sample_sort<int64_t>(ctx, d, n, o, no, st, false);
+}
+int dsort_sample_merge_dev_i32(dsort_ctx *ctx, const int32_t *d, size_t n, int32_t **o, size_t *no, void *st) {
+    return sample_sort<int32_t>(ctx, d, n, o, no, st, true);
+}
+int dsort_sample_merge_dev_i64(dsort_ctx *ctx, const int64_t *d, size_t n, int64_t **o, size_t *no, void *st) {
+    return sample_sort<int64_t>(ctx, d, n, o, no, st, true);
 }
 
 int dsort_plan_sample_positions(size_t n, int s, uint64_t *idx) {

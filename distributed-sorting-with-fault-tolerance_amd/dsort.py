@@ -29,7 +29,8 @@ EXPORTS = [
     "dsort_sort_dev_i64", "dsort_sort_dev_copy_i32", "dsort_sort_dev_copy_i64",
     "dsort_merge_i32", "dsort_merge_i64", "dsort_merge_dev_i32", "dsort_merge_dev_i64",
     "dsort_comm_unique_id", "dsort_comm_init", "dsort_comm_abort", "dsort_comm_destroy",
-    "dsort_sample_sort_dev_i32", "dsort_sample_sort_dev_i64", "dsort_plan_splitters_i32",
+    "dsort_sample_sort_dev_i32", "dsort_sample_sort_dev_i64", "dsort_sample_merge_dev_i32",
+    "dsort_sample_merge_dev_i64", "dsort_plan_splitters_i32",
     "dsort_plan_splitters_i64", "dsort_plan_cuts_i32", "dsort_plan_cuts_i64",
     "dsort_plan_sample_positions", "dsort_gen_uniform_i32", "dsort_gen_uniform_i64",
     "dsort_gen_zipf_i64", "dsort_fingerprint_i32", "dsort_fingerprint_i64",
@@ -92,6 +93,8 @@ def load():
         "dsort_comm_destroy": (ctypes.c_int, [P]),
         "dsort_sample_sort_dev_i32": (ctypes.c_int, [P, P, SZ, ctypes.POINTER(P), ctypes.POINTER(SZ), P]),
         "dsort_sample_sort_dev_i64": (ctypes.c_int, [P, P, SZ, ctypes.POINTER(P), ctypes.POINTER(SZ), P]),
+        "dsort_sample_merge_dev_i32": (ctypes.c_int, [P, P, SZ, ctypes.POINTER(P), ctypes.POINTER(SZ), P]),
+        "dsort_sample_merge_dev_i64": (ctypes.c_int, [P, P, SZ, ctypes.POINTER(P), ctypes.POINTER(SZ), P]),
         "dsort_plan_splitters_i32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, P, P, P, P, P]),
         "dsort_plan_splitters_i64": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, P, P, P, P, P]),
         "dsort_plan_cuts_i32": (ctypes.c_int, [P, SZ, ctypes.c_int, ctypes.c_int, P, P, P, P]),

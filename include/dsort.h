@@ -131,6 +131,13 @@ int dsort_sample_sort_dev_i32(dsort_ctx *ctx, const int32_t *d_keys, size_t n_lo
                               int32_t **d_out, size_t *n_out, void *stream);
 int dsort_sample_sort_dev_i64(dsort_ctx *ctx, const int64_t *d_keys, size_t n_local,
                               int64_t **d_out, size_t *n_out, void *stream);
+/* The exchange half alone: `d_sorted` is this rank's already sorted local run (e.g. a fault
+ * survivor that sorted its own chunk and a dead rank's chunk, then merged them).  Same output
+ * contract as dsort_sample_sort_dev_*. */
+int dsort_sample_merge_dev_i32(dsort_ctx *ctx, const int32_t *d_sorted, size_t n_local,
+                               int32_t **d_out, size_t *n_out, void *stream);
+int dsort_sample_merge_dev_i64(dsort_ctx *ctx, const int64_t *d_sorted, size_t n_local,
+                               int64_t **d_out, size_t *n_out, void *stream);
 
 /* ---------------------------------------------------------------- sample-sort planning  */
 /* Host-side planning rules of the sample sort, exported so that the CPU tests (gloo, no GPU)
