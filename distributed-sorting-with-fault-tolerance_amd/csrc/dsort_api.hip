@@ -54,6 +54,20 @@ int ensure(dsort_ctx *ctx, void **buf, size_t *have, size_t need, const char *wh
     return DSORT_OK;
 }
 
+// grow-only pinned host buffer
+static int ensure_host(dsort_ctx *ctx, void **buf, size_t *have, size_t need) {
+    if (need <= *have && *buf) return DSORT_OK;
+    if (*buf) (void)hipHostFree(*buf);
+    *buf = nullptr;
+    *have = 0;
+    if (hipHostMalloc(buf, need, hipHostMallocDefault) != hipSuccess) {
+        *buf = nullptr;
+        return set_err(ctx, DSORT_ENOMEM, "hipHostMalloc failed (" + std::to_string(need) + " bytes)");
+    }
+    *have = need;
+    return DSORT_OK;
+}
+
 static hipStream_t pick(dsort_ctx *ctx, void *stream) {
     if (stream == DSORT_NULL_STREAM) return static_cast<hipStream_t>(nullptr);
     return stream ? static_cast<hipStream_t>(stream) : ctx->stream;
@@ -333,9 +347,11 @@ template <typename T>
 static int sample_sort(dsort_ctx *ctx, const T *d_in, size_t n_local, T **d_out, size_t *n_out,
                        void *stream, bool presorted) {
     if (!ctx || !d_out || !n_out || (n_local && !d_in)) return set_err(ctx, DSORT_EINVAL, "null argument");
-    if (!ctx->comm) return set_err(ctx, DSORT_ECOMM, "communicator not initialised (dsort_comm_init)");
+    if (!ctx->comm && !ctx->has_transport)
+        return set_err(ctx, DSORT_ECOMM, "communicator not initialised (dsort_comm_init)");
     hipStream_t s = pick(ctx, stream);
     const int P = ctx->nranks, me = ctx->rank, S = kSamplesPerRank;
+    const bool host_tx = ctx->has_transport;
     int rc;
     const T *d_keys;
     dsort_stats st{};
@@ -389,13 +405,30 @@ static int sample_sort(dsort_ctx *ctx, const T *d_in, size_t n_local, T **d_out,
     uint64_t nl = n_local;
     DSORT_HIP(ctx, hipMemcpyAsync(dsm + off_cnt, &nl, 8, hipMemcpyHostToDevice, s));
     // 3. all-gather samples and sizes
-    DSORT_NCCL(ctx, ncclGroupStart());
-    DSORT_NCCL(ctx, ncclAllGather(dsm + off_samp, dsm + off_all, (size_t)S, nccl_type<T>(), ctx->comm, s));
-    DSORT_NCCL(ctx, ncclAllGather(dsm + off_cnt, dsm + off_n, 1, ncclUint64, ctx->comm, s));
-    DSORT_NCCL(ctx, ncclGroupEnd());
-    DSORT_HIP(ctx, hipMemcpyAsync(hsm + off_all, dsm + off_all, (size_t)P * S * sizeof(T) + (size_t)P * 8,
-                                  hipMemcpyDeviceToHost, s));
-    DSORT_HIP(ctx, hipStreamSynchronize(s));
+    if (!host_tx) {
+        DSORT_NCCL(ctx, ncclGroupStart());
+        DSORT_NCCL(ctx, ncclAllGather(dsm + off_samp, dsm + off_all, (size_t)S, nccl_type<T>(), ctx->comm, s));
+        DSORT_NCCL(ctx, ncclAllGather(dsm + off_cnt, dsm + off_n, 1, ncclUint64, ctx->comm, s));
+        DSORT_NCCL(ctx, ncclGroupEnd());
+        DSORT_HIP(ctx, hipMemcpyAsync(hsm + off_all, dsm + off_all, (size_t)P * S * sizeof(T) + (size_t)P * 8,
+                                      hipMemcpyDeviceToHost, s));
+        DSORT_HIP(ctx, hipStreamSynchronize(s));
+    } else {
+        // [S samples | n_local] per rank through the caller's all-gather
+        const size_t rec = (size_t)S * sizeof(T) + 8;
+        rc = ensure_host(ctx, &ctx->xfer, &ctx->xfer_bytes, rec * (size_t)(P + 1));
+        if (rc) return rc;
+        char *mine = static_cast<char *>(ctx->xfer), *all = mine + rec;
+        DSORT_HIP(ctx, hipMemcpyAsync(mine, dsm + off_samp, (size_t)S * sizeof(T), hipMemcpyDeviceToHost, s));
+        DSORT_HIP(ctx, hipStreamSynchronize(s));
+        memcpy(mine + (size_t)S * sizeof(T), &nl, 8);
+        if (ctx->transport.allgather(ctx->transport.user, mine, all, rec))
+            return set_err(ctx, DSORT_ECOMM, "host transport allgather (samples) failed");
+        for (int r = 0; r < P; ++r) {
+            memcpy(hsm + off_all + (size_t)r * S * sizeof(T), all + (size_t)r * rec, (size_t)S * sizeof(T));
+            memcpy(hsm + off_n + (size_t)r * 8, all + (size_t)r * rec + (size_t)S * sizeof(T), 8);
+        }
+    }
     // 4. splitters on the host (tiny: P*S composites)
     {
         const T *hs = reinterpret_cast<const T *>(hsm + off_all);
@@ -421,11 +454,15 @@ static int sample_sort(dsort_ctx *ctx, const T *d_in, size_t n_local, T **d_out,
     const uint64_t *hcut = reinterpret_cast<const uint64_t *>(hsm + off_cut);
     uint64_t *hcnt = reinterpret_cast<uint64_t *>(hsm + off_cnt);
     for (int r = 0; r < P; ++r) hcnt[r] = hcut[r + 1] - hcut[r];
-    DSORT_HIP(ctx, hipMemcpyAsync(dsm + off_cnt, hcnt, (size_t)P * 8, hipMemcpyHostToDevice, s));
     // 6. count matrix
-    DSORT_NCCL(ctx, ncclAllGather(dsm + off_cnt, dsm + off_mat, (size_t)P, ncclUint64, ctx->comm, s));
-    DSORT_HIP(ctx, hipMemcpyAsync(hsm + off_mat, dsm + off_mat, (size_t)P * P * 8, hipMemcpyDeviceToHost, s));
-    DSORT_HIP(ctx, hipStreamSynchronize(s));
+    if (!host_tx) {
+        DSORT_HIP(ctx, hipMemcpyAsync(dsm + off_cnt, hcnt, (size_t)P * 8, hipMemcpyHostToDevice, s));
+        DSORT_NCCL(ctx, ncclAllGather(dsm + off_cnt, dsm + off_mat, (size_t)P, ncclUint64, ctx->comm, s));
+        DSORT_HIP(ctx, hipMemcpyAsync(hsm + off_mat, dsm + off_mat, (size_t)P * P * 8, hipMemcpyDeviceToHost, s));
+        DSORT_HIP(ctx, hipStreamSynchronize(s));
+    } else if (ctx->transport.allgather(ctx->transport.user, hcnt, hsm + off_mat, (size_t)P * 8)) {
+        return set_err(ctx, DSORT_ECOMM, "host transport allgather (counts) failed");
+    }
     const uint64_t *mat = reinterpret_cast<const uint64_t *>(hsm + off_mat);  // mat[src*P + dst]
     std::vector<size_t> rlen(P);
     std::vector<uint64_t> roff(P + 1, 0);
@@ -440,16 +477,38 @@ static int sample_sort(dsort_ctx *ctx, const T *d_in, size_t n_local, T **d_out,
     if (rc) return rc;
     T *rb = static_cast<T *>(ctx->recv);
     // 7. key exchange: one send and one receive per peer link, grouped (RCCL all-to-all-v)
-    DSORT_NCCL(ctx, ncclGroupStart());
-    for (int r = 0; r < P; ++r) {
-        if (r == me) continue;
-        if (hcnt[r]) DSORT_NCCL(ctx, ncclSend(d_keys + hcut[r], hcnt[r], nccl_type<T>(), r, ctx->comm, s));
-        if (rlen[r]) DSORT_NCCL(ctx, ncclRecv(rb + roff[r], rlen[r], nccl_type<T>(), r, ctx->comm, s));
+    if (!host_tx) {
+        DSORT_NCCL(ctx, ncclGroupStart());
+        for (int r = 0; r < P; ++r) {
+            if (r == me) continue;
+            if (hcnt[r]) DSORT_NCCL(ctx, ncclSend(d_keys + hcut[r], hcnt[r], nccl_type<T>(), r, ctx->comm, s));
+            if (rlen[r]) DSORT_NCCL(ctx, ncclRecv(rb + roff[r], rlen[r], nccl_type<T>(), r, ctx->comm, s));
+        }
+        DSORT_NCCL(ctx, ncclGroupEnd());
+        if (hcnt[me])
+            DSORT_HIP(ctx, hipMemcpyAsync(rb + roff[me], d_keys + hcut[me], hcnt[me] * sizeof(T),
+                                          hipMemcpyDeviceToDevice, s));
+    } else {
+        // host-staged all-to-all-v: D2H the sorted run, exchange, H2D the received runs
+        rc = ensure_host(ctx, &ctx->xfer, &ctx->xfer_bytes, (n_local ? n_local : 1) * sizeof(T));
+        if (rc) return rc;
+        rc = ensure_host(ctx, &ctx->xfer2, &ctx->xfer2_bytes, (nrecv ? nrecv : 1) * sizeof(T));
+        if (rc) return rc;
+        if (n_local)
+            DSORT_HIP(ctx, hipMemcpyAsync(ctx->xfer, d_keys, n_local * sizeof(T), hipMemcpyDeviceToHost, s));
+        DSORT_HIP(ctx, hipStreamSynchronize(s));
+        std::vector<size_t> sc(P), sd(P), rcn(P), rd(P);
+        for (int r = 0; r < P; ++r) {
+            sc[r] = hcnt[r] * sizeof(T);
+            sd[r] = hcut[r] * sizeof(T);
+            rcn[r] = rlen[r] * sizeof(T);
+            rd[r] = roff[r] * sizeof(T);
+        }
+        if (ctx->transport.alltoallv(ctx->transport.user, ctx->xfer, sc.data(), sd.data(), ctx->xfer2,
+                                     rcn.data(), rd.data()))
+            return set_err(ctx, DSORT_ECOMM, "host transport alltoallv (keys) failed");
+        if (nrecv) DSORT_HIP(ctx, hipMemcpyAsync(rb, ctx->xfer2, nrecv * sizeof(T), hipMemcpyHostToDevice, s));
     }
-    DSORT_NCCL(ctx, ncclGroupEnd());
-    if (hcnt[me])
-        DSORT_HIP(ctx, hipMemcpyAsync(rb + roff[me], d_keys + hcut[me], hcnt[me] * sizeof(T),
-                                      hipMemcpyDeviceToDevice, s));
     if (ctx->ev_ok) {
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[3], s));
         ctx->ev_mask |= 8u;
@@ -525,6 +584,8 @@ int dsort_finalize(dsort_ctx *ctx) {
         if (b) hipFree(b);
     if (ctx->red_host) hipHostFree(ctx->red_host);
     if (ctx->small_host) hipHostFree(ctx->small_host);
+    if (ctx->xfer) (void)hipHostFree(ctx->xfer);
+    if (ctx->xfer2) (void)hipHostFree(ctx->xfer2);
     if (ctx->groups_host) (void)hipHostFree(ctx->groups_host);
     if (ctx->groups_ev) (void)hipEventDestroy(ctx->groups_ev);
     for (auto &e : ctx->ev)
@@ -625,13 +686,28 @@ int dsort_comm_unique_id(char id[DSORT_UNIQUE_ID_BYTES]) {
 
 int dsort_comm_init(dsort_ctx *ctx, int nranks, int rank, const char id[DSORT_UNIQUE_ID_BYTES]) {
     if (!ctx || !id || nranks < 1 || rank < 0 || rank >= nranks) return set_err(ctx, DSORT_EINVAL, "bad argument");
-    if (ctx->comm) return set_err(ctx, DSORT_EINVAL, "communicator already initialised");
+    if (ctx->comm || ctx->has_transport) return set_err(ctx, DSORT_EINVAL, "communicator already initialised");
     DSORT_HIP(ctx, hipSetDevice(ctx->device));
     ncclUniqueId u;
     memcpy(&u, id, sizeof(u));
     ncclComm_t c = nullptr;
-    DSORT_NCCL(ctx, ncclCommInitRank(&c, nranks, u, rank));
+    const ncclResult_t r = ncclCommInitRank(&c, nranks, u, rank);
+    if (r != ncclSuccess)
+        return set_err(ctx, DSORT_ECOMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r) +
+                                             " (RCCL needs one GPU per rank; ranks sharing a GPU use "
+                                             "dsort_comm_init_transport)");
     ctx->comm = c;
+    ctx->nranks = nranks;
+    ctx->rank = rank;
+    return DSORT_OK;
+}
+
+int dsort_comm_init_transport(dsort_ctx *ctx, int nranks, int rank, const dsort_transport *t) {
+    if (!ctx || !t || !t->allgather || !t->alltoallv || nranks < 1 || rank < 0 || rank >= nranks)
+        return set_err(ctx, DSORT_EINVAL, "bad argument");
+    if (ctx->comm || ctx->has_transport) return set_err(ctx, DSORT_EINVAL, "communicator already initialised");
+    ctx->transport = *t;
+    ctx->has_transport = true;
     ctx->nranks = nranks;
     ctx->rank = rank;
     return DSORT_OK;
@@ -639,6 +715,7 @@ int dsort_comm_init(dsort_ctx *ctx, int nranks, int rank, const char id[DSORT_UN
 
 int dsort_comm_abort(dsort_ctx *ctx) {
     if (!ctx) return DSORT_EINVAL;
+    ctx->has_transport = false;
     if (ctx->comm) ncclCommAbort(ctx->comm);
     ctx->comm = nullptr;
     ctx->nranks = 1;
@@ -648,6 +725,7 @@ int dsort_comm_abort(dsort_ctx *ctx) {
 
 int dsort_comm_destroy(dsort_ctx *ctx) {
     if (!ctx) return DSORT_EINVAL;
+    ctx->has_transport = false;
     if (ctx->comm) {
         hipStreamSynchronize(ctx->stream);
         ncclCommDestroy(ctx->comm);

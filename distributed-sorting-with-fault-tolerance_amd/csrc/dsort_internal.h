@@ -86,6 +86,12 @@ struct dsort_ctx {
     uint64_t *red_host = nullptr;  // pinned mirror
     // sample sort (multi-GPU)
     ncclComm *comm = nullptr;
+    bool has_transport = false;   // host transport instead of RCCL (dsort_comm_init_transport)
+    dsort_transport transport = {};
+    void *xfer = nullptr;         // pinned host staging of the host transport
+    size_t xfer_bytes = 0;
+    void *xfer2 = nullptr;
+    size_t xfer2_bytes = 0;
     int nranks = 1;
     int rank = 0;
     void *local = nullptr;  // locally sorted chunk

@@ -28,7 +28,8 @@ EXPORTS = [
     "dsort_synchronize", "dsort_sort_i32", "dsort_sort_i64", "dsort_sort_dev_i32",
     "dsort_sort_dev_i64", "dsort_sort_dev_copy_i32", "dsort_sort_dev_copy_i64",
     "dsort_merge_i32", "dsort_merge_i64", "dsort_merge_dev_i32", "dsort_merge_dev_i64",
-    "dsort_comm_unique_id", "dsort_comm_init", "dsort_comm_abort", "dsort_comm_destroy",
+    "dsort_comm_unique_id", "dsort_comm_init", "dsort_comm_init_transport", "dsort_comm_abort",
+    "dsort_comm_destroy",
     "dsort_sample_sort_dev_i32", "dsort_sample_sort_dev_i64", "dsort_sample_merge_dev_i32",
     "dsort_sample_merge_dev_i64", "dsort_plan_splitters_i32",
     "dsort_plan_splitters_i64", "dsort_plan_cuts_i32", "dsort_plan_cuts_i64",
@@ -53,6 +54,63 @@ class Stats(ctypes.Structure):
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                ctypes.c_size_t)
+ALLTOALLV_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t),
+                                ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t),
+                                ctypes.POINTER(ctypes.c_size_t))
+
+
+class Transport(ctypes.Structure):
+    """dsort_transport: the sample sort's exchanges through host callbacks (dsort.h)."""
+    _fields_ = [("user", ctypes.c_void_p), ("allgather", ALLGATHER_FN), ("alltoallv", ALLTOALLV_FN)]
+
+
+def torch_dist_transport(world):
+    """A dsort_transport over torch.distributed's default process group (gloo: CPU tensors).
+    For ranks that share a GPU, where RCCL refuses to build a communicator."""
+    import torch.distributed as dist
+
+    def _allgather(user, send, recv, nbytes):
+        try:
+            mine = torch.frombuffer(bytearray(ctypes.string_at(send, nbytes)), dtype=torch.uint8) \
+                if nbytes else torch.empty(0, dtype=torch.uint8)
+            outs = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(world)]
+            dist.all_gather(outs, mine)
+            if nbytes:
+                whole = torch.cat(outs).numpy()
+                ctypes.memmove(recv, whole.ctypes.data, whole.nbytes)
+            return 0
+        except Exception as e:  # pragma: no cover - reported through the C error path
+            print("dsort host transport allgather:", e, flush=True)
+            return 1
+
+    def _alltoallv(user, send, sc, sd, recv, rc, rd):
+        try:
+            scounts = [int(sc[i]) for i in range(world)]
+            rcounts = [int(rc[i]) for i in range(world)]
+            chunks = b"".join(ctypes.string_at(send + int(sd[i]), scounts[i]) if scounts[i] else b""
+                              for i in range(world))
+            inp = torch.frombuffer(bytearray(chunks), dtype=torch.uint8) if chunks else torch.empty(0, dtype=torch.uint8)
+            out = torch.empty(sum(rcounts), dtype=torch.uint8)
+            dist.all_to_all_single(out, inp, output_split_sizes=rcounts, input_split_sizes=scounts)
+            o = out.numpy()
+            off = 0
+            for i in range(world):
+                if rcounts[i]:
+                    ctypes.memmove(recv + int(rd[i]), o.ctypes.data + off, rcounts[i])
+                off += rcounts[i]
+            return 0
+        except Exception as e:  # pragma: no cover
+            print("dsort host transport alltoallv:", e, flush=True)
+            return 1
+
+    t = Transport(None, ALLGATHER_FN(_allgather), ALLTOALLV_FN(_alltoallv))
+    t._keep = (_allgather, _alltoallv)  # the C side holds raw function pointers
+    return t
 
 
 _lib = None
@@ -89,6 +147,7 @@ def load():
         "dsort_merge_dev_i64": (ctypes.c_int, [P, P, P, ctypes.c_int, P, P]),
         "dsort_comm_unique_id": (ctypes.c_int, [P]),
         "dsort_comm_init": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, P]),
+        "dsort_comm_init_transport": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(Transport)]),
         "dsort_comm_abort": (ctypes.c_int, [P]),
         "dsort_comm_destroy": (ctypes.c_int, [P]),
         "dsort_sample_sort_dev_i32": (ctypes.c_int, [P, P, SZ, ctypes.POINTER(P), ctypes.POINTER(SZ), P]),
@@ -317,6 +376,10 @@ class Context:
         assert len(uid) == 128
         buf = ctypes.create_string_buffer(uid, 128)
         self.check(self.lib.dsort_comm_init(self.h, nranks, rank, buf))
+
+    def comm_init_transport(self, nranks, rank, transport):
+        self._transport = transport  # keep the callbacks alive while the library may call them
+        self.check(self.lib.dsort_comm_init_transport(self.h, nranks, rank, ctypes.byref(transport)))
 
     def comm_destroy(self):
         self.check(self.lib.dsort_comm_destroy(self.h))

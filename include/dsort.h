@@ -116,6 +116,20 @@ int dsort_merge_dev_i64(dsort_ctx *ctx, const int64_t *d_in, const size_t lens[]
 #define DSORT_UNIQUE_ID_BYTES 128
 int dsort_comm_unique_id(char id[DSORT_UNIQUE_ID_BYTES]);
 int dsort_comm_init(dsort_ctx *ctx, int nranks, int rank, const char id[DSORT_UNIQUE_ID_BYTES]);
+/* Host transport: the sample sort's three exchanges (samples, counts, keys) through caller
+ * callbacks on HOST buffers instead of RCCL.  RCCL needs one GPU per rank; this serves ranks
+ * that share a GPU (tests on a 1-GPU box drive it with gloo) or hosts without a usable RCCL.
+ * All sizes in bytes; every callback returns 0 on success.
+ *   allgather: rank r's `bytes` from `send` land at recv + r*bytes on every rank.
+ *   alltoallv: send[sdispls[d] .. +scounts[d]) goes to rank d, which receives it at
+ *              recv[rdispls[s] .. +rcounts[s]) for source s. */
+typedef struct dsort_transport {
+    void *user;
+    int (*allgather)(void *user, const void *send, void *recv, size_t bytes);
+    int (*alltoallv)(void *user, const void *send, const size_t *scounts, const size_t *sdispls,
+                     void *recv, const size_t *rcounts, const size_t *rdispls);
+} dsort_transport;
+int dsort_comm_init_transport(dsort_ctx *ctx, int nranks, int rank, const dsort_transport *t);
 /* Abort in-flight collectives (fault path: a peer died) and drop the communicator. */
 int dsort_comm_abort(dsort_ctx *ctx);
 int dsort_comm_destroy(dsort_ctx *ctx);

@@ -1,6 +1,8 @@
-"""Sample sort with several ranks.  On the 1-GPU box all ranks share cuda:0 (if RCCL accepts
-that); the driver's 8-GPU bench runs one rank per GPU.  Checks: the concatenation of the rank
-slices equals numpy.sort of the whole synthetic input (bit-exact), slices are balanced."""
+"""Sample sort with several ranks.  On the 1-GPU box all ranks share cuda:0, which RCCL refuses
+("invalid usage": one GPU per rank), so these ranks run the SAME libdsort sample sort with the
+exchanges through the host transport (gloo); the RCCL exchange itself is exercised with one rank
+here and with one rank per GPU by the driver's multi-GPU bench.  Checks: the concatenation of the
+rank slices equals numpy.sort of the whole synthetic input (bit-exact), slices are balanced."""
 import json
 import os
 import subprocess
@@ -16,11 +18,12 @@ pytestmark = pytest.mark.gpu
 DRIVER = os.path.join(REPO, "tests", "mp_samplesort.py")
 
 
-def run_ranks(tmp_path, world, n, dtype="i32", dist="uniform"):
+def run_ranks(tmp_path, world, n, dtype="i32", dist="uniform", transport="host"):
     port = free_port()
     out = str(tmp_path / "ss")
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
-    procs = [subprocess.Popen([sys.executable, DRIVER, str(r), str(world), str(port), str(n), dtype, dist, out],
+    procs = [subprocess.Popen([sys.executable, DRIVER, str(r), str(world), str(port), str(n), dtype, dist, out,
+                               transport],
                               env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(world)]
     logs = []
     for p in procs:
@@ -55,6 +58,16 @@ def test_sample_sort_zipf_i64(tmp_path):
     assert np.array_equal(np.concatenate(outs), np.sort(ins))
     sizes = [o.size for o in outs]
     assert max(sizes) <= 1.3 * n / 2, sizes  # the heavy key is split across ranks
+
+
+def test_sample_sort_rccl_single_rank(tmp_path):
+    ins, outs, meta = run_ranks(tmp_path, 1, 1_000_003, transport="rccl")
+    assert np.array_equal(np.concatenate(outs), np.sort(ins))
+
+
+def test_rccl_refuses_shared_gpu_with_clear_error(tmp_path):
+    with pytest.raises(AssertionError, match="one GPU per rank"):
+        run_ranks(tmp_path, 2, 1000, transport="rccl")
 
 
 def test_sample_sort_tiny_and_empty_ranks(tmp_path):
