@@ -12,7 +12,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libdsort.so")
+# DSORT_LIB: an alternative build of the same library (A/B experiments of compile-time variants)
+LIB_PATH = os.environ.get("DSORT_LIB") or os.path.join(HERE, "lib", "libdsort.so")
 
 try:  # shared HIP runtime (see module docstring); absence of torch is fine on the CPU box
     import torch  # noqa: F401
