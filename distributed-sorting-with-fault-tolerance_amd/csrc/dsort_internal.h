@@ -128,6 +128,13 @@ int sort_device(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipStream_t 
 template <typename T>
 int merge_device(dsort_ctx *ctx, const T *d_in, const size_t *lens, int k, T *d_out,
                  hipStream_t s);
+// int32 path on wave-register bitonic networks (dsort_wave.hip); sort_device/merge_device route
+// 32-bit keys here unless DSORT_KERNELS=legacy selects the LDS merge-path kernels.
+int wave_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys, size_t n, hipStream_t s,
+                  bool timed);
+int wave_merge_i32(dsort_ctx *ctx, const int32_t *d_in, const size_t *lens, int k, int32_t *d_out,
+                   hipStream_t s);
+bool use_legacy_kernels();
 
 }  // namespace dsort
 

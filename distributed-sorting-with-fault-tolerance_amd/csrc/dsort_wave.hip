@@ -1,0 +1,742 @@
+// dsort_wave.hip -- the int32 sort and merge on wave-wide register bitonic networks (gfx950).
+//
+// Replaces merge_sort()/merge() (reference client.c:140-173) and the merge loop of
+// merge_chunks() (server.c:481-515) for 32-bit keys.  Same result as the legacy LDS merge-path
+// kernels of dsort_sort.hip (the input multiset in ascending signed order), different machine
+// mapping:
+//
+//   * A wave holds 1024 keys, 16 per lane.  Every merge step of the sort is a bitonic network
+//     executed in registers: compare-exchanges between registers of one lane, cross-lane ones
+//     through DPP (quad_perm, row_ror, row_shl/shr, row_mirror) and v_med3_i32 with a per-lane
+//     +-inf constant (one instruction gives the min to the lower lane and the max to the upper),
+//     and the two row-crossing bits by v_permlane16/32_swap transpositions.  No per-lane
+//     merge-path search and no data-dependent LDS addressing: LDS is only read and written with
+//     consecutive lanes on consecutive words.
+//   * block_sort_w_kernel: one workgroup (16 waves) sorts a TILE of 16384 keys: each wave sorts
+//     its 1024 keys in registers (Batcher network per lane, then bitonic merges of 32..1024),
+//     then four LDS levels merge runs of 1024 -> 16384.
+//   * mergew_kernel: one workgroup merges one output tile of a k-way pass: the F input windows
+//     (cut by partk_kernel, dsort_part.h) are staged back to back in LDS and merged in log2(F)
+//     pairwise levels.
+//   * An LDS level cuts every pair of runs into windows of <= 1024 outputs.  One wave finds the
+//     window's merge-path split at both ends with a 64-ary search (64 probes per step, ballot),
+//     loads A ascending, +inf padding, B descending -- a bitonic sequence -- and sorts it with
+//     the 10-stage half-cleaner network.  Windows are held in registers across a barrier, so the
+//     level merges in place in one LDS buffer.
+//
+// Algorithmic HBM traffic: 8 bytes per key for the tile sort and for every pass.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+
+#include <climits>
+#include <cstdlib>
+#include <vector>
+
+#include "dsort_internal.h"
+#include "dsort_part.h"
+
+namespace dsort {
+namespace wv {
+
+constexpr int R = 16;              // keys per lane
+constexpr int WK = 64 * R;         // keys per wave: one bitonic window
+constexpr int WAVES = 16;          // waves per workgroup
+constexpr int THREADS = 64 * WAVES;
+constexpr int TILE = WK * WAVES;   // keys per workgroup tile (64 KiB of LDS)
+constexpr int KMAX = INT32_MAX;
+constexpr int KMIN = INT32_MIN;
+constexpr int kWaveMaxLogF = 5;    // fan-in cap of one merge pass (<= 2 windows per wave)
+constexpr int SLACK = TILE / 32;   // cut tolerance of partk
+constexpr int TNOM = TILE - 2 * SLACK;
+
+// DPP controls (gfx9 encoding)
+constexpr int QP_1032 = 0xB1;      // lane ^ 1
+constexpr int QP_2301 = 0x4E;      // lane ^ 2
+constexpr int QP_3210 = 0x1B;      // lane ^ 3
+constexpr int ROW_SHL4 = 0x104;    // lane i reads lane i + 4 (within a row of 16)
+constexpr int ROW_SHR4 = 0x114;    // lane i reads lane i - 4
+constexpr int ROW_ROR8 = 0x128;    // lane ^ 8
+constexpr int ROW_MIRROR = 0x140;  // lane ^ 15
+constexpr int ROW_HMIRROR = 0x141; // lane ^ 7
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+// median of three: with c = -inf it is min(a, b), with c = +inf max(a, b)
+__device__ __forceinline__ int med3(int a, int b, int c) {
+    int r;
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+template <int CTRL>
+__device__ __forceinline__ int dpp(int x) {
+    return __builtin_amdgcn_mov_dpp(x, CTRL, 0xF, 0xF, false);
+}
+
+// value of lane ^ 4: two bank-masked row shifts (banks 0,2 read +4, banks 1,3 read -4)
+__device__ __forceinline__ int dpp_xor4(int x) {
+    const int p = __builtin_amdgcn_mov_dpp(x, ROW_SHL4, 0xF, 0x5, false);
+    return __builtin_amdgcn_update_dpp(p, x, ROW_SHR4, 0xF, 0xA, false);
+}
+
+__device__ __forceinline__ void cex(int &a, int &b) {
+    const int lo = a < b ? a : b;
+    const int hi = a < b ? b : a;
+    a = lo;
+    b = hi;
+}
+
+// +inf on lanes whose bit b is set (they keep the max of a compare-exchange), -inf elsewhere
+__device__ __forceinline__ int lane_side(int b) { return ((lane_id() >> b) & 1) ? KMAX : KMIN; }
+
+__device__ __forceinline__ void swap32(int &a, int &b) {
+    const auto r = __builtin_amdgcn_permlane32_swap((unsigned)a, (unsigned)b, false, false);
+    a = (int)r[0];
+    b = (int)r[1];
+}
+__device__ __forceinline__ void swap16(int &a, int &b) {
+    const auto r = __builtin_amdgcn_permlane16_swap((unsigned)a, (unsigned)b, false, false);
+    a = (int)r[0];
+    b = (int)r[1];
+}
+
+// ------------------------------------------------------------------------------------------
+// Half-cleaner network on a reg-major window: x[i] at lane t is element e = 64 i + t of a
+// bitonic sequence of 1024 keys; afterwards the sequence is ascending, element
+// out_elem(i, t) in x[i] at lane t (bits 5 and 4 are moved between lanes and registers by the
+// permlane transpositions).
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ constexpr int out_hi(int i) {
+    return ((i >> 3) & 1) << 9 | ((i >> 2) & 1) << 8 | (i & 1) << 5 | ((i >> 1) & 1) << 4;
+}
+__device__ __forceinline__ int out_lo(int t) {
+    return ((t >> 4) & 1) << 7 | ((t >> 5) & 1) << 6 | (t & 15);
+}
+
+__device__ __forceinline__ void merge_net(int (&x)[R], int c0, int c1, int c2, int c3) {
+#pragma unroll
+    for (int b = 3; b >= 0; --b) {  // element bits 9..6 = register bits 3..0
+#pragma unroll
+        for (int i = 0; i < R; ++i)
+            if (!(i & (1 << b))) cex(x[i], x[i | (1 << b)]);
+    }
+#pragma unroll
+    for (int k = 0; k < R; k += 2) {  // element bit 5: lane bit 5 <-> register bit 0
+        swap32(x[k], x[k + 1]);
+        cex(x[k], x[k + 1]);
+    }
+#pragma unroll
+    for (int k = 0; k < R; ++k) {  // element bit 4: lane bit 4 <-> register bit 1
+        if (k & 2) continue;
+        swap16(x[k], x[k + 2]);
+        cex(x[k], x[k + 2]);
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i) x[i] = med3(x[i], dpp<ROW_ROR8>(x[i]), c3);
+#pragma unroll
+    for (int i = 0; i < R; ++i) x[i] = med3(x[i], dpp_xor4(x[i]), c2);
+#pragma unroll
+    for (int i = 0; i < R; ++i) x[i] = med3(x[i], dpp<QP_2301>(x[i]), c1);
+#pragma unroll
+    for (int i = 0; i < R; ++i) x[i] = med3(x[i], dpp<QP_1032>(x[i]), c0);
+}
+
+// ------------------------------------------------------------------------------------------
+// Sort of one wave's 1024 keys in registers, lane-major: x[i] at lane t is element 16 t + i.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void sort16(int (&v)[R]) {  // Batcher odd-even merge sort, 63 cex
+#pragma unroll
+    for (int p = 1; p < R; p <<= 1) {
+#pragma unroll
+        for (int k = p; k >= 1; k >>= 1) {
+#pragma unroll
+            for (int j = k % p; j + k < R; j += 2 * k) {
+#pragma unroll
+                for (int i = 0; i < k; ++i) {
+                    if (i + j + k < R && (i + j) / (2 * p) == (i + j + k) / (2 * p))
+                        cex(v[i + j], v[i + j + k]);
+                }
+            }
+        }
+    }
+}
+
+// Half-cleaner on element bit b of a lane-major wave (b <= 8).
+template <int B>
+__device__ __forceinline__ void hc_lane_major(int (&x)[R], const int (&c)[6]) {
+    if constexpr (B <= 3) {
+#pragma unroll
+        for (int i = 0; i < R; ++i)
+            if (!(i & (1 << B))) cex(x[i], x[i | (1 << B)]);
+    } else if constexpr (B == 4) {
+#pragma unroll
+        for (int i = 0; i < R; ++i) x[i] = med3(x[i], dpp<QP_1032>(x[i]), c[0]);
+    } else if constexpr (B == 5) {
+#pragma unroll
+        for (int i = 0; i < R; ++i) x[i] = med3(x[i], dpp<QP_2301>(x[i]), c[1]);
+    } else if constexpr (B == 6) {
+#pragma unroll
+        for (int i = 0; i < R; ++i) x[i] = med3(x[i], dpp_xor4(x[i]), c[2]);
+    } else if constexpr (B == 7) {
+#pragma unroll
+        for (int i = 0; i < R; ++i) x[i] = med3(x[i], dpp<ROW_ROR8>(x[i]), c[3]);
+    } else {  // B == 8: lane bit 4, through a permlane16 transposition with register bit 0
+        static_assert(B == 8, "half-cleaner bit out of range");
+#pragma unroll
+        for (int k = 0; k < R; k += 2) {
+            swap16(x[k], x[k + 1]);
+            cex(x[k], x[k + 1]);
+            swap16(x[k], x[k + 1]);
+        }
+    }
+}
+
+// Partner of the mirror stage of a merge of 2^M keys: lane t ^ (2^(M-4) - 1).
+template <int M>
+__device__ __forceinline__ int mirror_partner(int v) {
+    if constexpr (M == 5) return dpp<QP_1032>(v);
+    else if constexpr (M == 6) return dpp<QP_3210>(v);
+    else if constexpr (M == 7) return dpp<ROW_HMIRROR>(v);
+    else if constexpr (M == 8) return dpp<ROW_MIRROR>(v);
+    else if constexpr (M == 9) return __shfl_xor(v, 31);
+    else return __shfl_xor(v, 63);
+}
+
+template <int B, int M>
+__device__ __forceinline__ void hc_down(int (&x)[R], const int (&c)[6]) {
+    hc_lane_major<B>(x, c);
+    if constexpr (B > 0) hc_down<B - 1, M>(x, c);
+}
+
+// Merge of sorted (ascending) blocks of 2^(M-1) keys into blocks of 2^M: the first stage
+// compares element e with its mirror e ^ (2^M - 1), then half-cleaners on bits M-2 .. 0.
+template <int M>
+__device__ __forceinline__ void merge_lane_major(int (&x)[R], const int (&c)[6]) {
+    int y[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) y[i] = med3(x[i], mirror_partner<M>(x[R - 1 - i]), c[M - 5]);
+#pragma unroll
+    for (int i = 0; i < R; ++i) x[i] = y[i];
+    hc_down<M - 2, M>(x, c);
+}
+
+__device__ __forceinline__ void sort_wave(int (&x)[R], const int (&c)[6]) {
+    sort16(x);
+    merge_lane_major<5>(x, c);
+    merge_lane_major<6>(x, c);
+    merge_lane_major<7>(x, c);
+    merge_lane_major<8>(x, c);
+    merge_lane_major<9>(x, c);
+    merge_lane_major<10>(x, c);
+}
+
+// ------------------------------------------------------------------------------------------
+// LDS levels
+// ------------------------------------------------------------------------------------------
+// Merge-path split: number of A keys among the first d outputs of merge(A, B), A first on ties
+// (A = s[pa, pa+na), B = s[pb, pb+nb)).  All lanes of the wave cooperate: each step probes 64
+// candidates at an odd stride (distinct LDS banks) and keeps the bracket the ballot points to.
+__device__ __forceinline__ int coop_split(const int *s, int pa, int na, int pb, int nb, int d) {
+    int lo = d > nb ? d - nb : 0;
+    int hi = d < na ? d : na;
+    const int lane = lane_id();
+#pragma unroll 1
+    while (lo < hi) {
+        const int len = hi - lo;
+        const int step = ((len + 63) >> 6) | 1;
+        const int a = lo + lane * step;
+        bool q = true;
+        if (a < hi) q = s[pa + a] > s[pb + d - 1 - a];
+        const unsigned long long m = __ballot(q);
+        const int j = m ? (int)__ffsll((long long)m) - 1 : 64;
+        const int nhi = lo + j * step < hi ? lo + j * step : hi;
+        lo = j ? lo + (j - 1) * step + 1 : lo;
+        hi = nhi;
+        lo = __builtin_amdgcn_readfirstlane(lo);
+        hi = __builtin_amdgcn_readfirstlane(hi);
+    }
+    return lo;
+}
+
+// Loads the bitonic window (reg-major): elements [0, qa) = A ascending from s[abase],
+// [qa, qa+pad) = +inf, [qa+pad, 1024) = B descending ending at s[bbase - 1023 + ...]:
+// element e >= qa+pad is s[bbase - e].  qa, pad are wave-uniform.
+__device__ __forceinline__ void load_window(const int *s, int abase, int bbase, int qa, int pad,
+                                            int (&x)[R]) {
+    const int t = lane_id();
+    const int qp = qa + pad;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        const int e0 = 64 * i;
+        if (e0 + 64 <= qa) {
+            x[i] = s[abase + e0 + t];
+        } else if (e0 >= qp) {
+            x[i] = s[bbase - e0 - t];
+        } else {
+            const int e = e0 + t;
+            int idx = e < qa ? abase + e : bbase - e;
+            idx = idx < 0 ? 0 : (idx > TILE - 1 ? TILE - 1 : idx);
+            const int v = s[idx];
+            x[i] = (e >= qa && e < qp) ? KMAX : v;
+        }
+    }
+}
+
+struct Window {
+    int obase;  // output position of element 0 (within the tile)
+    int wreal;  // real keys in the window (the rest are +inf padding)
+};
+
+// Merges the window of outputs [d0, d0 + wreal) of the pair A = s[pa, pa+na), B = s[pb, pb+nb)
+// into registers (layout of merge_net).
+__device__ __forceinline__ void merge_window(const int *s, int pa, int na, int pb, int nb, int d0,
+                                             int wreal, int (&x)[R], int c0, int c1, int c2,
+                                             int c3) {
+    const int a0 = coop_split(s, pa, na, pb, nb, d0);
+    const int a1 = coop_split(s, pa, na, pb, nb, d0 + wreal);
+    const int b0 = d0 - a0, b1 = d0 + wreal - a1;
+    const int qa = a1 - a0;
+    const int pad = WK - wreal;
+    (void)b1;
+    load_window(s, pa + a0 + 0, pb + b0 + (WK - 1) - 0, qa, pad, x);
+    merge_net(x, c0, c1, c2, c3);
+}
+
+__device__ __forceinline__ void store_window_lds(int *s, const Window &w, const int (&x)[R]) {
+    const int base = w.obase + out_lo(lane_id());
+    if (w.wreal == WK) {
+#pragma unroll
+        for (int i = 0; i < R; ++i) s[base + out_hi(i)] = x[i];
+    } else {
+        const int lo = out_lo(lane_id());
+#pragma unroll
+        for (int i = 0; i < R; ++i)
+            if (out_hi(i) + lo < w.wreal) s[base + out_hi(i)] = x[i];
+    }
+}
+
+__device__ __forceinline__ void store_window_global(int *out, const Window &w, int limit,
+                                                    const int (&x)[R]) {
+    // writes positions [obase, obase + min(wreal, limit - obase)) of the tile
+    const int lo = out_lo(lane_id());
+    int *p = out + w.obase + lo;
+    int lim = limit - w.obase;
+    lim = lim < w.wreal ? lim : w.wreal;
+    if (lim >= WK) {
+#pragma unroll
+        for (int i = 0; i < R; ++i) p[out_hi(i)] = x[i];
+    } else {
+#pragma unroll
+        for (int i = 0; i < R; ++i)
+            if (out_hi(i) + lo < lim) p[out_hi(i)] = x[i];
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// 1. Tile sort.
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(THREADS, 8) block_sort_w_kernel(const int *in, int *out,
+                                                                    uint64_t n) {
+    // `in` may alias `out`: every workgroup reads its tile before it writes it
+    __shared__ __attribute__((aligned(16))) int s[TILE];
+    const int t = lane_id();
+    const int w = threadIdx.x >> 6;
+    const uint64_t base = (uint64_t)blockIdx.x * TILE;
+    const uint64_t rem = n - base;
+    const int valid = rem < (uint64_t)TILE ? (int)rem : TILE;
+    const int c[6] = {lane_side(0), lane_side(1), lane_side(2), lane_side(3), lane_side(4),
+                      lane_side(5)};
+
+    int x[R];
+    if (valid == TILE && (reinterpret_cast<uintptr_t>(in) & 15) == 0) {
+        const int4 *src = reinterpret_cast<const int4 *>(in + base) + w * (WK / 4);
+#pragma unroll
+        for (int q = 0; q < R / 4; ++q) {
+            const int4 v = src[q * 64 + t];
+            x[4 * q] = v.x;
+            x[4 * q + 1] = v.y;
+            x[4 * q + 2] = v.z;
+            x[4 * q + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < R / 4; ++q) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int e = w * WK + 4 * (q * 64 + t) + j;
+                x[4 * q + j] = e < valid ? in[base + e] : KMAX;
+            }
+        }
+    }
+    sort_wave(x, c);
+    // lane-major run of the wave -> LDS
+    {
+        int4 *dst = reinterpret_cast<int4 *>(s + w * WK + t * R);
+#pragma unroll
+        for (int q = 0; q < R / 4; ++q) dst[q] = make_int4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int r = WK; r < TILE; r <<= 1) {
+        const int wpp = (2 * r) / WK;  // windows per pair
+        const int j = w / wpp, o = w % wpp;
+        const int ps = j * 2 * r;
+        merge_window(s, ps, r, ps + r, r, o * WK, WK, x, c[0], c[1], c[2], c[3]);
+        const Window win{ps + o * WK, WK};
+        __syncthreads();
+        if (2 * r == TILE) {
+            store_window_global(out + base, win, valid, x);
+        } else {
+            store_window_lds(s, win, x);
+            __syncthreads();
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// 2. Merge of one output tile of a k-way pass (cuts from partk_kernel).
+// ------------------------------------------------------------------------------------------
+template <int LOGF, bool REG>
+__global__ void __launch_bounds__(THREADS, 8) mergew_kernel(const int *__restrict__ in,
+                                                            int *__restrict__ out, PassDesc pd,
+                                                            int tnom,
+                                                            const uint32_t *__restrict__ splits) {
+    constexpr int F = 1 << LOGF;
+    constexpr int MAXWIN = (WAVES + F / 2 + WAVES - 1) / WAVES;
+    constexpr int NCHUNK = TILE / 64;
+    __shared__ __attribute__((aligned(16))) int s[TILE];
+    __shared__ int soff[F + 1];
+    __shared__ int64_t gdelta[F];        // global index of tile key e in segment sg = gdelta[sg] + e
+    __shared__ uint8_t chunkseg[NCHUNK + 1];
+    __shared__ uint64_t s_out;
+    __shared__ int s_total;
+
+    const int t = lane_id();
+    const int w = threadIdx.x >> 6;
+    const uint64_t j = blockIdx.x;
+    TileInfo ti;
+    const GroupK *g = tile_info<REG>(pd, j, tnom, ti);
+    if (threadIdx.x < 64) {
+        const int i = t & (F - 1);
+        uint64_t rs, rl;
+        run_range<REG>(pd, ti, g, i, rs, rl);
+        const uint32_t s0 = splits[j * F + i];
+        const uint32_t s1 = ti.jr + 1 == ti.ntg ? (uint32_t)rl : splits[(j + 1) * F + i];
+        const int len = (int)(s1 - s0);
+        int incl = len;
+        uint64_t before = s0;  // output offset of the tile = keys of the group below its cut
+        for (int o = 1; o < F; o <<= 1) {
+            const int v = __shfl_up(incl, o);
+            if (i >= o) incl += v;
+            before += __shfl_xor(before, o);
+        }
+        if (t < F) {
+            soff[i + 1] = incl;
+            gdelta[i] = (int64_t)(rs + s0) - (int64_t)(incl - len);
+            if (i == F - 1) s_total = incl;
+            if (i == 0) {
+                soff[0] = 0;
+                s_out = ti.base + before;
+            }
+        }
+    }
+    __syncthreads();
+    const int total = __builtin_amdgcn_readfirstlane(s_total);
+    // segment of the first key of every 64-key chunk
+    if (threadIdx.x <= NCHUNK) {
+        const int e = threadIdx.x * 64;
+        int lo = 0, hi = F - 1;  // last segment starting at or before e
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (soff[mid] <= e) lo = mid;
+            else hi = mid - 1;
+        }
+        chunkseg[threadIdx.x] = (uint8_t)lo;
+    }
+    __syncthreads();
+    // Staging: key e of the tile is loaded by thread e % THREADS (coalesced within a segment).
+    // The segments a wave's 64 consecutive keys touch are known per chunk, so the segment of a
+    // key costs no divergent search; all 16 loads are in flight before the LDS stores.
+    {
+        int v[R];
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const int e = threadIdx.x + k * THREADS;
+            const int c = w + k * WAVES;
+            const int first = __builtin_amdgcn_readfirstlane((int)chunkseg[c]);
+            const int lastc = __builtin_amdgcn_readfirstlane((int)chunkseg[c + 1]);
+            int sg = first;
+            for (int q = first + 1; q <= lastc; ++q) sg += soff[q] <= e ? 1 : 0;
+            const int64_t gi = gdelta[sg] + e;
+            v[k] = e < total ? in[gi] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const int e = threadIdx.x + k * THREADS;
+            if (e < total) s[e] = v[k];
+        }
+    }
+    __syncthreads();
+
+    const int c0 = lane_side(0), c1 = lane_side(1), c2 = lane_side(2), c3 = lane_side(3);
+    const uint64_t so = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(s_out >> 32)) << 32) |
+                        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)s_out);
+    int *outp = out + so;
+#pragma unroll 1
+    for (int l = 0; l < LOGF; ++l) {
+        const int npairs = F >> (l + 1);
+        // window table: lane p < npairs owns pair p
+        int ps = 0, pe = 0, nw = 0;
+        if (t < npairs) {
+            ps = soff[t << (l + 1)];
+            pe = soff[(t + 1) << (l + 1)];
+            nw = (pe - ps + WK - 1) / WK;
+        }
+        int incl = nw;
+        for (int o = 1; o < 32; o <<= 1) {
+            const int v = __shfl_up(incl, o);
+            if (t >= o) incl += v;
+        }
+        const int nwin = __builtin_amdgcn_readlane(incl, 31);
+        const bool last = l + 1 == LOGF;
+        // parameters of this wave's windows (wave-uniform, in SGPRs)
+        int wps[MAXWIN], wpm[MAXWIN], wpe[MAXWIN], wd0[MAXWIN], wreal[MAXWIN];
+#pragma unroll
+        for (int h = 0; h < MAXWIN; ++h) {
+            const int k = w + h * WAVES;
+            wreal[h] = 0;
+            wps[h] = wpm[h] = wpe[h] = wd0[h] = 0;
+            if (k < nwin) {
+                const unsigned long long below = __ballot(t < npairs && incl <= k);
+                const int p = __builtin_amdgcn_readfirstlane(__popcll(below));  // pair of window k
+                const int pps = __builtin_amdgcn_readlane(ps, p);
+                const int ppe = __builtin_amdgcn_readlane(pe, p);
+                const int first = __builtin_amdgcn_readlane(incl - nw, p);
+                const int d0 = (k - first) * WK;
+                wps[h] = pps;
+                wpe[h] = ppe;
+                wpm[h] = __builtin_amdgcn_readfirstlane(soff[(2 * p + 1) << l]);
+                wd0[h] = d0;
+                wreal[h] = ppe - pps - d0 < WK ? ppe - pps - d0 : WK;
+            }
+        }
+        int x[MAXWIN][R];
+#pragma unroll
+        for (int h = 0; h < MAXWIN; ++h) {
+            if (wreal[h] > 0)
+                merge_window(s, wps[h], wpm[h] - wps[h], wpm[h], wpe[h] - wpm[h], wd0[h], wreal[h],
+                             x[h], c0, c1, c2, c3);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int h = 0; h < MAXWIN; ++h) {
+            if (wreal[h] > 0) {
+                const Window win{wps[h] + wd0[h], wreal[h]};
+                if (last) store_window_global(outp, win, total, x[h]);
+                else store_window_lds(s, win, x[h]);
+            }
+        }
+        if (!last) __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Host side
+// ------------------------------------------------------------------------------------------
+static inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
+static int ceil_log2(uint64_t x) {
+    int p = 0;
+    while ((1ull << p) < x) ++p;
+    return p;
+}
+static int max_logf() {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("DSORT_MAX_LOGF");
+        int x = e ? atoi(e) : 4;
+        v = x < 1 ? 1 : (x > kWaveMaxLogF ? kWaveMaxLogF : x);
+    }
+    return v;
+}
+static std::vector<int> plan_passes(uint64_t runs) {
+    std::vector<int> out;
+    const int bits = ceil_log2(runs);
+    if (bits == 0) return out;
+    const int cap = max_logf();
+    const int P = (bits + cap - 1) / cap;
+    for (int p = 0; p < P; ++p) out.push_back(bits / P + (p < bits % P ? 1 : 0));
+    return out;
+}
+
+template <bool REG>
+static int launch_pass_w(dsort_ctx *ctx, const int *src, int *dst, const PassDesc &pd, int logf,
+                         uint64_t ntiles, hipStream_t s, bool timed) {
+    int rc = ensure(ctx, &ctx->splits, &ctx->splits_bytes,
+                    (size_t)(ntiles + 1) * (size_t)(1 << logf) * sizeof(uint32_t), "split vectors");
+    if (rc) return rc;
+    uint32_t *sp = static_cast<uint32_t *>(ctx->splits);
+    hipLaunchKernelGGL((partk_kernel<int32_t, REG>), dim3((unsigned)ceil_div(ntiles, 4)), dim3(256), 0,
+                       s, src, pd, TNOM, SLACK, sp, ntiles);
+    DSORT_HIP(ctx, hipGetLastError());
+    const bool kt = timed && ctx->ev_ok && ctx->kev_used + 2 <= dsort_ctx::kMaxKev;
+    if (kt) DSORT_HIP(ctx, hipEventRecord(ctx->kev[ctx->kev_used], s));
+    const dim3 grid((unsigned)ntiles), block(THREADS);
+    switch (logf) {
+        case 1: hipLaunchKernelGGL((mergew_kernel<1, REG>), grid, block, 0, s, src, dst, pd, TNOM, sp); break;
+        case 2: hipLaunchKernelGGL((mergew_kernel<2, REG>), grid, block, 0, s, src, dst, pd, TNOM, sp); break;
+        case 3: hipLaunchKernelGGL((mergew_kernel<3, REG>), grid, block, 0, s, src, dst, pd, TNOM, sp); break;
+        case 4: hipLaunchKernelGGL((mergew_kernel<4, REG>), grid, block, 0, s, src, dst, pd, TNOM, sp); break;
+        case 5: hipLaunchKernelGGL((mergew_kernel<5, REG>), grid, block, 0, s, src, dst, pd, TNOM, sp); break;
+        default: return set_err(ctx, DSORT_EINVAL, "bad pass fan-in");
+    }
+    DSORT_HIP(ctx, hipGetLastError());
+    if (kt) {
+        DSORT_HIP(ctx, hipEventRecord(ctx->kev[ctx->kev_used + 1], s));
+        ctx->kev_used += 2;
+    }
+    return DSORT_OK;
+}
+
+}  // namespace wv
+
+int wave_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys, size_t n, hipStream_t s,
+                  bool timed) {
+    using namespace wv;
+    ctx->stats = dsort_stats{};
+    ctx->stats.keys_in = n;
+    ctx->stats.keys_out = n;
+    ctx->stats.tile_keys = TILE;
+    ctx->ev_mask = 0;
+    ctx->kev_used = 0;
+    ctx->last_stream = s;
+    if (n < 2) {
+        if (n == 1 && d_in != d_keys)
+            DSORT_HIP(ctx, hipMemcpyAsync(d_keys, d_in, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+        return DSORT_OK;
+    }
+    const uint64_t tiles = ceil_div(n, TILE);
+    const std::vector<int> plan = plan_passes(tiles);
+    const int passes = (int)plan.size();
+    ctx->stats.merge_passes = passes;
+    int32_t *scratch = nullptr;
+    if (passes > 0) {
+        int rc = ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, n * sizeof(int32_t), "sort scratch");
+        if (rc) return rc;
+        scratch = static_cast<int32_t *>(ctx->scratch);
+    }
+    int32_t *bufs[2] = {d_keys, scratch};
+    int cur = (passes % 2 == 0) ? 0 : 1;
+    if (timed && ctx->ev_ok) {
+        DSORT_HIP(ctx, hipEventRecord(ctx->ev[0], s));
+        ctx->ev_mask |= 1u;
+    }
+    hipLaunchKernelGGL(block_sort_w_kernel, dim3((unsigned)tiles), dim3(THREADS), 0, s, d_in,
+                       bufs[cur], (uint64_t)n);
+    DSORT_HIP(ctx, hipGetLastError());
+    if (timed && ctx->ev_ok) {
+        DSORT_HIP(ctx, hipEventRecord(ctx->ev[1], s));
+        ctx->ev_mask |= 2u;
+    }
+    uint64_t Rr = TILE;
+    for (int p = 0; p < passes; ++p) {
+        PassDesc pd{(uint64_t)n, Rr, 1 << plan[p], 0, nullptr};
+        const uint64_t gsize = Rr << plan[p];
+        const uint64_t ngroups = ceil_div(n, gsize);
+        const uint64_t tpg = ceil_div(gsize, (uint64_t)TNOM);
+        const uint64_t mtiles = (ngroups - 1) * tpg + ceil_div(n - (ngroups - 1) * gsize, (uint64_t)TNOM);
+        int rc = launch_pass_w<true>(ctx, bufs[cur], bufs[cur ^ 1], pd, plan[p], mtiles, s, timed);
+        if (rc) return rc;
+        Rr <<= plan[p];
+        cur ^= 1;
+    }
+    if (timed && ctx->ev_ok) {
+        DSORT_HIP(ctx, hipEventRecord(ctx->ev[2], s));
+        ctx->ev_mask |= 4u;
+    }
+    return DSORT_OK;
+}
+
+int wave_merge_i32(dsort_ctx *ctx, const int32_t *d_in, const size_t *lens, int k, int32_t *d_out,
+                   hipStream_t s) {
+    using namespace wv;
+    constexpr int MAXF = 1 << kWaveMaxLogF;
+    ctx->stats = dsort_stats{};
+    ctx->last_stream = s;
+    ctx->kev_used = 0;
+    uint64_t n = 0;
+    std::vector<uint64_t> rl(lens, lens + k);
+    for (int j = 0; j < k; ++j) n += lens[j];
+    ctx->stats.keys_in = ctx->stats.keys_out = n;
+    ctx->stats.tile_keys = TILE;
+    if (n == 0) return DSORT_OK;
+    if (k == 1) {
+        DSORT_HIP(ctx, hipMemcpyAsync(d_out, d_in, n * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+        return DSORT_OK;
+    }
+    int levels = 0;
+    for (uint64_t r = (uint64_t)k; r > 1; r = ceil_div(r, MAXF)) ++levels;
+    ctx->stats.merge_passes = levels;
+    int rc;
+    if (levels > 1) {
+        rc = ensure(ctx, &ctx->scratch2, &ctx->scratch2_bytes, n * sizeof(int32_t), "merge scratch");
+        if (rc) return rc;
+    }
+    int32_t *dsts[2] = {d_out, static_cast<int32_t *>(ctx->scratch2)};
+    int which = (levels % 2 == 1) ? 0 : 1;
+    const int32_t *src = d_in;
+    if (!ctx->groups_ev && hipEventCreateWithFlags(&ctx->groups_ev, hipEventDisableTiming) != hipSuccess)
+        return set_err(ctx, DSORT_EHIP, "hipEventCreate");
+    for (int l = 0; l < levels; ++l) {
+        const int nr = (int)rl.size();
+        const int per = nr < MAXF ? nr : MAXF;
+        const int logf = ceil_log2((uint64_t)per) < 1 ? 1 : ceil_log2((uint64_t)per);
+        const int ng = (nr + MAXF - 1) / MAXF;
+        const size_t gbytes = (size_t)ng * sizeof(GroupK);
+        if (ctx->groups_ev_pending) DSORT_HIP(ctx, hipEventSynchronize(ctx->groups_ev));
+        ctx->groups_ev_pending = false;
+        if (ctx->groups_host_bytes < gbytes) {
+            if (ctx->groups_host) (void)hipHostFree(ctx->groups_host);
+            ctx->groups_host = nullptr;
+            ctx->groups_host_bytes = 0;
+            DSORT_HIP(ctx, hipHostMalloc(&ctx->groups_host, gbytes, hipHostMallocDefault));
+            ctx->groups_host_bytes = gbytes;
+        }
+        rc = ensure(ctx, &ctx->groups, &ctx->groups_bytes, gbytes, "group table");
+        if (rc) return rc;
+        GroupK *gh = static_cast<GroupK *>(ctx->groups_host);
+        std::vector<uint64_t> next;
+        uint64_t base = 0, tiles = 0;
+        for (int gi = 0; gi < ng; ++gi) {
+            GroupK &gk = gh[gi];
+            gk.base = base;
+            gk.first_tile = tiles;
+            gk.nruns = 0;
+            gk.pad = 0;
+            uint64_t tot = 0;
+            gk.roff[0] = 0;
+            for (int r = gi * MAXF; r < nr && r < (gi + 1) * MAXF; ++r) {
+                tot += rl[r];
+                gk.roff[++gk.nruns] = tot;
+            }
+            for (int r = (int)gk.nruns + 1; r <= kMaxF; ++r) gk.roff[r] = tot;
+            gk.total = tot;
+            tiles += ceil_div(tot, (uint64_t)TNOM);
+            base += tot;
+            next.push_back(tot);
+        }
+        DSORT_HIP(ctx, hipMemcpyAsync(ctx->groups, gh, gbytes, hipMemcpyHostToDevice, s));
+        DSORT_HIP(ctx, hipEventRecord(ctx->groups_ev, s));
+        ctx->groups_ev_pending = true;
+        PassDesc pd{n, 0, 1 << logf, ng, static_cast<const GroupK *>(ctx->groups)};
+        int32_t *dst = dsts[which];
+        rc = launch_pass_w<false>(ctx, src, dst, pd, logf, tiles, s, false);
+        if (rc) return rc;
+        rl.swap(next);
+        src = dst;
+        which ^= 1;
+    }
+    return DSORT_OK;
+}
+
+}  // namespace dsort
