@@ -62,6 +62,23 @@ constexpr int ROW_HMIRROR = 0x141; // lane ^ 7
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
+#ifdef DSORT_STAMPS
+// Diagnostic build only: per-workgroup phase timestamps of mergew (s_memtime), read back by
+// dsort_debug_stamps().  Stamp k of workgroup b at g_stamps[b * 32 + k] (wave 0, lane 0) and the
+// wave-15 view at +16.
+constexpr int kStampTiles = 1 << 17;
+__device__ unsigned long long g_stamps[kStampTiles * 32];
+#define STAMP(k)                                                                              \
+    do {                                                                                      \
+        if ((threadIdx.x & 63) == 0 && (threadIdx.x >> 6) % 15 == 0 && blockIdx.x < kStampTiles) \
+            g_stamps[blockIdx.x * 32 + (threadIdx.x >> 6 ? 16 : 0) + (k)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define STAMP(k) \
+    do {         \
+    } while (0)
+#endif
+
 // median of three: with c = -inf it is min(a, b), with c = +inf max(a, b)
 __device__ __forceinline__ int med3(int a, int b, int c) {
     int r;
@@ -74,10 +91,18 @@ __device__ __forceinline__ int dpp(int x) {
     return __builtin_amdgcn_mov_dpp(x, CTRL, 0xF, 0xF, false);
 }
 
-// value of lane ^ 4: two bank-masked row shifts (banks 0,2 read +4, banks 1,3 read -4)
-__device__ __forceinline__ int dpp_xor4(int x) {
-    const int p = __builtin_amdgcn_mov_dpp(x, ROW_SHL4, 0xF, 0x5, false);
-    return __builtin_amdgcn_update_dpp(p, x, ROW_SHR4, 0xF, 0xA, false);
+
+// compare-exchange with lane ^ 4: lanes in banks 0,2 (bit 2 clear) keep the min, banks 1,3 the
+// max; the DPP source of each half is the other half (row_shl:4 / row_shr:4)
+__device__ __forceinline__ int cex_xor4(int x) {
+    int y;
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_min_i32_dpp %0, %1, %1 row_shl:4 row_mask:0xf bank_mask:0x5\n\t"
+        "v_max_i32_dpp %0, %1, %1 row_shr:4 row_mask:0xf bank_mask:0xa"
+        : "=&v"(y)
+        : "v"(x));
+    return y;
 }
 
 __device__ __forceinline__ void cex(int &a, int &b) {
@@ -135,7 +160,7 @@ __device__ __forceinline__ void merge_net(int (&x)[R], int c0, int c1, int c2, i
 #pragma unroll
     for (int i = 0; i < R; ++i) x[i] = med3(x[i], dpp<ROW_ROR8>(x[i]), c3);
 #pragma unroll
-    for (int i = 0; i < R; ++i) x[i] = med3(x[i], dpp_xor4(x[i]), c2);
+    for (int i = 0; i < R; ++i) x[i] = cex_xor4(x[i]);
 #pragma unroll
     for (int i = 0; i < R; ++i) x[i] = med3(x[i], dpp<QP_2301>(x[i]), c1);
 #pragma unroll
@@ -177,7 +202,7 @@ __device__ __forceinline__ void hc_lane_major(int (&x)[R], const int (&c)[6]) {
         for (int i = 0; i < R; ++i) x[i] = med3(x[i], dpp<QP_2301>(x[i]), c[1]);
     } else if constexpr (B == 6) {
 #pragma unroll
-        for (int i = 0; i < R; ++i) x[i] = med3(x[i], dpp_xor4(x[i]), c[2]);
+        for (int i = 0; i < R; ++i) x[i] = cex_xor4(x[i]);
     } else if constexpr (B == 7) {
 #pragma unroll
         for (int i = 0; i < R; ++i) x[i] = med3(x[i], dpp<ROW_ROR8>(x[i]), c[3]);
@@ -234,48 +259,74 @@ __device__ __forceinline__ void sort_wave(int (&x)[R], const int (&c)[6]) {
 // ------------------------------------------------------------------------------------------
 // LDS levels
 // ------------------------------------------------------------------------------------------
-// Merge-path split: number of A keys among the first d outputs of merge(A, B), A first on ties
-// (A = s[pa, pa+na), B = s[pb, pb+nb)).  All lanes of the wave cooperate: each step probes 64
-// candidates at an odd stride (distinct LDS banks) and keeps the bracket the ballot points to.
-__device__ __forceinline__ int coop_split(const int *s, int pa, int na, int pb, int nb, int d) {
-    int lo = d > nb ? d - nb : 0;
-    int hi = d < na ? d : na;
-    const int lane = lane_id();
-#pragma unroll 1
-    while (lo < hi) {
-        const int len = hi - lo;
-        const int step = ((len + 63) >> 6) | 1;
-        const int a = lo + lane * step;
-        bool q = true;
-        if (a < hi) q = s[pa + a] > s[pb + d - 1 - a];
-        const unsigned long long m = __ballot(q);
-        const int j = m ? (int)__ffsll((long long)m) - 1 : 64;
-        const int nhi = lo + j * step < hi ? lo + j * step : hi;
-        lo = j ? lo + (j - 1) * step + 1 : lo;
-        hi = nhi;
-        lo = __builtin_amdgcn_readfirstlane(lo);
-        hi = __builtin_amdgcn_readfirstlane(hi);
-    }
-    return lo;
+// Merge-path splits of a window: numbers of A keys among the first d0 and d1 outputs of
+// merge(A, B), A first on ties (A = s[pa, pa+na), B = s[pb, pb+nb); all arguments wave-uniform).
+// All lanes of the wave cooperate: each step probes 64 candidates per split at an odd stride
+// (distinct LDS banks), and the ballot of "A[a] > B[d-1-a]" brackets the split 64x tighter; the
+// two searches advance together.
+__device__ __forceinline__ int split_step(const int *s, int pa, int pb, int d, int lane, int &lo,
+                                          int &hi) {
+    // one 64-ary step of one search; returns 1 while the bracket is still open
+    if (lo >= hi) return 0;
+    const int len = hi - lo;
+    const int st = ((len + 63) >> 6) | 1;
+    const int off = lane * st;
+    bool q = true;
+    if (off < len) q = s[pa + lo + off] > s[pb + d - 1 - lo - off];
+    const unsigned long long m = __ballot(q);
+    const int j = m ? (int)__ffsll((long long)m) - 1 : 64;
+    const int nhi = lo + j * st < hi ? lo + j * st : hi;
+    lo = j ? lo + (j - 1) * st + 1 : lo;
+    hi = nhi;
+    return 1;
 }
 
-// Loads the bitonic window (reg-major): elements [0, qa) = A ascending from s[abase],
-// [qa, qa+pad) = +inf, [qa+pad, 1024) = B descending ending at s[bbase - 1023 + ...]:
-// element e >= qa+pad is s[bbase - e].  qa, pad are wave-uniform.
-__device__ __forceinline__ void load_window(const int *s, int abase, int bbase, int qa, int pad,
+__device__ __forceinline__ void coop_split2(const int *s, int pa, int na, int pb, int nb, int d0,
+                                            int d1, int &r0, int &r1) {
+    int lo0 = d0 > nb ? d0 - nb : 0, hi0 = d0 < na ? d0 : na;
+    int lo1 = d1 > nb ? d1 - nb : 0, hi1 = d1 < na ? d1 : na;
+    const int lane = lane_id();
+#pragma unroll 1
+    while (lo0 < hi0 || lo1 < hi1) {
+        split_step(s, pa, pb, d0, lane, lo0, hi0);
+        split_step(s, pa, pb, d1, lane, lo1, hi1);
+        lo0 = __builtin_amdgcn_readfirstlane(lo0);
+        hi0 = __builtin_amdgcn_readfirstlane(hi0);
+        lo1 = __builtin_amdgcn_readfirstlane(lo1);
+        hi1 = __builtin_amdgcn_readfirstlane(hi1);
+    }
+    r0 = lo0;
+    r1 = lo1;
+}
+
+// A window of a merge level: outputs [d0, d0 + wreal) of merge(A = s[pa, pa+na),
+// B = s[pb, pb+nb)) land at tile positions [obase, obase + wreal).  Wave-uniform.
+struct Win {
+    int pa, na, pb, nb, d0, wreal;
+};
+
+// Loads the bitonic window (reg-major, element e = 64 i + t in x[i]): [0, qa) = A ascending,
+// [qa, qa+pad) = +inf, [qa+pad, 1024) = B descending.  qa and pad are wave-uniform, so every
+// register but the one or two that straddle a boundary is a plain LDS read at an immediate
+// offset from one of two per-lane bases.
+__device__ __forceinline__ void load_window(const int *s, int a_first, int b_last, int qa, int pad,
                                             int (&x)[R]) {
+    // a_first: LDS index of element 0 (A[a0]); element e of the B part is s[b_last - e]
+    // (b_last = index of B[b0] + 1023)
     const int t = lane_id();
     const int qp = qa + pad;
+    const int *sa = s + a_first + t;                    // element 64 i + t of A: sa[64 i]
+    const int *sb = s + b_last - t - 64 * (R - 1);      // element 64 i + t of B: sb[64 (15 - i)]
 #pragma unroll
     for (int i = 0; i < R; ++i) {
         const int e0 = 64 * i;
         if (e0 + 64 <= qa) {
-            x[i] = s[abase + e0 + t];
+            x[i] = sa[64 * i];
         } else if (e0 >= qp) {
-            x[i] = s[bbase - e0 - t];
+            x[i] = sb[64 * (R - 1 - i)];
         } else {
             const int e = e0 + t;
-            int idx = e < qa ? abase + e : bbase - e;
+            int idx = e < qa ? a_first + e : b_last - e;
             idx = idx < 0 ? 0 : (idx > TILE - 1 ? TILE - 1 : idx);
             const int v = s[idx];
             x[i] = (e >= qa && e < qp) ? KMAX : v;
@@ -283,53 +334,46 @@ __device__ __forceinline__ void load_window(const int *s, int abase, int bbase, 
     }
 }
 
-struct Window {
-    int obase;  // output position of element 0 (within the tile)
-    int wreal;  // real keys in the window (the rest are +inf padding)
-};
-
-// Merges the window of outputs [d0, d0 + wreal) of the pair A = s[pa, pa+na), B = s[pb, pb+nb)
-// into registers (layout of merge_net).
-__device__ __forceinline__ void merge_window(const int *s, int pa, int na, int pb, int nb, int d0,
-                                             int wreal, int (&x)[R], int c0, int c1, int c2,
-                                             int c3) {
-    const int a0 = coop_split(s, pa, na, pb, nb, d0);
-    const int a1 = coop_split(s, pa, na, pb, nb, d0 + wreal);
-    const int b0 = d0 - a0, b1 = d0 + wreal - a1;
+// Merges window w into registers (layout of merge_net).
+__device__ __forceinline__ void merge_window(const int *s, const Win &w, int (&x)[R], int c0,
+                                             int c1, int c2, int c3) {
+    int a0, a1;
+    coop_split2(s, w.pa, w.na, w.pb, w.nb, w.d0, w.d0 + w.wreal, a0, a1);
+#ifdef DSORT_ABL_SPLIT2  // ablation: a second, discarded split search (marginal cost)
+    {
+        int z0, z1;
+        coop_split2(s, w.pa, w.na, w.pb, w.nb, w.d0 + 1, w.d0 + w.wreal - 1, z0, z1);
+        asm volatile("" ::"s"(z0), "s"(z1));
+    }
+#endif
+    const int b0 = w.d0 - a0;
     const int qa = a1 - a0;
-    const int pad = WK - wreal;
-    (void)b1;
-    load_window(s, pa + a0 + 0, pb + b0 + (WK - 1) - 0, qa, pad, x);
+    load_window(s, w.pa + a0, w.pb + b0 + (WK - 1), qa, WK - w.wreal, x);
+#ifdef DSORT_ABL_NET2  // ablation: a second, discarded network (marginal cost)
+    {
+        int z[R];
+#pragma unroll
+        for (int i = 0; i < R; ++i) z[i] = x[i] ^ i;
+        merge_net(z, c0, c1, c2, c3);
+#pragma unroll
+        for (int i = 0; i < R; ++i) asm volatile("" ::"v"(z[i]));
+    }
+#endif
     merge_net(x, c0, c1, c2, c3);
 }
 
-__device__ __forceinline__ void store_window_lds(int *s, const Window &w, const int (&x)[R]) {
-    const int base = w.obase + out_lo(lane_id());
-    if (w.wreal == WK) {
-#pragma unroll
-        for (int i = 0; i < R; ++i) s[base + out_hi(i)] = x[i];
-    } else {
-        const int lo = out_lo(lane_id());
-#pragma unroll
-        for (int i = 0; i < R; ++i)
-            if (out_hi(i) + lo < w.wreal) s[base + out_hi(i)] = x[i];
-    }
-}
-
-__device__ __forceinline__ void store_window_global(int *out, const Window &w, int limit,
-                                                    const int (&x)[R]) {
-    // writes positions [obase, obase + min(wreal, limit - obase)) of the tile
-    const int lo = out_lo(lane_id());
-    int *p = out + w.obase + lo;
-    int lim = limit - w.obase;
-    lim = lim < w.wreal ? lim : w.wreal;
-    if (lim >= WK) {
+// Stores a merged window (merge_net layout) at tile positions [obase, obase + wreal) of `dst`
+// (LDS or global); `lo` = out_lo(lane).
+template <typename P>
+__device__ __forceinline__ void store_window(P *dst, int obase, int wreal, int lo, const int (&x)[R]) {
+    P *p = dst + obase + lo;
+    if (wreal >= WK) {
 #pragma unroll
         for (int i = 0; i < R; ++i) p[out_hi(i)] = x[i];
     } else {
 #pragma unroll
         for (int i = 0; i < R; ++i)
-            if (out_hi(i) + lo < lim) p[out_hi(i)] = x[i];
+            if (out_hi(i) + lo < wreal) p[out_hi(i)] = x[i];
     }
 }
 
@@ -377,18 +421,20 @@ __global__ void __launch_bounds__(THREADS, 8) block_sort_w_kernel(const int *in,
         for (int q = 0; q < R / 4; ++q) dst[q] = make_int4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
     }
     __syncthreads();
+    const int lo = out_lo(t);
 #pragma unroll 1
     for (int r = WK; r < TILE; r <<= 1) {
         const int wpp = (2 * r) / WK;  // windows per pair
         const int j = w / wpp, o = w % wpp;
         const int ps = j * 2 * r;
-        merge_window(s, ps, r, ps + r, r, o * WK, WK, x, c[0], c[1], c[2], c[3]);
-        const Window win{ps + o * WK, WK};
+        const Win win{ps, r, ps + r, r, o * WK, WK};
+        merge_window(s, win, x, c[0], c[1], c[2], c[3]);
         __syncthreads();
         if (2 * r == TILE) {
-            store_window_global(out + base, win, valid, x);
+            const int lim = valid - (ps + o * WK);
+            if (lim > 0) store_window(out + base, ps + o * WK, lim, lo, x);
         } else {
-            store_window_lds(s, win, x);
+            store_window(s, ps + o * WK, WK, lo, x);
             __syncthreads();
         }
     }
@@ -408,13 +454,18 @@ __global__ void __launch_bounds__(THREADS, 8) mergew_kernel(const int *__restric
     __shared__ __attribute__((aligned(16))) int s[TILE];
     __shared__ int soff[F + 1];
     __shared__ int64_t gdelta[F];        // global index of tile key e in segment sg = gdelta[sg] + e
-    __shared__ uint8_t chunkseg[NCHUNK + 1];
+    __shared__ int64_t cbase[NCHUNK];    // chunk c inside one segment: key 64c + i at cbase[c] + i
+    __shared__ uint8_t cseg[NCHUNK];     // segment of key 64c
+    __shared__ uint8_t cmix[NCHUNK];     // chunk c spans a segment boundary
     __shared__ uint64_t s_out;
     __shared__ int s_total;
+    __shared__ int4 wtab_a[LOGF][WAVES * MAXWIN];  // per level and window: pa, na, pb, nb
+    __shared__ int2 wtab_b[LOGF][WAVES * MAXWIN];  // d0, wreal (0 = no window)
 
     const int t = lane_id();
     const int w = threadIdx.x >> 6;
     const uint64_t j = blockIdx.x;
+    STAMP(0);
     TileInfo ti;
     const GroupK *g = tile_info<REG>(pd, j, tnom, ti);
     if (threadIdx.x < 64) {
@@ -442,9 +493,11 @@ __global__ void __launch_bounds__(THREADS, 8) mergew_kernel(const int *__restric
         }
     }
     __syncthreads();
+    STAMP(1);
     const int total = __builtin_amdgcn_readfirstlane(s_total);
-    // segment of the first key of every 64-key chunk
-    if (threadIdx.x <= NCHUNK) {
+    const uint64_t sstart0 = ti.base;  // a key index that exists (loads past `total` read it)
+    // per 64-key chunk: the segment of its first key, and whether its keys span segments
+    if (threadIdx.x < NCHUNK) {
         const int e = threadIdx.x * 64;
         int lo = 0, hi = F - 1;  // last segment starting at or before e
         while (lo < hi) {
@@ -452,92 +505,139 @@ __global__ void __launch_bounds__(THREADS, 8) mergew_kernel(const int *__restric
             if (soff[mid] <= e) lo = mid;
             else hi = mid - 1;
         }
-        chunkseg[threadIdx.x] = (uint8_t)lo;
+        cseg[threadIdx.x] = (uint8_t)lo;
+        cbase[threadIdx.x] = gdelta[lo] + e;
+        const int eend = e + 63 < total ? e + 63 : total - 1;
+        cmix[threadIdx.x] = (lo < F - 1 && soff[lo + 1] <= eend) ? 1 : 0;
     }
     __syncthreads();
+    STAMP(2);
+    // Window table of every level, built once by wave 0 from the segment offsets alone (they do
+    // not depend on the keys): level l merges pairs of 2^l-segment groups; pair p is cut into
+    // ceil(len / 1024) windows; window k of the level goes to wave k % 16 (k < 16 * MAXWIN).
+    if (w == 0) {
+#pragma unroll 1
+        for (int l = 0; l < LOGF; ++l) {
+            const int npairs = F >> (l + 1);
+            int ps = 0, pm = 0, pe = 0, nw = 0;
+            if (t < npairs) {
+                ps = soff[t << (l + 1)];
+                pm = soff[((2 * t + 1) << l)];
+                pe = soff[(t + 1) << (l + 1)];
+                nw = (pe - ps + WK - 1) / WK;
+            }
+            int incl = nw;
+            for (int o = 1; o < 16; o <<= 1) {
+                const int v = __shfl_up(incl, o);
+                if (t >= o) incl += v;
+            }
+            // lane k (< WAVES * MAXWIN) describes window k: its pair is the number of pairs whose
+            // windows all come before k
+            int p = 0;
+            for (int q = 0; q < npairs; ++q) p += __builtin_amdgcn_readlane(incl, q) <= t ? 1 : 0;
+            const int pp = p < npairs ? p : 0;
+            const int fps = __shfl(ps, pp), fpm = __shfl(pm, pp), fpe = __shfl(pe, pp);
+            const int first = __shfl(incl - nw, pp);
+            if (t < WAVES * MAXWIN) {
+                int4 a;
+                int2 b;
+                if (p < npairs) {
+                    const int d0 = (t - first) * WK;
+                    const int len = fpe - fps;
+                    a = make_int4(fps, fpm - fps, fpm, fpe - fpm);
+                    b = make_int2(d0, len - d0 < WK ? len - d0 : WK);
+                } else {
+                    a = make_int4(0, 0, 0, 0);
+                    b = make_int2(0, 0);  // no window
+                }
+                wtab_a[l][t] = a;
+                wtab_b[l][t] = b;
+            }
+        }
+    }
     // Staging: key e of the tile is loaded by thread e % THREADS (coalesced within a segment).
-    // The segments a wave's 64 consecutive keys touch are known per chunk, so the segment of a
-    // key costs no divergent search; all 16 loads are in flight before the LDS stores.
+    // A chunk inside one segment addresses its keys as cbase + lane; only the rare chunk that
+    // spans a segment boundary looks its segment up.  Addresses are formed first and all 16
+    // loads issued unconditionally (branch joins with loads in flight would serialize them).
     {
         int v[R];
 #pragma unroll
         for (int k = 0; k < R; ++k) {
             const int e = threadIdx.x + k * THREADS;
             const int c = w + k * WAVES;
-            const int first = __builtin_amdgcn_readfirstlane((int)chunkseg[c]);
-            const int lastc = __builtin_amdgcn_readfirstlane((int)chunkseg[c + 1]);
-            int sg = first;
-            for (int q = first + 1; q <= lastc; ++q) sg += soff[q] <= e ? 1 : 0;
-            const int64_t gi = gdelta[sg] + e;
-            v[k] = e < total ? in[gi] : 0;
+            int64_t gi;
+            if (__builtin_amdgcn_readfirstlane((int)cmix[c])) {
+                const int first = __builtin_amdgcn_readfirstlane((int)cseg[c]);
+                int sg = first;
+#pragma unroll 1
+                for (int q = first + 1; q < F; ++q) {
+                    const int so = __builtin_amdgcn_readfirstlane(soff[q]);
+                    if (so > c * 64 + 63) break;
+                    sg += so <= e ? 1 : 0;
+                }
+                gi = gdelta[sg] + e;
+            } else {
+                const int64_t cb = cbase[c];
+                const int64_t cbu = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(cb >> 32)) << 32) |
+                                              (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)cb));
+                gi = cbu + t;
+            }
+            if (c * 64 + 64 > total) gi = e < total ? gi : (int64_t)sstart0;  // wave-uniform test
+#ifdef DSORT_ABL_STAGE2  // ablation: a second, discarded load of the key (marginal cost)
+            {
+                const int z = in[gi & ~(int64_t)1];
+                asm volatile("" ::"v"(z));
+            }
+#endif
+            v[k] = in[gi];
         }
 #pragma unroll
         for (int k = 0; k < R; ++k) {
             const int e = threadIdx.x + k * THREADS;
-            if (e < total) s[e] = v[k];
+            if ((w + k * WAVES) * 64 + 64 <= total) s[e] = v[k];
+            else if (e < total) s[e] = v[k];
         }
     }
+    STAMP(3);
     __syncthreads();
+    STAMP(4);
 
     const int c0 = lane_side(0), c1 = lane_side(1), c2 = lane_side(2), c3 = lane_side(3);
+    const int lo = out_lo(t);
     const uint64_t so = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(s_out >> 32)) << 32) |
                         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)s_out);
     int *outp = out + so;
 #pragma unroll 1
     for (int l = 0; l < LOGF; ++l) {
-        const int npairs = F >> (l + 1);
-        // window table: lane p < npairs owns pair p
-        int ps = 0, pe = 0, nw = 0;
-        if (t < npairs) {
-            ps = soff[t << (l + 1)];
-            pe = soff[(t + 1) << (l + 1)];
-            nw = (pe - ps + WK - 1) / WK;
-        }
-        int incl = nw;
-        for (int o = 1; o < 32; o <<= 1) {
-            const int v = __shfl_up(incl, o);
-            if (t >= o) incl += v;
-        }
-        const int nwin = __builtin_amdgcn_readlane(incl, 31);
         const bool last = l + 1 == LOGF;
-        // parameters of this wave's windows (wave-uniform, in SGPRs)
-        int wps[MAXWIN], wpm[MAXWIN], wpe[MAXWIN], wd0[MAXWIN], wreal[MAXWIN];
+        Win win[MAXWIN];
 #pragma unroll
         for (int h = 0; h < MAXWIN; ++h) {
-            const int k = w + h * WAVES;
-            wreal[h] = 0;
-            wps[h] = wpm[h] = wpe[h] = wd0[h] = 0;
-            if (k < nwin) {
-                const unsigned long long below = __ballot(t < npairs && incl <= k);
-                const int p = __builtin_amdgcn_readfirstlane(__popcll(below));  // pair of window k
-                const int pps = __builtin_amdgcn_readlane(ps, p);
-                const int ppe = __builtin_amdgcn_readlane(pe, p);
-                const int first = __builtin_amdgcn_readlane(incl - nw, p);
-                const int d0 = (k - first) * WK;
-                wps[h] = pps;
-                wpe[h] = ppe;
-                wpm[h] = __builtin_amdgcn_readfirstlane(soff[(2 * p + 1) << l]);
-                wd0[h] = d0;
-                wreal[h] = ppe - pps - d0 < WK ? ppe - pps - d0 : WK;
-            }
+            const int4 a = wtab_a[l][w + h * WAVES];
+            const int2 b = wtab_b[l][w + h * WAVES];
+            win[h].pa = __builtin_amdgcn_readfirstlane(a.x);
+            win[h].na = __builtin_amdgcn_readfirstlane(a.y);
+            win[h].pb = __builtin_amdgcn_readfirstlane(a.z);
+            win[h].nb = __builtin_amdgcn_readfirstlane(a.w);
+            win[h].d0 = __builtin_amdgcn_readfirstlane(b.x);
+            win[h].wreal = __builtin_amdgcn_readfirstlane(b.y);
         }
         int x[MAXWIN][R];
 #pragma unroll
-        for (int h = 0; h < MAXWIN; ++h) {
-            if (wreal[h] > 0)
-                merge_window(s, wps[h], wpm[h] - wps[h], wpm[h], wpe[h] - wpm[h], wd0[h], wreal[h],
-                             x[h], c0, c1, c2, c3);
-        }
+        for (int h = 0; h < MAXWIN; ++h)
+            if (win[h].wreal > 0) merge_window(s, win[h], x[h], c0, c1, c2, c3);
+        STAMP(5 + 2 * l);
         __syncthreads();
 #pragma unroll
         for (int h = 0; h < MAXWIN; ++h) {
-            if (wreal[h] > 0) {
-                const Window win{wps[h] + wd0[h], wreal[h]};
-                if (last) store_window_global(outp, win, total, x[h]);
-                else store_window_lds(s, win, x[h]);
+            if (win[h].wreal > 0) {
+                const int ob = win[h].pa + win[h].d0;
+                if (last) store_window(outp, ob, win[h].wreal, lo, x[h]);
+                else store_window(s, ob, win[h].wreal, lo, x[h]);
             }
         }
         if (!last) __syncthreads();
+        STAMP(6 + 2 * l);
     }
 }
 
@@ -599,6 +699,12 @@ static int launch_pass_w(dsort_ctx *ctx, const int *src, int *dst, const PassDes
 }
 
 }  // namespace wv
+
+#ifdef DSORT_STAMPS
+extern "C" int dsort_debug_stamps(void *host, size_t bytes) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(wv::g_stamps), bytes) == hipSuccess ? 0 : -1;
+}
+#endif
 
 int wave_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys, size_t n, hipStream_t s,
                   bool timed) {

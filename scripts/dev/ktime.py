@@ -1,0 +1,33 @@
+#!/usr/bin/env python3
+"""Kernel timing without verification (for ablation variants via DSORT_LIB): sorts N uniform
+int32 keys `reps` times and prints the per-stage device times of the fastest call."""
+import argparse
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(REPO, "distributed-sorting-with-fault-tolerance_amd"))
+import torch  # noqa: E402
+import dsort  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--keys", type=lambda s: int(eval(s, {}, {})), default=1 << 30)
+ap.add_argument("--reps", type=int, default=4)
+a = ap.parse_args()
+tag = os.environ.get("DSORT_LIB")
+tag = os.path.basename(os.path.dirname(tag)) if tag else "default"
+ctx = dsort.Context(0)
+t = torch.empty(a.keys, dtype=torch.int32, device="cuda")
+ctx.gen_uniform(t, 0x5EED2026)
+o = torch.empty_like(t)
+best = None
+for _ in range(a.reps):
+    ctx.sort_dev(t, o)
+    st = ctx.stats()
+    if best is None or st["total_ms"] < best["total_ms"]:
+        best = st
+torch.cuda.synchronize()
+n = max(best["merge_kernel_launches"], 1)
+print(f"{tag:>14s}: total {best['total_ms']:.3f} ms  block {best['block_sort_ms']:.3f}  "
+      f"merge-kernel avg {best['merge_kernel_ms'] / n:.3f} ms x{best['merge_kernel_launches']}  "
+      f"passes {best['merge_passes']}", flush=True)
