@@ -52,6 +52,12 @@ def parse():
     ap.add_argument("--dist", choices=["uniform", "zipf"], default="uniform")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-keys", type=lambda s: int(eval(s, {}, {})), default=1 << 25)
+    ap.add_argument("--kill-rank", type=int, default=None,
+                    help="BASELINE config C5: fault-tolerance run (launch WITHOUT torchrun: the master "
+                         "spawns one worker per GPU); this worker dies mid-sort")
+    ap.add_argument("--kill-after-pass", type=int, default=1,
+                    help="the dying worker SIGKILLs itself after this merge pass of its local sort")
+    ap.add_argument("--reassign", choices=["first-live", "next-live"], default="first-live")
     return ap.parse_args()
 
 
@@ -124,6 +130,21 @@ def cpu_baseline(sample_keys):
                    f"on equal chunks ({t1 - t0:.2f} s) + reference merge_chunks incl. output.txt "
                    f"text write ({t2 - t1:.2f} s); host nproc={os.cpu_count()}; chunks sorted={ok}"),
     }
+
+
+def pmc_traffic(kernel, n, w):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
+    (profiles/r1_pmc_traffic.json: FETCH_SIZE x2 + WRITE_SIZE, see its calibration note), scaled
+    to this run's key count; None when the file is absent or was measured on another key width."""
+    path = os.path.join(REPO, "profiles", "r1_pmc_traffic.json")
+    try:
+        with open(path) as f:
+            rec = json.load(f)["kernels"][kernel]
+    except (OSError, KeyError, ValueError):
+        return None
+    if w != 4:
+        return None
+    return round(rec["traffic_bytes"] * n / (1 << 30))
 
 
 # ------------------------------------------------------------------------- GPU runs
@@ -246,8 +267,43 @@ def run_multi(args):
                                                 "n_gpu": sz}
 
 
+def run_fault(args):
+    """BASELINE config C5 through ftsort.Master (server.c's role): a fault-free run, then a run in
+    which worker `--kill-rank` dies after merge pass `--kill-after-pass` of its local sort; the
+    survivors detect it, rebuild the communicator and sort the dead chunk from its replica."""
+    import ftsort
+
+    ndev = torch.cuda.device_count()
+    share = args.gpus > ndev  # one GPU box: the workers share it and exchange through gloo
+    devices = [0] * args.gpus if share else list(range(args.gpus))
+    transport = "host" if share or args.gpus == 1 else "rccl"
+    r = ftsort.fault_run(args.gpus, args.keys, args.kill_rank, args.kill_after_pass,
+                         "i32" if args.dtype == "i32" else "i64", args.dist, transport, devices, args.reassign)
+    if not r["ok"]:
+        raise SystemExit(f"bench: fault run failed verification: {json.dumps(r)}")
+    free, fault = r["fault_free"], r["fault"]
+    out = {"metric": "recovery time after one GPU worker failure mid-sort (BASELINE config C5)",
+           "value": round(r["recovery_ms"], 3), "unit": "ms", "n_gpus": args.gpus, "higher_is_better": False,
+           "dtype": "int32" if args.dtype == "i32" else "int64", "data": f"synthetic {args.dist} keys",
+           "config": {"workload": f"sample sort of {args.keys} keys over {args.gpus} workers, worker "
+                                  f"{args.kill_rank} killed after merge pass {args.kill_after_pass}",
+                      "transport": transport, "reassign": args.reassign, "devices": devices},
+           "fault_free_ms": round(free["t_end_ms"], 3), "fault_ms": round(fault["t_end_ms"], 3),
+           "fault_free_keys_per_s": args.keys / (free["t_end_ms"] * 1e-3),
+           "fault_keys_per_s": args.keys / (fault["t_end_ms"] * 1e-3),
+           "fault_seen_by_master_ms": fault["t_fault_seen_ms"],
+           "survivors_notified_ms": fault["t_survivors_notified_ms"],
+           "plan": fault["plan"], "slices": fault["slices"], "verified": True}
+    print(json.dumps(out), flush=True)
+
+
 def main():
     args = parse()
+    if args.kill_rank is not None:
+        if "WORLD_SIZE" in os.environ:
+            raise SystemExit("--kill-rank runs its own master and workers: launch it without torchrun")
+        run_fault(args)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus != world and world != 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
@@ -268,9 +324,9 @@ def main():
                                         f"(BASELINE metric size); tile {k['tile']} keys, {k['passes']} merge passes",
                             "keys": n, "parallelism": "1 GPU"}
         result["roofline"] = {
-            "bound": "hbm", "kernel": "merge2_kernel (merge-path pass)", "achieved": round(achieved, 1),
+            "bound": "hbm", "kernel": "mergew_kernel (k-way merge pass)", "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": None, "avg_launch_ms": round(avg_launch_ms, 4),
+            "traffic": pmc_traffic("mergew_kernel", n, k["w"]), "avg_launch_ms": round(avg_launch_ms, 4),
             "algorithmic_bytes_per_launch": bytes_per_launch,
             "block_sort_ms": round(k["block_ms"] / args.steps, 3),
             "whole_sort_single_pass_bound_frac": round(2 * k["w"] * n / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),

@@ -135,6 +135,10 @@ int wave_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys, size_t n
 int wave_merge_i32(dsort_ctx *ctx, const int32_t *d_in, const size_t *lens, int k, int32_t *d_out,
                    hipStream_t s);
 bool use_legacy_kernels();
+// Fault injection for the fault-tolerance tests and bench (BASELINE config C5): when
+// DSORT_INJECT_KILL_AFTER_PASS=k is set, the process SIGKILLs itself right after merge pass k of a
+// local sort has finished on the GPU -- a worker dying mid-sort.  No effect otherwise.
+void fault_point(hipStream_t s, int pass_done);
 
 }  // namespace dsort
 

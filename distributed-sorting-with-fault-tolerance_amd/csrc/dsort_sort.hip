@@ -29,6 +29,7 @@
 #include <algorithm>
 #include <climits>
 #include <cstdlib>
+#include <csignal>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -437,6 +438,14 @@ static int launch_pass(dsort_ctx *ctx, const T *src, T *dst, const PassDesc &pd,
     return DSORT_OK;
 }
 
+void fault_point(hipStream_t s, int pass_done) {
+    const char *e = getenv("DSORT_INJECT_KILL_AFTER_PASS");  // read per call: armed per sort
+    if (e && atoi(e) == pass_done) {
+        (void)hipStreamSynchronize(s);
+        raise(SIGKILL);
+    }
+}
+
 bool use_legacy_kernels() {
     static int v = -1;
     if (v < 0) {
@@ -502,6 +511,7 @@ int sort_device(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipStream_t 
         if (rc) return rc;
         R <<= plan[p];
         cur ^= 1;
+        fault_point(s, p);
     }
     if (timed && ctx->ev_ok) {
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[2], s));

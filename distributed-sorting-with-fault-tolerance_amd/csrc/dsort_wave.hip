@@ -755,6 +755,7 @@ int wave_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys, size_t n
         if (rc) return rc;
         Rr <<= plan[p];
         cur ^= 1;
+        fault_point(s, p);
     }
     if (timed && ctx->ev_ok) {
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[2], s));

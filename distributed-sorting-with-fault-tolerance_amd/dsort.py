@@ -70,9 +70,10 @@ class Transport(ctypes.Structure):
     _fields_ = [("user", ctypes.c_void_p), ("allgather", ALLGATHER_FN), ("alltoallv", ALLTOALLV_FN)]
 
 
-def torch_dist_transport(world):
-    """A dsort_transport over torch.distributed's default process group (gloo: CPU tensors).
-    For ranks that share a GPU, where RCCL refuses to build a communicator."""
+def torch_dist_transport(world, pg=None):
+    """A dsort_transport over a torch.distributed process group (gloo: CPU tensors; the default
+    group unless `pg` is given).  For ranks that share a GPU, where RCCL refuses to build a
+    communicator, and for the survivors' group after a fault (ftsort.py)."""
     import torch.distributed as dist
 
     def _allgather(user, send, recv, nbytes):
@@ -80,7 +81,10 @@ def torch_dist_transport(world):
             mine = torch.frombuffer(bytearray(ctypes.string_at(send, nbytes)), dtype=torch.uint8) \
                 if nbytes else torch.empty(0, dtype=torch.uint8)
             outs = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(world)]
-            dist.all_gather(outs, mine)
+            if pg is None:
+                dist.all_gather(outs, mine)
+            else:
+                pg.allgather([outs], [mine]).wait()
             if nbytes:
                 whole = torch.cat(outs).numpy()
                 ctypes.memmove(recv, whole.ctypes.data, whole.nbytes)
@@ -97,7 +101,10 @@ def torch_dist_transport(world):
                               for i in range(world))
             inp = torch.frombuffer(bytearray(chunks), dtype=torch.uint8) if chunks else torch.empty(0, dtype=torch.uint8)
             out = torch.empty(sum(rcounts), dtype=torch.uint8)
-            dist.all_to_all_single(out, inp, output_split_sizes=rcounts, input_split_sizes=scounts)
+            if pg is None:
+                dist.all_to_all_single(out, inp, output_split_sizes=rcounts, input_split_sizes=scounts)
+            else:
+                pg.alltoall_base(out, inp, rcounts, scounts).wait()
             o = out.numpy()
             off = 0
             for i in range(world):
@@ -395,6 +402,16 @@ class Context:
         self.check(getattr(self.lib, f"dsort_sample_sort_dev_{sfx}")(self.h, t.data_ptr(), t.numel(),
                                                                       ctypes.byref(outp), ctypes.byref(nout),
                                                                       self._stream()))
+        return outp.value or 0, nout.value
+
+    def sample_merge_dev(self, t):
+        """Exchange half of the sample sort for an already sorted local run `t`
+        (dsort_sample_merge_dev_*).  Returns (device pointer int, n_out) like sample_sort_dev."""
+        sfx = self._tsfx(t)
+        outp, nout = P(), SZ()
+        self.check(getattr(self.lib, f"dsort_sample_merge_dev_{sfx}")(self.h, t.data_ptr(), t.numel(),
+                                                                       ctypes.byref(outp), ctypes.byref(nout),
+                                                                       self._stream()))
         return outp.value or 0, nout.value
 
     def copy_d2h(self, host, dptr, nbytes):
