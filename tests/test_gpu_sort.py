@@ -16,6 +16,7 @@ CASES = json.load(open(os.path.join(GOLDEN, "cases.json")))
 INT_MIN, INT_MAX = -(2**31), 2**31 - 1
 I64_MIN, I64_MAX = -(2**63), 2**63 - 1
 TILE32, TILE64 = 8192, 4096
+WTILE = 16384  # int32 tile of the wave-register kernels (dsort_wave.hip)
 
 
 def sha(b):
@@ -71,8 +72,9 @@ def test_golden_merge_sort(gpu_ctx, case):
     assert np.array_equal(gpu_ctx.sort(a.copy()), exp)
 
 
-SIZES = [0, 1, 2, 3, 15, 16, 17, 511, 4096, TILE32 - 1, TILE32, TILE32 + 1, 2 * TILE32,
-         3 * TILE32 + 5, 5 * TILE32 - 7, 17 * TILE32 + 123, 100003, 1 << 20, (1 << 20) + 3333]
+SIZES = [0, 1, 2, 3, 15, 16, 17, 511, 1023, 1024, 1025, 4096, TILE32 - 1, TILE32, TILE32 + 1, 2 * TILE32,
+         3 * TILE32 + 5, 5 * TILE32 - 7, WTILE - 1, WTILE + 1, 2 * WTILE - 1, 17 * TILE32 + 123, 100003,
+         17 * WTILE + 1, 1 << 20, (1 << 20) + 3333]
 
 
 def _dist(rng, kind, n, dt):
@@ -190,6 +192,49 @@ def test_zipf_i64_sort(gpu_ctx):
     host = t.cpu().numpy()
     top = np.unique(host[: 1 << 20], return_counts=True)[1].max() / (1 << 20)
     assert top > 0.05  # heavy hitter present
+    out = torch.empty_like(t)
+    gpu_ctx.sort_dev(t, out)
+    assert np.array_equal(out.cpu().numpy(), np.sort(host))
+
+
+@pytest.mark.parametrize("k", [2, 7, 17, 32])
+def test_merge_unbalanced_runs_i32(gpu_ctx, oracle, k):
+    """One long run among tiny ones: pairs of every size, windows per pair from 1 to many, partial
+    windows and empty segments in the same merge tile (dsort_wave.hip, mergew_kernel)."""
+    rng = np.random.default_rng(1000 + k)
+    lens = [int(x) for x in rng.integers(0, 60, k)]
+    lens[k // 2] = 5 * WTILE + 333
+    runs = [np.sort(rng.integers(INT_MIN, INT_MAX, m, dtype=np.int64, endpoint=True)).astype(np.int32)
+            for m in lens]
+    assert np.array_equal(gpu_ctx.merge(runs), oracle.merge_runs(runs))
+
+
+@pytest.mark.parametrize("k", [31, 32, 64, 65])
+def test_merge_many_random_runs_i32(gpu_ctx, oracle, k):
+    rng = np.random.default_rng(77 + k)
+    lens = rng.integers(0, 40000, k)
+    runs = [np.sort(rng.integers(-50, 50, int(m))).astype(np.int32) for m in lens]  # many duplicates
+    assert np.array_equal(gpu_ctx.merge(runs), oracle.merge_runs(runs))
+
+
+def test_heavy_duplicates_i32(gpu_ctx):
+    """Zipf-like int32 keys: the tile cuts fall inside runs of one key (partk's exact tie cut)."""
+    rng = np.random.default_rng(5)
+    n = (1 << 23) + 99
+    a = np.minimum(rng.zipf(1.3, n), 2**31 - 1).astype(np.int64)
+    a = (a * 2654435761) % (2**32) - 2**31
+    a = a.astype(np.int32)
+    assert np.unique(a[: 1 << 16], return_counts=True)[1].max() > (1 << 16) // 5
+    assert np.array_equal(gpu_ctx.sort(a.copy()), np.sort(a))
+
+
+@pytest.mark.parametrize("n", [16 * WTILE + 1, 256 * WTILE + 12345])
+def test_sort_i32_pass_boundaries(gpu_ctx, n):
+    """Tile counts just past one and two merge passes of fan-in 16."""
+    import torch
+    t = torch.empty(n, dtype=torch.int32, device="cuda")
+    gpu_ctx.gen_uniform(t, 99, 0)
+    host = t.cpu().numpy()
     out = torch.empty_like(t)
     gpu_ctx.sort_dev(t, out)
     assert np.array_equal(out.cpu().numpy(), np.sort(host))
