@@ -110,14 +110,58 @@ __device__ __forceinline__ T key_at(T lo, T hi, double frac) {
     return (T)((U)lo + o);
 }
 
+// 16-byte vector of keys (int4 / longlong2)
+template <typename T> struct Vec16Part;
+template <> struct Vec16Part<int32_t> { using type = int4; };
+template <> struct Vec16Part<int64_t> { using type = longlong2; };
+
+// #keys <= v in A[u, h) for a short window (at most 4 16-byte chunks of keys): every chunk
+// that overlaps the window is loaded at once (one memory round trip instead of a dependent
+// binary search); `end` bounds the array so a chunk never reads past it.
+template <typename T>
+__device__ __forceinline__ uint64_t count_le_window(const T *A, uint64_t u, uint64_t h, T v,
+                                                    const T *end) {
+    using V = typename Vec16Part<T>::type;
+    constexpr int N = 16 / (int)sizeof(T);
+    const T *p0 = A + u;
+    const T *ph = A + h;
+    const T *pa = reinterpret_cast<const T *>(reinterpret_cast<uintptr_t>(p0) & ~(uintptr_t)15);
+    T x[5][N];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const T *q = pa + k * N;
+        if (q < ph && q + N <= end) {
+            const V w = *reinterpret_cast<const V *>(q);
+            const T *pw = reinterpret_cast<const T *>(&w);
+#pragma unroll
+            for (int j = 0; j < N; ++j) x[k][j] = pw[j];
+        } else {
+#pragma unroll
+            for (int j = 0; j < N; ++j) x[k][j] = (q + j < ph && q + j < end) ? q[j] : key_max<T>();
+        }
+    }
+    uint64_t cnt = 0;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            const T *e = pa + k * N + j;
+            cnt += (e >= p0 && e < ph && x[k][j] <= v) ? 1 : 0;
+        }
+    }
+    return u + cnt;
+}
+
 // #keys <= v in A[u, h), knowing A[u..h) lies within [klo, khi]: interpolation probes while the
-// window is large, then binary search.  Each probe is one dependent load.
+// window is large, then one vector count of the last <= 4 chunks.  Each probe is one dependent
+// load.
 template <typename T>
 __device__ __forceinline__ uint64_t upper_bound_interp(const T *A, uint64_t u, uint64_t h, T v,
-                                                       T klo, T khi) {
+                                                       T klo, T khi, const T *end) {
     using U = typename Unsigned<T>::type;
+    constexpr uint64_t WIN = 64 / sizeof(T) - 16 / sizeof(T);  // fits 4 chunks at any alignment
 #pragma unroll 1
-    for (int it = 0; it < 4 && h - u > 32; ++it) {
+    for (int it = 0; it < 6 && h - u > WIN; ++it) {
         if (v < klo) return u;
         if (v >= khi) return h;
         const double frac = (double)((U)v - (U)klo) / ((double)((U)khi - (U)klo) + 1.0);
@@ -132,12 +176,13 @@ __device__ __forceinline__ uint64_t upper_bound_interp(const T *A, uint64_t u, u
             khi = x;
         }
     }
-    while (u < h) {
+#pragma unroll 1
+    while (h - u > WIN) {
         const uint64_t m = (u + h) >> 1;
         if (A[m] <= v) u = m + 1;
         else h = m;
     }
-    return u;
+    return u < h ? count_le_window(A, u, h, v, end) : u;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -199,7 +244,7 @@ __global__ void __launch_bounds__(256) partk_kernel(const T *__restrict__ in, Pa
             const U q = range / (U)(C + 1), rr = range % (U)(C + 1);
             cand = (T)((U)lo + q * (U)(c + 1) + (rr * (U)(c + 1)) / (U)(C + 1));
         }
-        const uint64_t u = upper_bound_interp(A, ilo, ihi, cand, lo, hi);
+        const uint64_t u = upper_bound_interp(A, ilo, ihi, cand, lo, hi, in + pd.n);
         uint64_t tot = u;
         for (int o = 1; o < F; o <<= 1) tot += __shfl_xor(tot, o);
         // a candidate whose cut already lands within the slack ends the search
