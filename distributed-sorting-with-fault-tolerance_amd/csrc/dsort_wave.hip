@@ -306,30 +306,40 @@ struct Win {
 };
 
 // Loads the bitonic window (reg-major, element e = 64 i + t in x[i]): [0, qa) = A ascending,
-// [qa, qa+pad) = +inf, [qa+pad, 1024) = B descending.  qa and pad are wave-uniform, so every
-// register but the one or two that straddle a boundary is a plain LDS read at an immediate
-// offset from one of two per-lane bases.
+// [qa, qa+pad) = +inf, [qa+pad, 1024) = B descending.  Branch-free: for every register both
+// candidates are read (immediate offsets from two per-lane bases, so all 32 reads are in flight
+// together) and one compare + select keeps the right one; the LDS array carries WK slack slots
+// so the unselected read never leaves it.  qa and pad are wave-uniform.
 __device__ __forceinline__ void load_window(const int *s, int a_first, int b_last, int qa, int pad,
                                             int (&x)[R]) {
     // a_first: LDS index of element 0 (A[a0]); element e of the B part is s[b_last - e]
-    // (b_last = index of B[b0] + 1023)
     const int t = lane_id();
-    const int qp = qa + pad;
     const int *sa = s + a_first + t;                    // element 64 i + t of A: sa[64 i]
     const int *sb = s + b_last - t - 64 * (R - 1);      // element 64 i + t of B: sb[64 (15 - i)]
+    // two halves of 8 registers: 16 reads in flight per half, 16 temporaries live
 #pragma unroll
-    for (int i = 0; i < R; ++i) {
-        const int e0 = 64 * i;
-        if (e0 + 64 <= qa) {
-            x[i] = sa[64 * i];
-        } else if (e0 >= qp) {
-            x[i] = sb[64 * (R - 1 - i)];
+    for (int hlf = 0; hlf < 2; ++hlf) {
+        int va[R / 2], vb[R / 2];
+#pragma unroll
+        for (int k = 0; k < R / 2; ++k) {
+            const int i = hlf * (R / 2) + k;
+            va[k] = sa[64 * i];
+            vb[k] = sb[64 * (R - 1 - i)];
+        }
+        if (pad == 0) {
+#pragma unroll
+            for (int k = 0; k < R / 2; ++k) {
+                const int i = hlf * (R / 2) + k;
+                x[i] = t < qa - 64 * i ? va[k] : vb[k];
+            }
         } else {
-            const int e = e0 + t;
-            int idx = e < qa ? a_first + e : b_last - e;
-            idx = idx < 0 ? 0 : (idx > TILE - 1 ? TILE - 1 : idx);
-            const int v = s[idx];
-            x[i] = (e >= qa && e < qp) ? KMAX : v;
+            const int qp = qa + pad;
+#pragma unroll
+            for (int k = 0; k < R / 2; ++k) {
+                const int i = hlf * (R / 2) + k;
+                const int v = t < qa - 64 * i ? va[k] : vb[k];
+                x[i] = (t >= qa - 64 * i && t < qp - 64 * i) ? KMAX : v;
+            }
         }
     }
 }
@@ -349,6 +359,14 @@ __device__ __forceinline__ void merge_window(const int *s, const Win &w, int (&x
     const int b0 = w.d0 - a0;
     const int qa = a1 - a0;
     load_window(s, w.pa + a0, w.pb + b0 + (WK - 1), qa, WK - w.wreal, x);
+#ifdef DSORT_ABL_LOAD2  // ablation: a second, discarded window load (marginal cost)
+    {
+        int z[R];
+        load_window(s, w.pa + a0, w.pb + b0 + (WK - 1), qa, WK - w.wreal, z);
+#pragma unroll
+        for (int i = 0; i < R; ++i) asm volatile("" ::"v"(z[i]));
+    }
+#endif
 #ifdef DSORT_ABL_NET2  // ablation: a second, discarded network (marginal cost)
     {
         int z[R];
@@ -383,9 +401,9 @@ __device__ __forceinline__ void store_window(P *dst, int obase, int wreal, int l
 __global__ void __launch_bounds__(THREADS, 8) block_sort_w_kernel(const int *in, int *out,
                                                                     uint64_t n) {
     // `in` may alias `out`: every workgroup reads its tile before it writes it
-    __shared__ __attribute__((aligned(16))) int s[TILE];
+    __shared__ __attribute__((aligned(16))) int s[TILE + WK];  // + slack read by load_window
     const int t = lane_id();
-    const int w = threadIdx.x >> 6;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
     const uint64_t base = (uint64_t)blockIdx.x * TILE;
     const uint64_t rem = n - base;
     const int valid = rem < (uint64_t)TILE ? (int)rem : TILE;
@@ -451,7 +469,7 @@ __global__ void __launch_bounds__(THREADS, 8) mergew_kernel(const int *__restric
     constexpr int F = 1 << LOGF;
     constexpr int MAXWIN = (WAVES + F / 2 + WAVES - 1) / WAVES;
     constexpr int NCHUNK = TILE / 64;
-    __shared__ __attribute__((aligned(16))) int s[TILE];
+    __shared__ __attribute__((aligned(16))) int s[TILE + WK];  // + slack read by load_window
     __shared__ int soff[F + 1];
     __shared__ int64_t gdelta[F];        // global index of tile key e in segment sg = gdelta[sg] + e
     __shared__ int64_t cbase[NCHUNK];    // chunk c inside one segment: key 64c + i at cbase[c] + i
@@ -463,7 +481,7 @@ __global__ void __launch_bounds__(THREADS, 8) mergew_kernel(const int *__restric
     __shared__ int2 wtab_b[LOGF][WAVES * MAXWIN];  // d0, wreal (0 = no window)
 
     const int t = lane_id();
-    const int w = threadIdx.x >> 6;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
     const uint64_t j = blockIdx.x;
     STAMP(0);
     TileInfo ti;
