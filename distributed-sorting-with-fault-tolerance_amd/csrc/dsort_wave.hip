@@ -266,13 +266,16 @@ __device__ __forceinline__ void sort_wave(int (&x)[R], const int (&c)[6]) {
 // two searches advance together.
 __device__ __forceinline__ int split_step(const int *s, int pa, int pb, int d, int lane, int &lo,
                                           int &hi) {
-    // one 64-ary step of one search; returns 1 while the bracket is still open
+    // one 64-ary step of one search; returns 1 while the bracket is still open.  Branch-free per
+    // lane: probes past the bracket read a clamped in-bounds index and count as "true".
     if (lo >= hi) return 0;
     const int len = hi - lo;
     const int st = ((len + 63) >> 6) | 1;
-    const int off = lane * st;
-    bool q = true;
-    if (off < len) q = s[pa + lo + off] > s[pb + d - 1 - lo - off];
+    const int off = (int)__umul24((unsigned)lane, (unsigned)st);
+    const int ia = pa + lo + off;                       // <= TILE + WK - 1 (slack slots)
+    int ib = pb + d - 1 - lo - off;
+    ib = ib < 0 ? 0 : ib;
+    const bool q = (off >= len) | (s[ia] > s[ib]);
     const unsigned long long m = __ballot(q);
     const int j = m ? (int)__ffsll((long long)m) - 1 : 64;
     const int nhi = lo + j * st < hi ? lo + j * st : hi;
