@@ -47,6 +47,7 @@ constexpr int TILE = WK * WAVES;   // keys per workgroup tile (64 KiB of LDS)
 constexpr int KMAX = INT32_MAX;
 constexpr int KMIN = INT32_MIN;
 constexpr int kWaveMaxLogF = 5;    // fan-in cap of one merge pass (<= 2 windows per wave)
+constexpr int kWaveMaxF = 1 << kWaveMaxLogF;
 constexpr int SLACK = TILE / 32;   // cut tolerance of partk
 constexpr int TNOM = TILE - 2 * SLACK;
 
@@ -474,10 +475,12 @@ __global__ void __launch_bounds__(THREADS, 8) mergew_kernel(const int *__restric
     constexpr int NCHUNK = TILE / 64;
     __shared__ __attribute__((aligned(16))) int s[TILE + WK];  // + slack read by load_window
     __shared__ int soff[F + 1];
-    __shared__ int64_t gdelta[F];        // global index of tile key e in segment sg = gdelta[sg] + e
-    __shared__ int64_t cbase[NCHUNK];    // chunk c inside one segment: key 64c + i at cbase[c] + i
-    __shared__ uint8_t cseg[NCHUNK];     // segment of key 64c
-    __shared__ uint8_t cmix[NCHUNK];     // chunk c spans a segment boundary
+    // Staging works on 16-byte-aligned chunks of 4 keys of each segment (absolute alignment):
+    __shared__ int64_t sgs[F];           // global index of the segment's first key
+    __shared__ int64_t sa0[F];           // global index of its first aligned chunk (may be < sgs)
+    __shared__ int slen[F];              // keys in the segment
+    __shared__ int cpre[F + 1];          // chunks before segment s (cpre[F] = chunks of the tile)
+    __shared__ uint8_t gseg[NCHUNK / 4 + 2];  // segment of chunk 64 G (first of wave group G)
     __shared__ uint64_t s_out;
     __shared__ int s_total;
     __shared__ int4 wtab_a[LOGF][WAVES * MAXWIN];  // per level and window: pa, na, pb, nb
@@ -503,9 +506,23 @@ __global__ void __launch_bounds__(THREADS, 8) mergew_kernel(const int *__restric
             if (i >= o) incl += v;
             before += __shfl_xor(before, o);
         }
+        // aligned chunks of segment i (absolute 16-B alignment of &in[g])
+        const int mis = (int)((reinterpret_cast<uintptr_t>(in) >> 2) & 3);
+        const int64_t gs = (int64_t)(rs + s0);
+        const int64_t a0 = ((gs + mis) & ~(int64_t)3) - mis;
+        const int nc = len ? (int)((gs + len + mis + 3) >> 2) - (int)((gs + mis) >> 2) : 0;
+        int cinc = nc;
+        for (int o = 1; o < F; o <<= 1) {
+            const int v = __shfl_up(cinc, o);
+            if (i >= o) cinc += v;
+        }
         if (t < F) {
             soff[i + 1] = incl;
-            gdelta[i] = (int64_t)(rs + s0) - (int64_t)(incl - len);
+            sgs[i] = gs;
+            sa0[i] = a0;
+            slen[i] = len;
+            cpre[i + 1] = cinc;
+            if (i == 0) cpre[0] = 0;
             if (i == F - 1) s_total = incl;
             if (i == 0) {
                 soff[0] = 0;
@@ -516,20 +533,17 @@ __global__ void __launch_bounds__(THREADS, 8) mergew_kernel(const int *__restric
     __syncthreads();
     STAMP(1);
     const int total = __builtin_amdgcn_readfirstlane(s_total);
-    const uint64_t sstart0 = ti.base;  // a key index that exists (loads past `total` read it)
-    // per 64-key chunk: the segment of its first key, and whether its keys span segments
-    if (threadIdx.x < NCHUNK) {
-        const int e = threadIdx.x * 64;
-        int lo = 0, hi = F - 1;  // last segment starting at or before e
+    const int nchunks = __builtin_amdgcn_readfirstlane(cpre[F]);
+    // segment of the first chunk of every 64-chunk wave group
+    if (threadIdx.x < NCHUNK / 4 + 2) {
+        const int q = threadIdx.x * 64;
+        int lo = 0, hi = F - 1;  // last segment whose chunks start at or before q
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
-            if (soff[mid] <= e) lo = mid;
+            if (cpre[mid] <= q) lo = mid;
             else hi = mid - 1;
         }
-        cseg[threadIdx.x] = (uint8_t)lo;
-        cbase[threadIdx.x] = gdelta[lo] + e;
-        const int eend = e + 63 < total ? e + 63 : total - 1;
-        cmix[threadIdx.x] = (lo < F - 1 && soff[lo + 1] <= eend) ? 1 : 0;
+        gseg[threadIdx.x] = (uint8_t)lo;
     }
     __syncthreads();
     STAMP(2);
@@ -576,47 +590,42 @@ __global__ void __launch_bounds__(THREADS, 8) mergew_kernel(const int *__restric
             }
         }
     }
-    // Staging: key e of the tile is loaded by thread e % THREADS (coalesced within a segment).
-    // A chunk inside one segment addresses its keys as cbase + lane; only the rare chunk that
-    // spans a segment boundary looks its segment up.  Addresses are formed first and all 16
-    // loads issued unconditionally (branch joins with loads in flight would serialize them).
+    // Staging: chunk q (4 keys, 16-B aligned in global memory) is loaded by thread q % THREADS
+    // with one dwordx4 (consecutive lanes on consecutive chunks of a segment: 1 KiB per wave
+    // instruction); the keys of a chunk that lie outside its segment are dropped.  An aligned
+    // 16-B block holding a key of the array never crosses a page, so edge chunks are safe.
     {
-        int v[R];
+        constexpr int NK = (TILE / 4 + kWaveMaxF + THREADS - 1) / THREADS;  // chunks per thread
+        int4 v[NK];
+        int ebase[NK], lo4[NK], hi4[NK];
 #pragma unroll
-        for (int k = 0; k < R; ++k) {
-            const int e = threadIdx.x + k * THREADS;
-            const int c = w + k * WAVES;
-            int64_t gi;
-            if (__builtin_amdgcn_readfirstlane((int)cmix[c])) {
-                const int first = __builtin_amdgcn_readfirstlane((int)cseg[c]);
+        for (int k = 0; k < NK; ++k) {
+            const int q = threadIdx.x + k * THREADS;
+            const int G = w + k * WAVES;
+            ebase[k] = 0;
+            lo4[k] = 0;
+            hi4[k] = 0;  // no valid key
+            if (G * 64 < nchunks) {  // wave-uniform
+                const int first = __builtin_amdgcn_readfirstlane((int)gseg[G]);
+                const int lastg = __builtin_amdgcn_readfirstlane((int)gseg[G + 1]);
                 int sg = first;
 #pragma unroll 1
-                for (int q = first + 1; q < F; ++q) {
-                    const int so = __builtin_amdgcn_readfirstlane(soff[q]);
-                    if (so > c * 64 + 63) break;
-                    sg += so <= e ? 1 : 0;
-                }
-                gi = gdelta[sg] + e;
-            } else {
-                const int64_t cb = cbase[c];
-                const int64_t cbu = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(cb >> 32)) << 32) |
-                                              (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)cb));
-                gi = cbu + t;
+                for (int qq = first + 1; qq <= lastg; ++qq) sg += cpre[qq] <= q ? 1 : 0;
+                const int qc = q < nchunks ? q : cpre[sg];  // past the last chunk: a valid one
+                const int64_t g = sa0[sg] + 4 * (int64_t)(qc - cpre[sg]);
+                const int off = (int)(g - sgs[sg]);  // key offset of the chunk in its segment
+                ebase[k] = soff[sg] + off;
+                lo4[k] = -off;                       // valid j: -off <= j < len - off
+                hi4[k] = q < nchunks ? slen[sg] - off : 0;
+                v[k] = *reinterpret_cast<const int4 *>(in + g);
             }
-            if (c * 64 + 64 > total) gi = e < total ? gi : (int64_t)sstart0;  // wave-uniform test
-#ifdef DSORT_ABL_STAGE2  // ablation: a second, discarded load of the key (marginal cost)
-            {
-                const int z = in[gi & ~(int64_t)1];
-                asm volatile("" ::"v"(z));
-            }
-#endif
-            v[k] = in[gi];
         }
 #pragma unroll
-        for (int k = 0; k < R; ++k) {
-            const int e = threadIdx.x + k * THREADS;
-            if ((w + k * WAVES) * 64 + 64 <= total) s[e] = v[k];
-            else if (e < total) s[e] = v[k];
+        for (int k = 0; k < NK; ++k) {
+            const int vals[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj)
+                if (jj >= lo4[k] && jj < hi4[k]) s[ebase[k] + jj] = vals[jj];
         }
     }
     STAMP(3);
