@@ -18,11 +18,12 @@
 //   * mergew_kernel: one workgroup merges one output tile of a k-way pass: the F input windows
 //     (cut by partk_kernel, dsort_part.h) are staged back to back in LDS and merged in log2(F)
 //     pairwise levels.
-//   * An LDS level cuts every pair of runs into windows of <= 1024 outputs.  One wave finds the
-//     window's merge-path split at both ends with a 64-ary search (64 probes per step, ballot),
-//     loads A ascending, +inf padding, B descending -- a bitonic sequence -- and sorts it with
-//     the 10-stage half-cleaner network.  Windows are held in registers across a barrier, so the
-//     level merges in place in one LDS buffer.
+//   * An LDS level cuts every pair of runs into windows of 1024 outputs.  The B run of a pair is
+//     kept descending in LDS (every level writes the groups that become B runs reversed), so
+//     after one 64-ary merge-path search for the window start (64 probes per step, ballot) the
+//     window is min(A[a0 + e], B[b0 + 1023 - e]) -- two ascending LDS reads and a v_min per key,
+//     a bitonic sequence -- sorted by the 10-stage half-cleaner network.  Windows are held in
+//     registers across a barrier, so the level merges in place in one LDS buffer.
 //
 // Algorithmic HBM traffic: 8 bytes per key for the tile sort and for every pass.
 #include <hip/hip_runtime.h>
@@ -55,8 +56,6 @@ constexpr int TNOM = TILE - 2 * SLACK;
 constexpr int QP_1032 = 0xB1;      // lane ^ 1
 constexpr int QP_2301 = 0x4E;      // lane ^ 2
 constexpr int QP_3210 = 0x1B;      // lane ^ 3
-constexpr int ROW_SHL4 = 0x104;    // lane i reads lane i + 4 (within a row of 16)
-constexpr int ROW_SHR4 = 0x114;    // lane i reads lane i - 4
 constexpr int ROW_ROR8 = 0x128;    // lane ^ 8
 constexpr int ROW_MIRROR = 0x140;  // lane ^ 15
 constexpr int ROW_HMIRROR = 0x141; // lane ^ 7
@@ -260,142 +259,119 @@ __device__ __forceinline__ void sort_wave(int (&x)[R], const int (&c)[6]) {
 // ------------------------------------------------------------------------------------------
 // LDS levels
 // ------------------------------------------------------------------------------------------
-// Merge-path splits of a window: numbers of A keys among the first d0 and d1 outputs of
-// merge(A, B), A first on ties (A = s[pa, pa+na), B = s[pb, pb+nb); all arguments wave-uniform).
-// All lanes of the wave cooperate: each step probes 64 candidates per split at an odd stride
-// (distinct LDS banks), and the ballot of "A[a] > B[d-1-a]" brackets the split 64x tighter; the
-// two searches advance together.
-__device__ __forceinline__ int split_step(const int *s, int pa, int pb, int d, int lane, int &lo,
-                                          int &hi) {
-    // one 64-ary step of one search; returns 1 while the bracket is still open.  Branch-free per
-    // lane: probes past the bracket read a clamped in-bounds index and count as "true".
-    if (lo >= hi) return 0;
-    const int len = hi - lo;
-    const int st = ((len + 63) >> 6) | 1;
-    const int off = (int)__umul24((unsigned)lane, (unsigned)st);
-    const int ia = pa + lo + off;                       // <= TILE + WK - 1 (slack slots)
-    int ib = pb + d - 1 - lo - off;
-    ib = ib < 0 ? 0 : ib;
-    const bool q = (off >= len) | (s[ia] > s[ib]);
-    const unsigned long long m = __ballot(q);
-    const int j = m ? (int)__ffsll((long long)m) - 1 : 64;
-    const int nhi = lo + j * st < hi ? lo + j * st : hi;
-    lo = j ? lo + (j - 1) * st + 1 : lo;
-    hi = nhi;
-    return 1;
-}
+// ---- Windows over a pair whose B run is stored DESCENDING in LDS -------------------------
+// Pair = A ascending at s[pa, pa+na) followed by B descending (B[k] at s[pbe - k], pbe = pa + na
+// + nb - 1).  For a window starting at output d0 with merge-path split (a0, b0 = d0 - a0), the
+// 1024 smallest keys of A[a0..] u B[b0..] are min(A[a0 + e], B[b0 + 1023 - e]), e < 1024, and in
+// that order they form a bitonic sequence.  Both operands are ascending LDS ranges
+// (s[pa + a0 + e] and s[pbe - b0 - 1023 + e]); when at least 1024 outputs remain from d0 a read
+// past either run lands on the other run's larger keys of the same pair and never wins the min
+// (DESIGN.md §3.3), so a full window needs one split search, 32 reads and 16 v_min.
 
-__device__ __forceinline__ void coop_split2(const int *s, int pa, int na, int pb, int nb, int d0,
-                                            int d1, int &r0, int &r1) {
-    int lo0 = d0 > nb ? d0 - nb : 0, hi0 = d0 < na ? d0 : na;
-    int lo1 = d1 > nb ? d1 - nb : 0, hi1 = d1 < na ? d1 : na;
+// Number of A keys among the first d outputs of merge(A, B) (one 64-ary search, wave-uniform).
+__device__ __forceinline__ int coop_split_desc(const int *s, int pa, int na, int pbe, int nb, int d) {
+    int lo = d > nb ? d - nb : 0, hi = d < na ? d : na;
     const int lane = lane_id();
 #pragma unroll 1
-    while (lo0 < hi0 || lo1 < hi1) {
-        split_step(s, pa, pb, d0, lane, lo0, hi0);
-        split_step(s, pa, pb, d1, lane, lo1, hi1);
-        lo0 = __builtin_amdgcn_readfirstlane(lo0);
-        hi0 = __builtin_amdgcn_readfirstlane(hi0);
-        lo1 = __builtin_amdgcn_readfirstlane(lo1);
-        hi1 = __builtin_amdgcn_readfirstlane(hi1);
+    while (lo < hi) {
+        const int len = hi - lo;
+        const int st = ((len + 63) >> 6) | 1;
+        const int off = (int)__umul24((unsigned)lane, (unsigned)st);
+        const int ia = pa + lo + off;                  // <= TILE + WK - 1 (slack slots)
+        int ib = pbe - d + 1 + lo + off;               // B[d - 1 - lo - off]
+        ib = ib > pbe ? pbe : ib;                      // probes past the bracket: in bounds
+        const bool q = (off >= len) | (s[ia] > s[ib]);
+        const unsigned long long m = __ballot(q);
+        const int j = m ? (int)__ffsll((long long)m) - 1 : 64;
+        const int nhi = lo + j * st < hi ? lo + j * st : hi;
+        lo = __builtin_amdgcn_readfirstlane(j ? lo + (j - 1) * st + 1 : lo);
+        hi = __builtin_amdgcn_readfirstlane(nhi);
     }
-    r0 = lo0;
-    r1 = lo1;
+    return lo;
 }
 
-// A window of a merge level: outputs [d0, d0 + wreal) of merge(A = s[pa, pa+na),
-// B = s[pb, pb+nb)) land at tile positions [obase, obase + wreal).  Wave-uniform.
-struct Win {
-    int pa, na, pb, nb, d0, wreal;
-};
-
-// Loads the bitonic window (reg-major, element e = 64 i + t in x[i]): [0, qa) = A ascending,
-// [qa, qa+pad) = +inf, [qa+pad, 1024) = B descending.  Branch-free: for every register both
-// candidates are read (immediate offsets from two per-lane bases, so all 32 reads are in flight
-// together) and one compare + select keeps the right one; the LDS array carries WK slack slots
-// so the unselected read never leaves it.  qa and pad are wave-uniform.
-__device__ __forceinline__ void load_window(const int *s, int a_first, int b_last, int qa, int pad,
-                                            int (&x)[R]) {
-    // a_first: LDS index of element 0 (A[a0]); element e of the B part is s[b_last - e]
+// Full window: x[i] at lane t = min(s[ia0 + e], s[ib0 + e]), e = 64 i + t.
+__device__ __forceinline__ void load_min(const int *s, int ia0, int ib0, int (&x)[R]) {
     const int t = lane_id();
-    const int *sa = s + a_first + t;                    // element 64 i + t of A: sa[64 i]
-    const int *sb = s + b_last - t - 64 * (R - 1);      // element 64 i + t of B: sb[64 (15 - i)]
-    // two halves of 8 registers: 16 reads in flight per half, 16 temporaries live
+    const int *sa = s + ia0 + t;
+    const int *sb = s + ib0 + t;
 #pragma unroll
     for (int hlf = 0; hlf < 2; ++hlf) {
-        int va[R / 2], vb[R / 2];
+        int vb[R / 2];
 #pragma unroll
         for (int k = 0; k < R / 2; ++k) {
             const int i = hlf * (R / 2) + k;
-            va[k] = sa[64 * i];
-            vb[k] = sb[64 * (R - 1 - i)];
+            x[i] = sa[64 * i];
+            vb[k] = sb[64 * i];
         }
-        if (pad == 0) {
 #pragma unroll
-            for (int k = 0; k < R / 2; ++k) {
-                const int i = hlf * (R / 2) + k;
-                x[i] = t < qa - 64 * i ? va[k] : vb[k];
-            }
-        } else {
-            const int qp = qa + pad;
-#pragma unroll
-            for (int k = 0; k < R / 2; ++k) {
-                const int i = hlf * (R / 2) + k;
-                const int v = t < qa - 64 * i ? va[k] : vb[k];
-                x[i] = (t >= qa - 64 * i && t < qp - 64 * i) ? KMAX : v;
-            }
+        for (int k = 0; k < R / 2; ++k) {
+            const int i = hlf * (R / 2) + k;
+            x[i] = x[i] < vb[k] ? x[i] : vb[k];
         }
     }
 }
 
-// Merges window w into registers (layout of merge_net).
-__device__ __forceinline__ void merge_window(const int *s, const Win &w, int (&x)[R], int c0,
-                                             int c1, int c2, int c3) {
-    int a0, a1;
-    coop_split2(s, w.pa, w.na, w.pb, w.nb, w.d0, w.d0 + w.wreal, a0, a1);
-#ifdef DSORT_ABL_SPLIT2  // ablation: a second, discarded split search (marginal cost)
-    {
-        int z0, z1;
-        coop_split2(s, w.pa, w.na, w.pb, w.nb, w.d0 + 1, w.d0 + w.wreal - 1, z0, z1);
-        asm volatile("" ::"s"(z0), "s"(z1));
-    }
-#endif
-    const int b0 = w.d0 - a0;
-    const int qa = a1 - a0;
-    load_window(s, w.pa + a0, w.pb + b0 + (WK - 1), qa, WK - w.wreal, x);
-#ifdef DSORT_ABL_LOAD2  // ablation: a second, discarded window load (marginal cost)
-    {
-        int z[R];
-        load_window(s, w.pa + a0, w.pb + b0 + (WK - 1), qa, WK - w.wreal, z);
+// Pair of fewer than 1024 keys (one window, d0 = 0): A[e] for e < na, B[1023 - e] for
+// e >= 1024 - nb, +inf elsewhere.
+__device__ __forceinline__ void load_min_short(const int *s, int pa, int na, int pbe, int nb,
+                                               int (&x)[R]) {
+    const int t = lane_id();
 #pragma unroll
-        for (int i = 0; i < R; ++i) asm volatile("" ::"v"(z[i]));
+    for (int i = 0; i < R; ++i) {
+        const int e = 64 * i + t;
+        int ib = pbe - 1023 + e;
+        ib = ib < 0 ? 0 : ib;
+        const int va = e < na ? s[pa + e] : KMAX;
+        const int vb = e >= WK - nb ? s[ib] : KMAX;
+        x[i] = va < vb ? va : vb;
     }
-#endif
-#ifdef DSORT_ABL_NET2  // ablation: a second, discarded network (marginal cost)
-    {
-        int z[R];
-#pragma unroll
-        for (int i = 0; i < R; ++i) z[i] = x[i] ^ i;
-        merge_net(z, c0, c1, c2, c3);
-#pragma unroll
-        for (int i = 0; i < R; ++i) asm volatile("" ::"v"(z[i]));
+}
+
+// A window of a pair with B descending: outputs [d0 + skip, d0 + skip + cnt) of the pair's merge
+// are kept (skip > 0 only for the last window of a pair, shifted back to end at the pair's end).
+struct WinD {
+    int pa, na, nb, d0, skip, cnt, desc;
+};
+
+__device__ __forceinline__ void merge_window_desc(const int *s, const WinD &w, int (&x)[R], int c0,
+                                                  int c1, int c2, int c3) {
+    const int pbe = w.pa + w.na + w.nb - 1;
+    if (w.na + w.nb >= WK) {
+        const int a0 = coop_split_desc(s, w.pa, w.na, pbe, w.nb, w.d0);
+        load_min(s, w.pa + a0, pbe - (w.d0 - a0) - (WK - 1), x);
+    } else {
+        load_min_short(s, w.pa, w.na, pbe, w.nb, x);
     }
-#endif
     merge_net(x, c0, c1, c2, c3);
 }
 
-// Stores a merged window (merge_net layout) at tile positions [obase, obase + wreal) of `dst`
-// (LDS or global); `lo` = out_lo(lane).
-template <typename P>
-__device__ __forceinline__ void store_window(P *dst, int obase, int wreal, int lo, const int (&x)[R]) {
-    P *p = dst + obase + lo;
-    if (wreal >= WK) {
+// Stores the kept outputs of a window: pair output position d lands at dst[ob + d] (ascending
+// group) or dst[ob + len - 1 - d] (descending group; LDS only: the last level is ascending).
+template <bool DESC, typename P>
+__device__ __forceinline__ void store_window_desc(P *dst, const WinD &w, int ob, int lo,
+                                                  const int (&x)[R]) {
+    const bool part = w.skip != 0 || w.cnt != WK;
+    if (!DESC || !w.desc) {
+        P *p = dst + ob + w.d0 + lo;
+        if (!part) {
 #pragma unroll
-        for (int i = 0; i < R; ++i) p[out_hi(i)] = x[i];
+            for (int i = 0; i < R; ++i) p[out_hi(i)] = x[i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < R; ++i)
+                if ((unsigned)(out_hi(i) + lo - w.skip) < (unsigned)w.cnt) p[out_hi(i)] = x[i];
+        }
     } else {
+        P *p = dst + ob + (w.na + w.nb - 1 - w.d0) - lo;
+        if (!part) {
 #pragma unroll
-        for (int i = 0; i < R; ++i)
-            if (out_hi(i) + lo < wreal) p[out_hi(i)] = x[i];
+            for (int i = 0; i < R; ++i) p[-out_hi(i)] = x[i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < R; ++i)
+                if ((unsigned)(out_hi(i) + lo - w.skip) < (unsigned)w.cnt) p[-out_hi(i)] = x[i];
+        }
     }
 }
 
@@ -436,11 +412,19 @@ __global__ void __launch_bounds__(THREADS, 8) block_sort_w_kernel(const int *in,
         }
     }
     sort_wave(x, c);
-    // lane-major run of the wave -> LDS
+    // lane-major run of the wave -> LDS; odd waves' runs (the B runs of the first level) are
+    // stored descending
     {
-        int4 *dst = reinterpret_cast<int4 *>(s + w * WK + t * R);
+        if (w & 1) {
+            int4 *dst = reinterpret_cast<int4 *>(s + w * WK + WK - R * (t + 1));
 #pragma unroll
-        for (int q = 0; q < R / 4; ++q) dst[q] = make_int4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
+            for (int q = 0; q < R / 4; ++q)
+                dst[3 - q] = make_int4(x[4 * q + 3], x[4 * q + 2], x[4 * q + 1], x[4 * q]);
+        } else {
+            int4 *dst = reinterpret_cast<int4 *>(s + w * WK + t * R);
+#pragma unroll
+            for (int q = 0; q < R / 4; ++q) dst[q] = make_int4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
+        }
     }
     __syncthreads();
     const int lo = out_lo(t);
@@ -449,14 +433,16 @@ __global__ void __launch_bounds__(THREADS, 8) block_sort_w_kernel(const int *in,
         const int wpp = (2 * r) / WK;  // windows per pair
         const int j = w / wpp, o = w % wpp;
         const int ps = j * 2 * r;
-        const Win win{ps, r, ps + r, r, o * WK, WK};
-        merge_window(s, win, x, c[0], c[1], c[2], c[3]);
+        const bool last = 2 * r == TILE;
+        WinD win{ps, r, r, o * WK, 0, WK, !last && (j & 1)};
+        merge_window_desc(s, win, x, c[0], c[1], c[2], c[3]);
         __syncthreads();
-        if (2 * r == TILE) {
-            const int lim = valid - (ps + o * WK);
-            if (lim > 0) store_window(out + base, ps + o * WK, lim, lo, x);
+        if (last) {
+            const int lim = valid - o * WK;
+            win.cnt = lim < WK ? lim : WK;
+            if (lim > 0) store_window_desc<false>(out + base, win, ps, lo, x);
         } else {
-            store_window(s, ps + o * WK, WK, lo, x);
+            store_window_desc<true>(s, win, ps, lo, x);
             __syncthreads();
         }
     }
@@ -482,13 +468,20 @@ __global__ void __launch_bounds__(THREADS, 8) mergew_kernel(const int *__restric
     __shared__ int cpre[F + 1];          // chunks before segment s (cpre[F] = chunks of the tile)
     __shared__ uint8_t gseg[NCHUNK / 4 + 2];  // segment of chunk 64 G (first of wave group G)
     __shared__ uint64_t s_out;
-    __shared__ int s_total;
-    __shared__ int4 wtab_a[LOGF][WAVES * MAXWIN];  // per level and window: pa, na, pb, nb
-    __shared__ int2 wtab_b[LOGF][WAVES * MAXWIN];  // d0, wreal (0 = no window)
-
+    __shared__ int4 wtab_a[LOGF][WAVES * MAXWIN];  // per level and window: pa, na, nb, d0
+    __shared__ int4 wtab_b[LOGF][WAVES * MAXWIN];  // skip, cnt (0 = no window), desc, -
     const int t = lane_id();
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
     const uint64_t j = blockIdx.x;
+#ifdef DSORT_SPREAD
+    // Experiment: spread the first generation of workgroups over one tile duration so that
+    // their HBM staging bursts do not coincide (later workgroups inherit the offsets).
+    if (blockIdx.x < 512) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+        const unsigned long long dly = (unsigned long long)((blockIdx.x * 37u) % 16u) * (DSORT_SPREAD / 16);
+        while (__builtin_amdgcn_s_memtime() - t0 < dly) __builtin_amdgcn_s_sleep(16);
+    }
+#endif
     STAMP(0);
     TileInfo ti;
     const GroupK *g = tile_info<REG>(pd, j, tnom, ti);
@@ -523,7 +516,6 @@ __global__ void __launch_bounds__(THREADS, 8) mergew_kernel(const int *__restric
             slen[i] = len;
             cpre[i + 1] = cinc;
             if (i == 0) cpre[0] = 0;
-            if (i == F - 1) s_total = incl;
             if (i == 0) {
                 soff[0] = 0;
                 s_out = ti.base + before;
@@ -532,7 +524,6 @@ __global__ void __launch_bounds__(THREADS, 8) mergew_kernel(const int *__restric
     }
     __syncthreads();
     STAMP(1);
-    const int total = __builtin_amdgcn_readfirstlane(s_total);
     const int nchunks = __builtin_amdgcn_readfirstlane(cpre[F]);
     // segment of the first chunk of every 64-chunk wave group
     if (threadIdx.x < NCHUNK / 4 + 2) {
@@ -547,12 +538,13 @@ __global__ void __launch_bounds__(THREADS, 8) mergew_kernel(const int *__restric
     }
     __syncthreads();
     STAMP(2);
-    // Window table of every level, built once by wave 0 from the segment offsets alone (they do
-    // not depend on the keys): level l merges pairs of 2^l-segment groups; pair p is cut into
-    // ceil(len / 1024) windows; window k of the level goes to wave k % 16 (k < 16 * MAXWIN).
-    if (w == 0) {
-#pragma unroll 1
-        for (int l = 0; l < LOGF; ++l) {
+    // Window table of every level, built from the segment offsets alone (they do not depend on
+    // the keys): level l merges pairs of 2^l-segment groups; pair p is cut into ceil(len / 1024)
+    // windows; window k of the level goes to wave k % 16 (k < 16 * MAXWIN).  Wave l builds the
+    // table of level l, in parallel with the other waves' staging.
+    if (w < LOGF) {
+        {
+            const int l = w;
             const int npairs = F >> (l + 1);
             int ps = 0, pm = 0, pe = 0, nw = 0;
             if (t < npairs) {
@@ -574,16 +566,16 @@ __global__ void __launch_bounds__(THREADS, 8) mergew_kernel(const int *__restric
             const int fps = __shfl(ps, pp), fpm = __shfl(pm, pp), fpe = __shfl(pe, pp);
             const int first = __shfl(incl - nw, pp);
             if (t < WAVES * MAXWIN) {
-                int4 a;
-                int2 b;
+                int4 a = make_int4(0, 0, 0, 0), b = make_int4(0, 0, 0, 0);  // cnt 0: no window
                 if (p < npairs) {
-                    const int d0 = (t - first) * WK;
                     const int len = fpe - fps;
-                    a = make_int4(fps, fpm - fps, fpm, fpe - fpm);
-                    b = make_int2(d0, len - d0 < WK ? len - d0 : WK);
-                } else {
-                    a = make_int4(0, 0, 0, 0);
-                    b = make_int2(0, 0);  // no window
+                    const int dn = (t - first) * WK;  // nominal start of the window
+                    const int rem = len - dn;
+                    // the last window of a pair of >= 1024 keys is shifted to end at the pair's end
+                    const int d0 = rem < WK && len >= WK ? len - WK : dn;
+                    a = make_int4(fps, fpm - fps, fpe - fpm, d0);
+                    // groups that become the B run of the next level are stored descending
+                    b = make_int4(dn - d0, rem < WK ? rem : WK, (l + 1 < LOGF) && (p & 1), 0);
                 }
                 wtab_a[l][t] = a;
                 wtab_b[l][t] = b;
@@ -597,12 +589,13 @@ __global__ void __launch_bounds__(THREADS, 8) mergew_kernel(const int *__restric
     {
         constexpr int NK = (TILE / 4 + kWaveMaxF + THREADS - 1) / THREADS;  // chunks per thread
         int4 v[NK];
-        int ebase[NK], lo4[NK], hi4[NK];
+        int ebase[NK], lo4[NK], hi4[NK], dirk[NK];
 #pragma unroll
         for (int k = 0; k < NK; ++k) {
             const int q = threadIdx.x + k * THREADS;
             const int G = w + k * WAVES;
             ebase[k] = 0;
+            dirk[k] = 1;
             lo4[k] = 0;
             hi4[k] = 0;  // no valid key
             if (G * 64 < nchunks) {  // wave-uniform
@@ -614,7 +607,9 @@ __global__ void __launch_bounds__(THREADS, 8) mergew_kernel(const int *__restric
                 const int qc = q < nchunks ? q : cpre[sg];  // past the last chunk: a valid one
                 const int64_t g = sa0[sg] + 4 * (int64_t)(qc - cpre[sg]);
                 const int off = (int)(g - sgs[sg]);  // key offset of the chunk in its segment
-                ebase[k] = soff[sg] + off;
+                // odd segments (B runs of level 0) are staged descending
+                dirk[k] = (sg & 1) ? -1 : 1;
+                ebase[k] = (sg & 1) ? soff[sg] + slen[sg] - 1 - off : soff[sg] + off;
                 lo4[k] = -off;                       // valid j: -off <= j < len - off
                 hi4[k] = q < nchunks ? slen[sg] - off : 0;
                 v[k] = *reinterpret_cast<const int4 *>(in + g);
@@ -625,7 +620,7 @@ __global__ void __launch_bounds__(THREADS, 8) mergew_kernel(const int *__restric
             const int vals[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
 #pragma unroll
             for (int jj = 0; jj < 4; ++jj)
-                if (jj >= lo4[k] && jj < hi4[k]) s[ebase[k] + jj] = vals[jj];
+                if (jj >= lo4[k] && jj < hi4[k]) s[ebase[k] + dirk[k] * jj] = vals[jj];
         }
     }
     STAMP(3);
@@ -640,30 +635,30 @@ __global__ void __launch_bounds__(THREADS, 8) mergew_kernel(const int *__restric
 #pragma unroll 1
     for (int l = 0; l < LOGF; ++l) {
         const bool last = l + 1 == LOGF;
-        Win win[MAXWIN];
+        WinD win[MAXWIN];
 #pragma unroll
         for (int h = 0; h < MAXWIN; ++h) {
             const int4 a = wtab_a[l][w + h * WAVES];
-            const int2 b = wtab_b[l][w + h * WAVES];
+            const int4 b = wtab_b[l][w + h * WAVES];
             win[h].pa = __builtin_amdgcn_readfirstlane(a.x);
             win[h].na = __builtin_amdgcn_readfirstlane(a.y);
-            win[h].pb = __builtin_amdgcn_readfirstlane(a.z);
-            win[h].nb = __builtin_amdgcn_readfirstlane(a.w);
-            win[h].d0 = __builtin_amdgcn_readfirstlane(b.x);
-            win[h].wreal = __builtin_amdgcn_readfirstlane(b.y);
+            win[h].nb = __builtin_amdgcn_readfirstlane(a.z);
+            win[h].d0 = __builtin_amdgcn_readfirstlane(a.w);
+            win[h].skip = __builtin_amdgcn_readfirstlane(b.x);
+            win[h].cnt = __builtin_amdgcn_readfirstlane(b.y);
+            win[h].desc = __builtin_amdgcn_readfirstlane(b.z);
         }
         int x[MAXWIN][R];
 #pragma unroll
         for (int h = 0; h < MAXWIN; ++h)
-            if (win[h].wreal > 0) merge_window(s, win[h], x[h], c0, c1, c2, c3);
+            if (win[h].cnt > 0) merge_window_desc(s, win[h], x[h], c0, c1, c2, c3);
         STAMP(5 + 2 * l);
         __syncthreads();
 #pragma unroll
         for (int h = 0; h < MAXWIN; ++h) {
-            if (win[h].wreal > 0) {
-                const int ob = win[h].pa + win[h].d0;
-                if (last) store_window(outp, ob, win[h].wreal, lo, x[h]);
-                else store_window(s, ob, win[h].wreal, lo, x[h]);
+            if (win[h].cnt > 0) {
+                if (last) store_window_desc<false>(outp, win[h], win[h].pa, lo, x[h]);
+                else store_window_desc<true>(s, win[h], win[h].pa, lo, x[h]);
             }
         }
         if (!last) __syncthreads();
