@@ -73,9 +73,19 @@ __device__ unsigned long long g_stamps[kStampTiles * 32];
         if ((threadIdx.x & 63) == 0 && (threadIdx.x >> 6) % 15 == 0 && blockIdx.x < kStampTiles) \
             g_stamps[blockIdx.x * 32 + (threadIdx.x >> 6 ? 16 : 0) + (k)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
+// wave 0's s_memrealtime (100 MHz, comparable across CUs) at tile start, staging start and end,
+// tile end, in free slots 13, 14, 15, 29
+#define RSTAMP(slot)                                                                          \
+    do {                                                                                      \
+        if (threadIdx.x == 0 && blockIdx.x < kStampTiles)                                     \
+            g_stamps[blockIdx.x * 32 + (slot)] = __builtin_amdgcn_s_memrealtime();            \
+    } while (0)
 #else
 #define STAMP(k) \
     do {         \
+    } while (0)
+#define RSTAMP(slot) \
+    do {             \
     } while (0)
 #endif
 
@@ -458,31 +468,20 @@ __global__ void __launch_bounds__(THREADS, 8) mergew_kernel(const int *__restric
                                                             const uint32_t *__restrict__ splits) {
     constexpr int F = 1 << LOGF;
     constexpr int MAXWIN = (WAVES + F / 2 + WAVES - 1) / WAVES;
-    constexpr int NCHUNK = TILE / 64;
     __shared__ __attribute__((aligned(16))) int s[TILE + WK];  // + slack read by load_window
-    __shared__ int soff[F + 1];
+    __shared__ int soff[F + 1];          // tile position of segment i (soff[F] = keys of the tile)
     // Staging works on 16-byte-aligned chunks of 4 keys of each segment (absolute alignment):
-    __shared__ int64_t sgs[F];           // global index of the segment's first key
-    __shared__ int64_t sa0[F];           // global index of its first aligned chunk (may be < sgs)
-    __shared__ int slen[F];              // keys in the segment
-    __shared__ int cpre[F + 1];          // chunks before segment s (cpre[F] = chunks of the tile)
-    __shared__ uint8_t gseg[NCHUNK / 4 + 2];  // segment of chunk 64 G (first of wave group G)
+    __shared__ int cpre[F + 1];          // chunks before segment i (cpre[F] = chunks of the tile)
+    __shared__ int4 sinfo[F];            // cpre[i], soff[i], keys, first chunk - first key (-3..0)
+    __shared__ int64_t sa0[F];           // global index of the segment's first aligned chunk
     __shared__ uint64_t s_out;
     __shared__ int4 wtab_a[LOGF][WAVES * MAXWIN];  // per level and window: pa, na, nb, d0
     __shared__ int4 wtab_b[LOGF][WAVES * MAXWIN];  // skip, cnt (0 = no window), desc, -
     const int t = lane_id();
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
     const uint64_t j = blockIdx.x;
-#ifdef DSORT_SPREAD
-    // Experiment: spread the first generation of workgroups over one tile duration so that
-    // their HBM staging bursts do not coincide (later workgroups inherit the offsets).
-    if (blockIdx.x < 512) {
-        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-        const unsigned long long dly = (unsigned long long)((blockIdx.x * 37u) % 16u) * (DSORT_SPREAD / 16);
-        while (__builtin_amdgcn_s_memtime() - t0 < dly) __builtin_amdgcn_s_sleep(16);
-    }
-#endif
     STAMP(0);
+    RSTAMP(13);
     TileInfo ti;
     const GroupK *g = tile_info<REG>(pd, j, tnom, ti);
     if (threadIdx.x < 64) {
@@ -511,9 +510,8 @@ __global__ void __launch_bounds__(THREADS, 8) mergew_kernel(const int *__restric
         }
         if (t < F) {
             soff[i + 1] = incl;
-            sgs[i] = gs;
             sa0[i] = a0;
-            slen[i] = len;
+            sinfo[i] = make_int4(cinc - nc, incl - len, len, (int)(a0 - gs));
             cpre[i + 1] = cinc;
             if (i == 0) cpre[0] = 0;
             if (i == 0) {
@@ -525,94 +523,87 @@ __global__ void __launch_bounds__(THREADS, 8) mergew_kernel(const int *__restric
     __syncthreads();
     STAMP(1);
     const int nchunks = __builtin_amdgcn_readfirstlane(cpre[F]);
-    // segment of the first chunk of every 64-chunk wave group
-    if (threadIdx.x < NCHUNK / 4 + 2) {
-        const int q = threadIdx.x * 64;
-        int lo = 0, hi = F - 1;  // last segment whose chunks start at or before q
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (cpre[mid] <= q) lo = mid;
-            else hi = mid - 1;
-        }
-        gseg[threadIdx.x] = (uint8_t)lo;
-    }
-    __syncthreads();
+    if (nchunks == 0) return;  // empty tile (workgroup-uniform)
     STAMP(2);
-    // Window table of every level, built from the segment offsets alone (they do not depend on
-    // the keys): level l merges pairs of 2^l-segment groups; pair p is cut into ceil(len / 1024)
-    // windows; window k of the level goes to wave k % 16 (k < 16 * MAXWIN).  Wave l builds the
-    // table of level l, in parallel with the other waves' staging.
-    if (w < LOGF) {
-        {
-            const int l = w;
-            const int npairs = F >> (l + 1);
-            int ps = 0, pm = 0, pe = 0, nw = 0;
-            if (t < npairs) {
-                ps = soff[t << (l + 1)];
-                pm = soff[((2 * t + 1) << l)];
-                pe = soff[(t + 1) << (l + 1)];
-                nw = (pe - ps + WK - 1) / WK;
-            }
-            int incl = nw;
-            for (int o = 1; o < 16; o <<= 1) {
-                const int v = __shfl_up(incl, o);
-                if (t >= o) incl += v;
-            }
-            // lane k (< WAVES * MAXWIN) describes window k: its pair is the number of pairs whose
-            // windows all come before k
-            int p = 0;
-            for (int q = 0; q < npairs; ++q) p += __builtin_amdgcn_readlane(incl, q) <= t ? 1 : 0;
-            const int pp = p < npairs ? p : 0;
-            const int fps = __shfl(ps, pp), fpm = __shfl(pm, pp), fpe = __shfl(pe, pp);
-            const int first = __shfl(incl - nw, pp);
-            if (t < WAVES * MAXWIN) {
-                int4 a = make_int4(0, 0, 0, 0), b = make_int4(0, 0, 0, 0);  // cnt 0: no window
-                if (p < npairs) {
-                    const int len = fpe - fps;
-                    const int dn = (t - first) * WK;  // nominal start of the window
-                    const int rem = len - dn;
-                    // the last window of a pair of >= 1024 keys is shifted to end at the pair's end
-                    const int d0 = rem < WK && len >= WK ? len - WK : dn;
-                    a = make_int4(fps, fpm - fps, fpe - fpm, d0);
-                    // groups that become the B run of the next level are stored descending
-                    b = make_int4(dn - d0, rem < WK ? rem : WK, (l + 1 < LOGF) && (p & 1), 0);
-                }
-                wtab_a[l][t] = a;
-                wtab_b[l][t] = b;
-            }
-        }
-    }
+    RSTAMP(14);
     // Staging: chunk q (4 keys, 16-B aligned in global memory) is loaded by thread q % THREADS
     // with one dwordx4 (consecutive lanes on consecutive chunks of a segment: 1 KiB per wave
     // instruction); the keys of a chunk that lie outside its segment are dropped.  An aligned
-    // 16-B block holding a key of the array never crosses a page, so edge chunks are safe.
+    // 16-B block holding a key of the array never crosses a page, so edge chunks are safe; lanes
+    // past the last chunk load the last chunk again and drop it.
     {
         constexpr int NK = (TILE / 4 + kWaveMaxF + THREADS - 1) / THREADS;  // chunks per thread
         int4 v[NK];
-        int ebase[NK], lo4[NK], hi4[NK], dirk[NK];
+        int ebase[NK], lo4[NK], hi4[NK], dirk[NK], qc[NK], sg[NK];
+        // All chunk addresses are computed branch-free and side by side (the searches of the NK
+        // chunks interleave), so the NK loads leave together; lanes past the last chunk load the
+        // last chunk again.
 #pragma unroll
         for (int k = 0; k < NK; ++k) {
             const int q = threadIdx.x + k * THREADS;
-            const int G = w + k * WAVES;
-            ebase[k] = 0;
-            dirk[k] = 1;
-            lo4[k] = 0;
-            hi4[k] = 0;  // no valid key
-            if (G * 64 < nchunks) {  // wave-uniform
-                const int first = __builtin_amdgcn_readfirstlane((int)gseg[G]);
-                const int lastg = __builtin_amdgcn_readfirstlane((int)gseg[G + 1]);
-                int sg = first;
-#pragma unroll 1
-                for (int qq = first + 1; qq <= lastg; ++qq) sg += cpre[qq] <= q ? 1 : 0;
-                const int qc = q < nchunks ? q : cpre[sg];  // past the last chunk: a valid one
-                const int64_t g = sa0[sg] + 4 * (int64_t)(qc - cpre[sg]);
-                const int off = (int)(g - sgs[sg]);  // key offset of the chunk in its segment
-                // odd segments (B runs of level 0) are staged descending
-                dirk[k] = (sg & 1) ? -1 : 1;
-                ebase[k] = (sg & 1) ? soff[sg] + slen[sg] - 1 - off : soff[sg] + off;
-                lo4[k] = -off;                       // valid j: -off <= j < len - off
-                hi4[k] = q < nchunks ? slen[sg] - off : 0;
-                v[k] = *reinterpret_cast<const int4 *>(in + g);
+            qc[k] = q < nchunks ? q : nchunks - 1;
+            sg[k] = 0;  // last segment whose chunks start at or before qc (a non-empty one)
+        }
+#pragma unroll
+        for (int st = F / 2; st >= 1; st >>= 1) {
+#pragma unroll
+            for (int k = 0; k < NK; ++k) sg[k] += cpre[sg[k] + st] <= qc[k] ? st : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < NK; ++k) {
+            const int4 si = sinfo[sg[k]];
+            const int c = 4 * (qc[k] - si.x);
+            const int off = si.w + c;  // key offset of the chunk in its segment
+            // odd segments (B runs of level 0) are staged descending
+            const bool odd = sg[k] & 1;
+            dirk[k] = odd ? -1 : 1;
+            ebase[k] = odd ? si.y + si.z - 1 - off : si.y + off;
+            lo4[k] = -off;  // valid j: -off <= j < len - off
+            hi4[k] = threadIdx.x + k * THREADS < nchunks ? si.z - off : 0;
+            v[k] = *reinterpret_cast<const int4 *>(in + sa0[sg[k]] + c);
+        }
+        // Window table of every level, built from the segment offsets alone (they do not depend on
+        // the keys): level l merges pairs of 2^l-segment groups; pair p is cut into ceil(len / 1024)
+        // windows; window k of the level goes to wave k % 16 (k < 16 * MAXWIN).  Wave l builds the
+        // table of level l while its staging loads are in flight.
+        if (w < LOGF) {
+            {
+                const int l = w;
+                const int npairs = F >> (l + 1);
+                int ps = 0, pm = 0, pe = 0, nw = 0;
+                if (t < npairs) {
+                    ps = soff[t << (l + 1)];
+                    pm = soff[((2 * t + 1) << l)];
+                    pe = soff[(t + 1) << (l + 1)];
+                    nw = (pe - ps + WK - 1) / WK;
+                }
+                int incl = nw;
+                for (int o = 1; o < 16; o <<= 1) {
+                    const int v = __shfl_up(incl, o);
+                    if (t >= o) incl += v;
+                }
+                // lane k (< WAVES * MAXWIN) describes window k: its pair is the number of pairs whose
+                // windows all come before k
+                int p = 0;
+                for (int q = 0; q < npairs; ++q) p += __builtin_amdgcn_readlane(incl, q) <= t ? 1 : 0;
+                const int pp = p < npairs ? p : 0;
+                const int fps = __shfl(ps, pp), fpm = __shfl(pm, pp), fpe = __shfl(pe, pp);
+                const int first = __shfl(incl - nw, pp);
+                if (t < WAVES * MAXWIN) {
+                    int4 a = make_int4(0, 0, 0, 0), b = make_int4(0, 0, 0, 0);  // cnt 0: no window
+                    if (p < npairs) {
+                        const int len = fpe - fps;
+                        const int dn = (t - first) * WK;  // nominal start of the window
+                        const int rem = len - dn;
+                        // the last window of a pair of >= 1024 keys is shifted to end at the pair's end
+                        const int d0 = rem < WK && len >= WK ? len - WK : dn;
+                        a = make_int4(fps, fpm - fps, fpe - fpm, d0);
+                        // groups that become the B run of the next level are stored descending
+                        b = make_int4(dn - d0, rem < WK ? rem : WK, (l + 1 < LOGF) && (p & 1), 0);
+                    }
+                    wtab_a[l][t] = a;
+                    wtab_b[l][t] = b;
+                }
             }
         }
 #pragma unroll
@@ -626,6 +617,7 @@ __global__ void __launch_bounds__(THREADS, 8) mergew_kernel(const int *__restric
     STAMP(3);
     __syncthreads();
     STAMP(4);
+    RSTAMP(15);
 
     const int c0 = lane_side(0), c1 = lane_side(1), c2 = lane_side(2), c3 = lane_side(3);
     const int lo = out_lo(t);
@@ -663,6 +655,7 @@ __global__ void __launch_bounds__(THREADS, 8) mergew_kernel(const int *__restric
         }
         if (!last) __syncthreads();
         STAMP(6 + 2 * l);
+        if (last) RSTAMP(29);
     }
 }
 

@@ -36,3 +36,25 @@ for wv, off in (("wave0", 0), ("wave15", 16)):
     print(f"{wv}: tile total median {np.median(tot):.0f} cyc p90 {np.percentile(tot, 90):.0f}")
     for k, nm in enumerate(names):
         print(f"   {nm:10s} median {np.median(d[:, k]):8.0f}  p90 {np.percentile(d[:, k], 90):8.0f}")
+
+# Concurrency of the staging phase among all workgroups, on the s_memrealtime stamps (100 MHz,
+# comparable across CUs; slots 13 tile start, 14 staging start, 15 staging end, 29 tile end):
+# if workgroups are phase-locked, staging overlaps in bursts.
+R = S[:, [13, 14, 15, 29]]
+R = R[R[:, 3] > R[:, 3].max() - 200000]  # tiles of the last launch (< 2 ms before its end)
+t0 = R[:, 0].min()
+grid = np.arange(t0, R[:, 3].max(), 2)
+stg = np.zeros(grid.size, np.int32)
+live = np.zeros(grid.size, np.int32)
+for s0, a, b, e in R:
+    stg[np.searchsorted(grid, a):np.searchsorted(grid, b)] += 1
+    live[np.searchsorted(grid, s0):np.searchsorted(grid, e)] += 1
+mid = slice(grid.size // 10, grid.size * 9 // 10)
+print(f"span {(R[:, 3].max() - t0) / 100:.0f} us; live WGs mean {live[mid].mean():.1f}; staging WGs "
+      f"mean {stg[mid].mean():.1f} p10 {np.percentile(stg[mid], 10):.0f} p50 "
+      f"{np.percentile(stg[mid], 50):.0f} p90 {np.percentile(stg[mid], 90):.0f} max {stg[mid].max()}")
+print(f"staging median {np.median(R[:, 2] - R[:, 1]) * 10:.0f} ns, tile median "
+      f"{np.median(R[:, 3] - R[:, 0]) * 10:.0f} ns")
+tl = np.arange(grid.size // 3, grid.size // 3 + 60 * 50, 50)  # 60 samples, 1 us apart
+print("staging WGs every 1 us:", " ".join(str(stg[i]) for i in tl))
+print("live WGs every 1 us:   ", " ".join(str(live[i]) for i in tl))
