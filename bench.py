@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--kill-after-pass", type=int, default=1,
                     help="the dying worker SIGKILLs itself after this merge pass of its local sort")
     ap.add_argument("--reassign", choices=["first-live", "next-live"], default="first-live")
+    ap.add_argument("--codec", action="store_true",
+                    help="time the GPU text codec (output.txt format + %%d parse) on --keys sorted keys")
     return ap.parse_args()
 
 
@@ -297,8 +299,79 @@ def run_fault(args):
     print(json.dumps(out), flush=True)
 
 
+def run_codec(args):
+    """the reference's text I/O on the GPU.  Formats `--keys` sorted uniform int32
+    keys to output.txt bytes (server.c:517-519) and parses them back (server.c:179/213's %d
+    tokens), each timed over `--steps` calls with the data resident in HBM; verifies the round
+    trip.  The CPU leg times the oracle's single-threaded codec on a 2^24-key sample."""
+    ctx = dsort.Context(0)
+    n = args.keys
+    keys = make_input(ctx, n, 0, "i32", "uniform")
+    ctx.sort_dev(keys)
+    text = torch.empty(12 * n, dtype=torch.uint8, device="cuda")
+    back = torch.empty(n, dtype=torch.int32, device="cuda")
+    for _ in range(args.warmup):
+        ln = ctx.format_text(keys, text)
+        ctx.parse_text(text, ln, back)
+    torch.cuda.synchronize()
+    res = {}
+    for name, fn in (("format", lambda: ctx.format_text(keys, text)),
+                     ("parse", lambda: ctx.parse_text(text, ln, back))):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.steps):
+            r = fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / args.steps
+        if name == "format":
+            ln = r
+        res[name] = ms
+    if not (ctx.parse_text(text, ln, back) == n and torch.equal(back, keys)):
+        raise SystemExit("bench: codec round trip failed")
+    moved = 4 * n + ln  # algorithmic bytes of either direction: the keys plus the text
+    out = {"metric": "output.txt format keys/sec (GPU text codec, SURVEY 8f.1)", "unit": "keys/s",
+           "value": n / (res["format"] * 1e-3), "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+           "higher_is_better": True, "dtype": "int32", "data": "synthetic uniform keys, sorted",
+           "config": {"workload": f"{n} sorted int32 keys <-> {ln} bytes of %d\\n text", "keys": n,
+                      "text_bytes": ln},
+           "format_ms": round(res["format"], 4), "parse_ms": round(res["parse"], 4),
+           "parse_keys_per_s": n / (res["parse"] * 1e-3),
+           "roofline": {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+                        "format_achieved": round(moved / (res["format"] * 1e-3) / 1e9, 1),
+                        "parse_achieved": round(moved / (res["parse"] * 1e-3) / 1e9, 1),
+                        "format_frac": round(moved / (res["format"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                        "parse_frac": round(moved / (res["parse"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                        "algorithmic_bytes": moved}}
+    if not args.no_cpu_baseline:
+        orc = ctypes.CDLL(os.path.join(REPO, "oracle", "liboracle.so"))
+        orc.oracle_format_i32.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]
+        orc.oracle_format_i32.restype = ctypes.c_long
+        orc.oracle_parse_i32.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]
+        orc.oracle_parse_i32.restype = ctypes.c_long
+        m = min(n, 1 << 24)
+        sample = keys[:m].cpu().numpy()
+        buf = np.empty(12 * m, np.uint8)
+        t0 = time.perf_counter()
+        L = orc.oracle_format_i32(sample.ctypes.data, m, buf.ctypes.data, buf.size)
+        t1 = time.perf_counter()
+        dst = np.empty(m, np.int32)
+        c = orc.oracle_parse_i32(buf.ctypes.data, L, dst.ctypes.data, m)
+        t2 = time.perf_counter()
+        assert c == m and np.array_equal(dst, sample)
+        out["cpu_baseline"] = {"value": m / (t1 - t0), "unit": "keys/s (format)", "cores": 1, "kind": "port",
+                               "parse_keys_per_s": m / (t2 - t1),
+                               "sample": f"{m} sorted uniform int32 keys, oracle_format_i32 / oracle_parse_i32 "
+                                         "(single thread)"}
+    print(json.dumps(out), flush=True)
+    ctx.close()
+
+
 def main():
     args = parse()
+    if args.codec:
+        run_codec(args)
+        return
     if args.kill_rank is not None:
         if "WORLD_SIZE" in os.environ:
             raise SystemExit("--kill-rank runs its own master and workers: launch it without torchrun")

@@ -68,10 +68,11 @@ static int ensure_host(dsort_ctx *ctx, void **buf, size_t *have, size_t need) {
     return DSORT_OK;
 }
 
-static hipStream_t pick(dsort_ctx *ctx, void *stream) {
+hipStream_t pick_stream(dsort_ctx *ctx, void *stream) {
     if (stream == DSORT_NULL_STREAM) return static_cast<hipStream_t>(nullptr);
     return stream ? static_cast<hipStream_t>(stream) : ctx->stream;
 }
+static hipStream_t pick(dsort_ctx *ctx, void *stream) { return pick_stream(ctx, stream); }
 
 // ------------------------------------------------------------------ utility kernels ------
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
@@ -579,7 +580,7 @@ int dsort_finalize(dsort_ctx *ctx) {
         ctx->comm = nullptr;
     }
     void *bufs[] = {ctx->scratch, ctx->scratch2, ctx->splits, ctx->groups, ctx->io, ctx->io2, ctx->red,
-                    ctx->local, ctx->recv, ctx->recv2, ctx->small};
+                    ctx->local, ctx->recv, ctx->recv2, ctx->small, ctx->text_status};
     for (void *b : bufs)
         if (b) hipFree(b);
     if (ctx->red_host) hipHostFree(ctx->red_host);

@@ -82,6 +82,8 @@ struct dsort_ctx {
     size_t io_bytes = 0;
     void *io2 = nullptr;
     size_t io2_bytes = 0;
+    void *text_status = nullptr;  // per-tile look-back status words of the text codec
+    size_t text_status_bytes = 0;
     void *red = nullptr;       // 64 B of reduction accumulators
     uint64_t *red_host = nullptr;  // pinned mirror
     // sample sort (multi-GPU)
@@ -118,6 +120,8 @@ struct dsort_ctx {
 namespace dsort {
 
 int set_err(dsort_ctx *ctx, int code, const std::string &msg);
+// the stream argument of the C-ABI: NULL = the context's stream, DSORT_NULL_STREAM = stream 0
+hipStream_t pick_stream(dsort_ctx *ctx, void *stream);
 int hip_err(dsort_ctx *ctx, hipError_t e, const char *what);
 int ensure(dsort_ctx *ctx, void **buf, size_t *have, size_t need, const char *what);
 

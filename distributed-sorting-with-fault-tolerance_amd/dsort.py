@@ -37,7 +37,8 @@ EXPORTS = [
     "dsort_plan_sample_positions", "dsort_gen_uniform_i32", "dsort_gen_uniform_i64",
     "dsort_gen_zipf_i64", "dsort_fingerprint_i32", "dsort_fingerprint_i64",
     "dsort_count_descents_i32", "dsort_count_descents_i64", "dsort_dev_alloc", "dsort_dev_free",
-    "dsort_copy_h2d", "dsort_copy_d2h", "dsort_write_text_i32",
+    "dsort_copy_h2d", "dsort_copy_d2h", "dsort_write_text_i32", "dsort_format_text_dev_i32",
+    "dsort_parse_text_dev_i32",
 ]
 
 
@@ -179,6 +180,8 @@ def load():
         "dsort_copy_h2d": (ctypes.c_int, [P, P, P, SZ]),
         "dsort_copy_d2h": (ctypes.c_int, [P, P, P, SZ]),
         "dsort_write_text_i32": (ctypes.c_int, [ctypes.c_char_p, P, SZ]),
+        "dsort_format_text_dev_i32": (ctypes.c_int, [P, P, SZ, P, SZ, ctypes.POINTER(SZ), P]),
+        "dsort_parse_text_dev_i32": (ctypes.c_int, [P, P, SZ, P, SZ, ctypes.POINTER(SZ), P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -364,6 +367,24 @@ class Context:
         self.check(getattr(self.lib, f"dsort_count_descents_{self._tsfx(t)}")(self.h, t.data_ptr(), n,
                                                                                ctypes.byref(c)))
         return c.value
+
+    def format_text(self, keys, text):
+        """output.txt bytes of int32 CUDA tensor `keys` into uint8 CUDA tensor `text` (>= 12 bytes
+        per key); returns the byte count (dsort_format_text_dev_i32)."""
+        assert keys.dtype == torch.int32 and text.dtype == torch.uint8
+        ln = ctypes.c_size_t()
+        self.check(self.lib.dsort_format_text_dev_i32(self.h, keys.data_ptr(), keys.numel(), text.data_ptr(),
+                                                      text.numel(), ctypes.byref(ln), self._stream()))
+        return ln.value
+
+    def parse_text(self, text, nbytes, keys):
+        """Parse the first `nbytes` of uint8 CUDA tensor `text` (16-byte aligned) into int32 CUDA
+        tensor `keys`; returns the token count (dsort_parse_text_dev_i32)."""
+        assert keys.dtype == torch.int32 and text.dtype == torch.uint8 and nbytes <= text.numel()
+        cnt = ctypes.c_size_t()
+        self.check(self.lib.dsort_parse_text_dev_i32(self.h, text.data_ptr(), nbytes, keys.data_ptr(),
+                                                     keys.numel(), ctypes.byref(cnt), self._stream()))
+        return cnt.value
 
     def stats(self):
         st = Stats()

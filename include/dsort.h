@@ -206,6 +206,24 @@ int dsort_copy_d2h(dsort_ctx *ctx, void *h_dst, const void *d_src, size_t bytes)
  * Host-only helper; returns DSORT_EINVAL if the file cannot be written. */
 int dsort_write_text_i32(const char *path, const int32_t *keys, size_t n);
 
+/* GPU text codec, asynchronous on `stream` (NULL: the context's stream) up to
+ * the returned length/count, which synchronizes.
+ *
+ * dsort_format_text_dev_i32 replaces the output loop of merge_chunks (server.c:517-519,
+ * fprintf(output, "%d\n", merged[i])): writes the output.txt bytes of n device keys to d_text
+ * (cap >= 12 * n bytes, else DSORT_EINVAL) and their count to *out_len.
+ *
+ * dsort_parse_text_dev_i32 replaces the two fscanf("%d") passes of main (server.c:179-182 and
+ * 212-214): parses whitespace-separated [+-]?[0-9]+ tokens of d_text (16-byte aligned, len bytes)
+ * into d_keys in file order; *n_out = the number of tokens (keys past cap are counted, not
+ * stored).  Values beyond int32 saturate at 2^32 and wrap (the oracle's rule; %d overflow is
+ * undefined in the reference).  A token that is not an integer returns DSORT_EINVAL, with its
+ * byte offset in dsort_last_error (the reference loops forever there). */
+int dsort_format_text_dev_i32(dsort_ctx *ctx, const int32_t *d_keys, size_t n, char *d_text,
+                              size_t cap, size_t *out_len, void *stream);
+int dsort_parse_text_dev_i32(dsort_ctx *ctx, const char *d_text, size_t len, int32_t *d_keys,
+                             size_t cap, size_t *n_out, void *stream);
+
 #ifdef __cplusplus
 }
 #endif
