@@ -353,4 +353,50 @@ int dsort_parse_text_dev_i32(dsort_ctx *ctx, const char *d_text, size_t len, int
     return DSORT_OK;
 }
 
+// Host-buffer forms for the C master (server.c's parse and output.txt write): stage through the
+// context's device arenas.
+int dsort_parse_text_i32(dsort_ctx *ctx, const char *text, size_t len, int32_t *keys, size_t cap,
+                         size_t *n_out) {
+    if (!ctx || !n_out || (len && !text) || (cap && !keys))
+        return set_err(ctx, DSORT_EINVAL, "null argument");
+    *n_out = 0;
+    if (!len) return DSORT_OK;
+    int rc = ensure(ctx, &ctx->io, &ctx->io_bytes, len, "text staging");
+    if (!rc) rc = ensure(ctx, &ctx->io2, &ctx->io2_bytes, (cap ? cap : 1) * sizeof(int32_t), "key staging");
+    if (rc) return rc;
+    hipStream_t s = ctx->stream;
+    DSORT_HIP(ctx, hipMemcpyAsync(ctx->io, text, len, hipMemcpyHostToDevice, s));
+    size_t cnt = 0;
+    rc = dsort_parse_text_dev_i32(ctx, static_cast<const char *>(ctx->io), len,
+                                  static_cast<int32_t *>(ctx->io2), cap, &cnt, s);
+    if (rc) return rc;
+    const size_t got = cnt < cap ? cnt : cap;
+    if (got) DSORT_HIP(ctx, hipMemcpyAsync(keys, ctx->io2, got * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    DSORT_HIP(ctx, hipStreamSynchronize(s));
+    *n_out = cnt;
+    return DSORT_OK;
+}
+
+int dsort_format_text_i32(dsort_ctx *ctx, const int32_t *keys, size_t n, char *text, size_t cap,
+                          size_t *len_out) {
+    if (!ctx || !len_out || (n && (!keys || !text)))
+        return set_err(ctx, DSORT_EINVAL, "null argument");
+    *len_out = 0;
+    if (!n) return DSORT_OK;
+    int rc = ensure(ctx, &ctx->io, &ctx->io_bytes, n * sizeof(int32_t), "key staging");
+    if (!rc) rc = ensure(ctx, &ctx->io2, &ctx->io2_bytes, 12 * n, "text staging");
+    if (rc) return rc;
+    hipStream_t s = ctx->stream;
+    DSORT_HIP(ctx, hipMemcpyAsync(ctx->io, keys, n * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    size_t ln = 0;
+    rc = dsort_format_text_dev_i32(ctx, static_cast<const int32_t *>(ctx->io), n,
+                                   static_cast<char *>(ctx->io2), 12 * n, &ln, s);
+    if (rc) return rc;
+    if (ln > cap) return set_err(ctx, DSORT_EINVAL, "text buffer too small");
+    DSORT_HIP(ctx, hipMemcpyAsync(text, ctx->io2, ln, hipMemcpyDeviceToHost, s));
+    DSORT_HIP(ctx, hipStreamSynchronize(s));
+    *len_out = ln;
+    return DSORT_OK;
+}
+
 }  // extern "C"

@@ -38,7 +38,7 @@ EXPORTS = [
     "dsort_gen_zipf_i64", "dsort_fingerprint_i32", "dsort_fingerprint_i64",
     "dsort_count_descents_i32", "dsort_count_descents_i64", "dsort_dev_alloc", "dsort_dev_free",
     "dsort_copy_h2d", "dsort_copy_d2h", "dsort_write_text_i32", "dsort_format_text_dev_i32",
-    "dsort_parse_text_dev_i32",
+    "dsort_parse_text_dev_i32", "dsort_parse_text_i32", "dsort_format_text_i32",
 ]
 
 
@@ -182,6 +182,8 @@ def load():
         "dsort_write_text_i32": (ctypes.c_int, [ctypes.c_char_p, P, SZ]),
         "dsort_format_text_dev_i32": (ctypes.c_int, [P, P, SZ, P, SZ, ctypes.POINTER(SZ), P]),
         "dsort_parse_text_dev_i32": (ctypes.c_int, [P, P, SZ, P, SZ, ctypes.POINTER(SZ), P]),
+        "dsort_parse_text_i32": (ctypes.c_int, [P, ctypes.c_char_p, SZ, P, SZ, ctypes.POINTER(SZ)]),
+        "dsort_format_text_i32": (ctypes.c_int, [P, P, SZ, P, SZ, ctypes.POINTER(SZ)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -385,6 +387,23 @@ class Context:
         self.check(self.lib.dsort_parse_text_dev_i32(self.h, text.data_ptr(), nbytes, keys.data_ptr(),
                                                      keys.numel(), ctypes.byref(cnt), self._stream()))
         return cnt.value
+
+    def parse_text_host(self, raw):
+        """Host bytes -> np.int32 keys through the GPU parser (dsort_parse_text_i32)."""
+        cap = len(raw) // 2 + 1
+        out = np.empty(cap, np.int32)
+        cnt = ctypes.c_size_t()
+        self.check(self.lib.dsort_parse_text_i32(self.h, raw, len(raw), _ptr(out), cap, ctypes.byref(cnt)))
+        return out[:cnt.value]
+
+    def format_text_host(self, keys):
+        """np.int32 keys -> output.txt bytes through the GPU formatter (dsort_format_text_i32)."""
+        keys = np.ascontiguousarray(keys, np.int32)
+        buf = ctypes.create_string_buffer(12 * keys.size + 1)
+        ln = ctypes.c_size_t()
+        self.check(self.lib.dsort_format_text_i32(self.h, _ptr(keys), keys.size, buf, len(buf),
+                                                  ctypes.byref(ln)))
+        return buf.raw[:ln.value]
 
     def stats(self):
         st = Stats()

@@ -1,11 +1,13 @@
 /* master.c -- the master node (role of the reference's server.c) with a GPU merge.
  *
  *   dsort_master [--workers N] [--proto v0|v1] [--device D] [--timeout SEC]
- *                [--retry-delay-ms MS] [--reassign first|least-loaded] [--output PATH] server.conf
+ *                [--retry-delay-ms MS] [--reassign first|least-loaded] [--codec gpu|cpu]
+ *                [--output PATH] server.conf
  *
  * Same session model as server.c: accept exactly N worker connections (server.c:148-157), then
  * read file names from stdin until "exit" (server.c:160-168).  Per file:
- *   1. parse whitespace-separated %d keys (server.c:177-182, 212-214);
+ *   1. parse whitespace-separated %d keys (server.c:177-182, 212-214), on the GPU by default
+ *      (dsort_parse_text_i32; --codec cpu keeps the host parser);
  *   2. split them into N contiguous chunks, chunk i holding n/N + (i < n%N) keys
  *      (server.c:185-216), and hand chunk i to worker i on its own thread (server.c:231-257);
  *   3. fault tolerance (server.c:297-477): a failed send or receive marks the worker dead and the
@@ -13,7 +15,8 @@
  *      result always lands in the chunk's own slot (server.c:415); a per-worker mutex held over
  *      the whole send->receive transaction serialises two chunks on one worker (server.c:344);
  *   4. merge the N sorted chunks on the GPU with dsort_merge_i32 -- where server.c:266 calls
- *      merge_chunks() -- and write output.txt, one "%d\n" per key (server.c:517-519).
+ *      merge_chunks() -- and write output.txt, one "%d\n" per key (server.c:517-519), formatted
+ *      on the GPU by default (dsort_format_text_i32).
  * Differences: liveness state is mutex-protected (the reference races on
  * is_alive[]), dead sockets are closed and stay dead, --timeout adds the deadline detection the
  * reference lacks, --reassign least-loaded is offered beside the reference's first-alive rule,
@@ -201,10 +204,29 @@ static long parse_keys(const char *t, size_t len, int32_t **out) {
     return (long)n;
 }
 
+/* output.txt: the GPU formatter (dsort_format_text_i32) or the host writer. */
+static int write_output(dsort_ctx *ctx, int gpu, const char *path, const int32_t *k, size_t n) {
+    if (!gpu) return dsort_write_text_i32(path, k, n);
+    char *buf = (char *)malloc(12 * n + 1);
+    size_t len = 0;
+    int rc = buf ? dsort_format_text_i32(ctx, k, n, buf, 12 * n + 1, &len) : DSORT_ENOMEM;
+    if (rc == 0) {
+        FILE *f = fopen(path, "w");
+        if (!f) {
+            rc = DSORT_EINVAL;
+        } else {
+            if (fwrite(buf, 1, len, f) != len) rc = DSORT_EINVAL;
+            if (fclose(f) != 0) rc = DSORT_EINVAL;
+        }
+    }
+    free(buf);
+    return rc;
+}
+
 static void usage(void) {
     fprintf(stderr, "usage: dsort_master [--workers N] [--proto v0|v1] [--device D] [--timeout SEC]\n"
                     "                    [--retry-delay-ms MS] [--reassign first|least-loaded]\n"
-                    "                    [--output PATH] server.conf\n");
+                    "                    [--codec gpu|cpu] [--output PATH] server.conf\n");
     exit(2);
 }
 
@@ -213,7 +235,7 @@ int main(int argc, char **argv) {
     memset(&cl, 0, sizeof cl);
     cl.n = 4; /* MAX_WORKERS, server.c:11 */
     cl.retry_delay_us = 100000;
-    int device = 0;
+    int device = 0, codec_gpu = 1;
     const char *out_path = "output.txt", *conf_path = NULL;
     for (int i = 1; i < argc; ++i) {
         if (!strcmp(argv[i], "--workers") && i + 1 < argc) cl.n = atoi(argv[++i]);
@@ -229,6 +251,11 @@ int main(int argc, char **argv) {
             ++i;
             if (!strcmp(argv[i], "first")) cl.least_loaded = 0;
             else if (!strcmp(argv[i], "least-loaded")) cl.least_loaded = 1;
+            else usage();
+        } else if (!strcmp(argv[i], "--codec") && i + 1 < argc) {
+            ++i;
+            if (!strcmp(argv[i], "gpu")) codec_gpu = 1;
+            else if (!strcmp(argv[i], "cpu")) codec_gpu = 0;
             else usage();
         } else if (!strcmp(argv[i], "--output") && i + 1 < argc) out_path = argv[++i];
         else if (argv[i][0] == '-') usage();
@@ -287,7 +314,24 @@ int main(int argc, char **argv) {
         char *text = read_file(name, &len);
         if (!text) { perror("Error opening file"); continue; }
         int32_t *keys = NULL;
-        long nk = parse_keys(text, len, &keys);
+        long nk;
+        if (codec_gpu) {
+            const size_t cap = len / 2 + 1;  /* at most one token per two bytes */
+            size_t cnt = 0;
+            keys = (int32_t *)malloc(cap * sizeof(int32_t));
+            rc = keys ? dsort_parse_text_i32(ctx, text, len, keys, cap, &cnt) : DSORT_ENOMEM;
+            if (rc && rc != DSORT_EINVAL) {
+                fprintf(stderr, "master: GPU parse failed (%d): %s\n", rc, dsort_last_error(ctx));
+                return 1;
+            }
+            nk = rc ? -1 : (long)cnt;
+            if (rc) {
+                free(keys);
+                keys = NULL;
+            }
+        } else {
+            nk = parse_keys(text, len, &keys);
+        }
         free(text);
         if (nk < 0) {
             fprintf(stderr, "master: %s contains a non-integer token; file skipped\n", name);
@@ -336,7 +380,7 @@ int main(int argc, char **argv) {
             int32_t *merged = (int32_t *)malloc((n ? n : 1) * sizeof(int32_t));
             rc = merged ? dsort_merge_i32(ctx, runs, lens, cl.n, merged) : DSORT_ENOMEM;
             double t_merged = now_ms();
-            if (rc == 0) rc = dsort_write_text_i32(out_path, merged, n);
+            if (rc == 0) rc = write_output(ctx, codec_gpu, out_path, merged, n);
             double t_written = now_ms();
             if (rc) {
                 fprintf(stderr, "master: merge/write failed (%d): %s\n", rc, dsort_last_error(ctx));

@@ -224,6 +224,15 @@ int dsort_format_text_dev_i32(dsort_ctx *ctx, const int32_t *d_keys, size_t n, c
 int dsort_parse_text_dev_i32(dsort_ctx *ctx, const char *d_text, size_t len, int32_t *d_keys,
                              size_t cap, size_t *n_out, void *stream);
 
+/* Host-buffer forms of the codec (synchronous; staged through the context's device arenas), for
+ * the C master at the server.c:179/213 parse and server.c:517-519 write positions.
+ * dsort_format_text_i32 returns DSORT_EINVAL if the text needs more than cap bytes (12 per key
+ * always suffice). */
+int dsort_parse_text_i32(dsort_ctx *ctx, const char *text, size_t len, int32_t *keys, size_t cap,
+                         size_t *n_out);
+int dsort_format_text_i32(dsort_ctx *ctx, const int32_t *keys, size_t n, char *text, size_t cap,
+                          size_t *len_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -60,3 +60,22 @@ int dsort_write_text_i32(const char *path, const int32_t *keys, size_t n) {
     free(buf);
     return (fclose(f) == 0 && ok) ? DSORT_OK : DSORT_EINVAL;
 }
+
+/* CPU stand-ins of the GPU text codec (host-buffer forms), for the master's plumbing tests. */
+int dsort_parse_text_i32(dsort_ctx *ctx, const char *text, size_t len, int32_t *keys, size_t cap,
+                         size_t *n_out) {
+    (void)ctx;
+    long n = oracle_parse_i32(text, len, keys, cap);
+    if (n < 0) return DSORT_EINVAL;
+    *n_out = (size_t)n;
+    return DSORT_OK;
+}
+
+int dsort_format_text_i32(dsort_ctx *ctx, const int32_t *keys, size_t n, char *text, size_t cap,
+                          size_t *len_out) {
+    (void)ctx;
+    long len = oracle_format_i32(keys, n, text, cap);
+    if (len < 0) return DSORT_EINVAL;
+    *len_out = (size_t)len;
+    return DSORT_OK;
+}

@@ -197,3 +197,16 @@ def test_format_parse_roundtrip_2p26(gpu_ctx):
     cnt = gpu_ctx.parse_text(buf, ln, back)
     assert cnt == n
     assert torch.equal(back, k)
+
+
+def test_host_buffer_forms_match_oracle(gpu_ctx, oracle, dsort_mod):
+    """dsort_parse_text_i32 / dsort_format_text_i32: the C master's parse and output.txt write."""
+    raw = open(os.path.join(GOLDEN, "ref_input.txt"), "rb").read()
+    assert np.array_equal(gpu_ctx.parse_text_host(raw), oracle.parse(raw))
+    a = np.random.default_rng(3).integers(INT_MIN, INT_MAX, 300001, endpoint=True).astype(np.int32)
+    txt = gpu_ctx.format_text_host(a)
+    assert txt == oracle.format(a)
+    assert np.array_equal(gpu_ctx.parse_text_host(txt), a)
+    assert gpu_ctx.format_text_host(np.zeros(0, np.int32)) == b""
+    with pytest.raises(dsort_mod.DsortError, match="byte 2$"):
+        gpu_ctx.parse_text_host(b"1 x")
