@@ -221,11 +221,15 @@ __global__ void __launch_bounds__(256) partk_kernel(const T *__restrict__ in, Pa
     // bracket: ilo = #keys < lo, ihi = #keys <= hi in run i; nlo = sum(ilo) <= d <= sum(ihi) = nhi
     uint64_t ilo = 0, ihi = rl;
     uint64_t nlo = 0, nhi = ti.gtotal;
-    bool interp = true;
+    // candidate selection: 0 = interpolation in key space (uniform-like keys), 1 = interpolation
+    // in the data (keys read from the run with the widest index bracket at the target's relative
+    // rank: any distribution, e.g. sparse heavy-duplicate Zipf keys), 2 = evenly spaced keys of
+    // that run (guaranteed progress).  A step that does not halve the bracket escalates.
+    int mode = 0;
     uint64_t cut_i = 0;
     bool done = false;
 #pragma unroll 1
-    for (int it = 0; it < 200 && !done; ++it) {
+    for (int it = 0; it < 4096 && !done; ++it) {
         if (nhi - nlo <= (uint64_t)slack) {  // cut just below lo: rank nlo in [d - slack, d]
             cut_i = ilo;
             done = true;
@@ -233,16 +237,29 @@ __global__ void __launch_bounds__(256) partk_kernel(const T *__restrict__ in, Pa
         }
         if (lo == hi) break;  // a single key left: exact tie split below
         T cand;
-        if (interp) {
-            const double n = (double)(nhi - nlo);
-            const double spread = fmax((double)slack * 0.5, 3.0 * sqrt(n));
-            const double r = C == 1 ? 0.0 : -spread + 2.0 * spread * (double)c / (double)(C - 1);
+        const double n = (double)(nhi - nlo);
+        const double spread = fmax((double)slack * 0.5, 3.0 * sqrt(n));
+        const double r = C == 1 ? 0.0 : -spread + 2.0 * spread * (double)c / (double)(C - 1);
+        if (mode == 0) {
             cand = key_at(lo, hi, ((double)d + r - (double)nlo) / n);
         } else {
-            using U = typename Unsigned<T>::type;
-            const U range = (U)hi - (U)lo;
-            const U q = range / (U)(C + 1), rr = range % (U)(C + 1);
-            cand = (T)((U)lo + q * (U)(c + 1) + (rr * (U)(c + 1)) / (U)(C + 1));
+            // the run with the widest bracket (ties: lowest run); its lane of candidate c reads
+            const uint64_t packed = wave_max(((ihi - ilo) << 6) | (uint64_t)(63 - i));
+            const int rr = 63 - (int)(packed & 63);
+            double frac = mode == 1 ? ((double)d + r - (double)nlo) / n : (double)(c + 1) / (double)(C + 1);
+            frac = frac < 0.0 ? 0.0 : (frac > 1.0 ? 1.0 : frac);
+            T mine = key_max<T>();
+            if (i == rr) {
+                const uint64_t range = ihi - ilo;  // > 0: the bracket holds more than slack keys
+                uint64_t pos = ilo + (uint64_t)(frac * (double)range);
+                pos = pos >= ihi ? ihi - 1 : pos;
+                mine = A[pos];
+            }
+            cand = __shfl(mine, c * F + rr);
+            // keep candidates in [lo, hi - 1] (non-decreasing in c): a candidate hi - 1 counts
+            // the keys below the block of the largest key, so a target inside a run of duplicates
+            // of hi collapses the bracket to that key on the next step
+            cand = cand < hi ? cand : (T)(hi - 1);
         }
         const uint64_t u = upper_bound_interp(A, ilo, ihi, cand, lo, hi, in + pd.n);
         uint64_t tot = u;
@@ -275,8 +292,14 @@ __global__ void __launch_bounds__(256) partk_kernel(const T *__restrict__ in, Pa
             ilo = ub_pr;
             nlo = tot_pr;
         }
-        // keep interpolating while it at least halves the bracket
-        interp = (nhi - nlo) * 2 <= before;
+        if (mode != 0) {
+            // tighten the key bracket to the keys actually inside the index bracket (keeps
+            // ilo = #keys < lo and ihi = #keys <= hi); one key left -> lo == hi
+            lo = wave_min(ilo < ihi ? A[ilo] : key_max<T>());
+            hi = wave_max(ilo < ihi ? A[ihi - 1] : key_min<T>());
+        }
+        const bool halved = (nhi - nlo) * 2 <= before;
+        mode = halved ? (mode == 2 ? 1 : mode) : (mode == 0 ? 1 : 2);
     }
     if (!done) {
         // lo == hi: ilo = #keys < key, ihi = #keys <= key; take d - sum(ilo) equal keys in run order

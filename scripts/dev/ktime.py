@@ -13,12 +13,29 @@ import dsort  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--keys", type=lambda s: int(eval(s, {}, {})), default=1 << 30)
 ap.add_argument("--reps", type=int, default=4)
+ap.add_argument("--dtype", choices=["i32", "i64"], default="i32")
+ap.add_argument("--dist", choices=["uniform", "zipf", "sorted", "reverse", "equal", "few", "byte"],
+                default="uniform")
 a = ap.parse_args()
 tag = os.environ.get("DSORT_LIB")
 tag = os.path.basename(os.path.dirname(tag)) if tag else "default"
+tag = f"{tag} {a.dtype} {a.dist}"
 ctx = dsort.Context(0)
-t = torch.empty(a.keys, dtype=torch.int32, device="cuda")
-ctx.gen_uniform(t, 0x5EED2026)
+t = torch.empty(a.keys, dtype=torch.int32 if a.dtype == "i32" else torch.int64, device="cuda")
+if a.dist == "zipf":
+    ctx.gen_zipf_i64(t, 0x5EED2026)
+else:
+    ctx.gen_uniform(t, 0x5EED2026)
+    if a.dist == "sorted":
+        t.copy_(torch.sort(t)[0])
+    elif a.dist == "reverse":
+        t.copy_(torch.sort(t, descending=True)[0])
+    elif a.dist == "equal":
+        t.fill_(12345)
+    elif a.dist == "few":  # 16 distinct keys spread over the whole range
+        t.copy_((t & 15) * (1 << 27) - (1 << 30))
+    elif a.dist == "byte":  # 256 distinct small keys
+        t.copy_(t & 255)
 o = torch.empty_like(t)
 best = None
 for _ in range(a.reps):
@@ -28,6 +45,6 @@ for _ in range(a.reps):
         best = st
 torch.cuda.synchronize()
 n = max(best["merge_kernel_launches"], 1)
-print(f"{tag:>14s}: total {best['total_ms']:.3f} ms  block {best['block_sort_ms']:.3f}  "
+print(f"{tag:>24s}: total {best['total_ms']:.3f} ms  block {best['block_sort_ms']:.3f}  "
       f"merge-kernel avg {best['merge_kernel_ms'] / n:.3f} ms x{best['merge_kernel_launches']}  "
       f"passes {best['merge_passes']}", flush=True)
