@@ -580,7 +580,8 @@ int dsort_finalize(dsort_ctx *ctx) {
         ctx->comm = nullptr;
     }
     void *bufs[] = {ctx->scratch, ctx->scratch2, ctx->splits, ctx->groups, ctx->io, ctx->io2, ctx->red,
-                    ctx->local, ctx->recv, ctx->recv2, ctx->small, ctx->text_status};
+                    ctx->local, ctx->recv, ctx->recv2, ctx->small, ctx->text_status,
+                    ctx->bucket};
     for (void *b : bufs)
         if (b) hipFree(b);
     if (ctx->red_host) hipHostFree(ctx->red_host);
@@ -589,6 +590,8 @@ int dsort_finalize(dsort_ctx *ctx) {
     if (ctx->xfer2) (void)hipHostFree(ctx->xfer2);
     if (ctx->groups_host) (void)hipHostFree(ctx->groups_host);
     if (ctx->groups_ev) (void)hipEventDestroy(ctx->groups_ev);
+    if (ctx->bucket_host) (void)hipHostFree(ctx->bucket_host);
+    if (ctx->bucket_ev) (void)hipEventDestroy(ctx->bucket_ev);
     for (auto &e : ctx->ev)
         if (e) (void)hipEventDestroy(e);
     for (auto &e : ctx->kev)

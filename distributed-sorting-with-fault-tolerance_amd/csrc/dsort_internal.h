@@ -56,6 +56,7 @@ struct PassDesc {
     int F;                   // runs per group, power of two
     int ngroups;             // irregular: entries in `groups`
     const GroupK *groups;    // irregular: group table (device memory)
+    const uint32_t *tile_group = nullptr;  // irregular, optional: group of every output tile
 };
 
 }  // namespace dsort
@@ -82,6 +83,11 @@ struct dsort_ctx {
     size_t io_bytes = 0;
     void *io2 = nullptr;
     size_t io2_bytes = 0;
+    void *bucket = nullptr;       // partition pass of the bucketed int32 sort (dsort_bucket.h)
+    size_t bucket_bytes = 0;
+    void *bucket_host = nullptr;  // pinned: bucket starts
+    size_t bucket_host_bytes = 0;
+    hipEvent_t bucket_ev = nullptr;
     void *text_status = nullptr;  // per-tile look-back status words of the text codec
     size_t text_status_bytes = 0;
     void *red = nullptr;       // 64 B of reduction accumulators

@@ -46,10 +46,14 @@ __device__ __forceinline__ const GroupK *tile_info(const PassDesc &pd, uint64_t 
         ti.jr = j - gi * tpg;
     } else {
         int lo = 0, hi = pd.ngroups - 1;  // last group with first_tile <= j
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (pd.groups[mid].first_tile <= j) lo = mid;
-            else hi = mid - 1;
+        if (pd.tile_group) {
+            lo = (int)pd.tile_group[j];  // one load instead of a dependent binary search
+        } else {
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (pd.groups[mid].first_tile <= j) lo = mid;
+                else hi = mid - 1;
+            }
         }
         g = pd.groups + lo;
         ti.base = g->base;

@@ -32,6 +32,7 @@
 
 #include <climits>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "dsort_internal.h"
@@ -388,15 +389,27 @@ __device__ __forceinline__ void store_window_desc(P *dst, const WinD &w, int ob,
 // ------------------------------------------------------------------------------------------
 // 1. Tile sort.
 // ------------------------------------------------------------------------------------------
+// tiles: NULL = tile j is keys [j * TILE, (j + 1) * TILE) of n; else tile j = tiles[j] (the
+// bucketed sort's tiles, which never cross a bucket), j < *ntiles.
 __global__ void __launch_bounds__(THREADS, 8) block_sort_w_kernel(const int *in, int *out,
-                                                                    uint64_t n) {
+                                                                    uint64_t n, const uint4 *tiles,
+                                                                    const uint32_t *ntiles) {
     // `in` may alias `out`: every workgroup reads its tile before it writes it
     __shared__ __attribute__((aligned(16))) int s[TILE + WK];  // + slack read by load_window
     const int t = lane_id();
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
-    const uint64_t base = (uint64_t)blockIdx.x * TILE;
-    const uint64_t rem = n - base;
-    const int valid = rem < (uint64_t)TILE ? (int)rem : TILE;
+    uint64_t base;
+    int valid;
+    if (tiles) {
+        if (blockIdx.x >= *ntiles) return;  // the grid is an upper bound
+        const uint4 r = tiles[blockIdx.x];  // TileRef: base (2 words), valid
+        base = (uint64_t)r.x | ((uint64_t)r.y << 32);
+        valid = (int)r.z;
+    } else {
+        base = (uint64_t)blockIdx.x * TILE;
+        const uint64_t rem = n - base;
+        valid = rem < (uint64_t)TILE ? (int)rem : TILE;
+    }
     const int c[6] = {lane_side(0), lane_side(1), lane_side(2), lane_side(3), lane_side(4),
                       lane_side(5)};
 
@@ -659,6 +672,8 @@ __global__ void __launch_bounds__(THREADS, 8) mergew_kernel(const int *__restric
     }
 }
 
+#include "dsort_bucket.h"
+
 // ------------------------------------------------------------------------------------------
 // Host side
 // ------------------------------------------------------------------------------------------
@@ -716,6 +731,205 @@ static int launch_pass_w(dsort_ctx *ctx, const int *src, int *dst, const PassDes
     return DSORT_OK;
 }
 
+// ---- bucketed sort (dsort_bucket.h) ------------------------------------------------------
+// Buckets of about 2^21 keys: at most 1024, and none below 2^25 keys (DSORT_BUCKETS=0 turns the
+// partition off, DSORT_BUCKETS=<B> forces B buckets).
+static int bucket_count(uint64_t n) {
+    const char *e = getenv("DSORT_BUCKETS");  // read per call: tests force small bucket counts
+    const int forced = e ? atoi(e) : -1;
+    if (forced == 0) return 0;
+    uint64_t B = forced > 0 ? (uint64_t)forced : (n >> 21);
+    if (forced < 0 && n < (1ull << 25)) return 0;
+    if (B > (uint64_t)BK_MAXB) B = BK_MAXB;
+    return B >= 2 ? (int)B : 0;
+}
+
+// Group tables of the merge passes inside buckets: pass p merges groups of up to 16
+// consecutive runs of one bucket; a bucket with a single run left is carried as a 1-run group.
+struct BucketPass {
+    int logf;
+    uint64_t ngroups, ntiles;
+    size_t group_off, tile_off;  // in the group / tile_group staging
+};
+
+static int bucket_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys, size_t n,
+                           hipStream_t s, bool timed, int B) {
+    const int BP = 1 << ceil_log2((uint64_t)B);
+    const uint64_t G = ceil_div(n, BK_WG);
+    const uint64_t nchunk = ceil_div(G, BK_CHUNK);
+    const uint32_t S = (uint32_t)B * BK_OS;
+    const uint64_t tmax = ceil_div(n, TILE) + 2 * (uint64_t)B;  // + a head and a tail per bucket
+    // device arena: samples, splitters, counts, chunk sums, offsets, bucket starts, tile table
+    size_t off = 0;
+    auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
+    const size_t o_smp = take((size_t)S * 8), o_spl = take((size_t)BP * 8),
+                 o_cnt = take((size_t)G * B * 4), o_part = take((size_t)nchunk * B * 8),
+                 o_offs = take((size_t)G * B * 8), o_bst = take((size_t)(B + 1) * 8),
+                 o_tpre = take((size_t)(B + 1) * 4), o_tt = take((size_t)tmax * sizeof(TileRef)),
+                 o_nt = take(4);
+    int rc = ensure(ctx, &ctx->bucket, &ctx->bucket_bytes, off, "bucket partition");
+    if (rc) return rc;
+    char *a = static_cast<char *>(ctx->bucket);
+    int64_t *smp = reinterpret_cast<int64_t *>(a + o_smp);
+    int64_t *spl = reinterpret_cast<int64_t *>(a + o_spl);
+    uint32_t *cnt = reinterpret_cast<uint32_t *>(a + o_cnt);
+    uint64_t *part = reinterpret_cast<uint64_t *>(a + o_part);
+    uint64_t *offs = reinterpret_cast<uint64_t *>(a + o_offs);
+    uint64_t *bst = reinterpret_cast<uint64_t *>(a + o_bst);
+    uint32_t *tpre = reinterpret_cast<uint32_t *>(a + o_tpre);
+    TileRef *tt = reinterpret_cast<TileRef *>(a + o_tt);
+    uint32_t *ntl = reinterpret_cast<uint32_t *>(a + o_nt);
+    rc = ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, n * sizeof(int32_t), "sort scratch");
+    if (rc) return rc;
+    int32_t *scratch = static_cast<int32_t *>(ctx->scratch);
+    if (ctx->bucket_host_bytes < (size_t)(B + 1) * 8) {
+        if (ctx->bucket_host) (void)hipHostFree(ctx->bucket_host);
+        ctx->bucket_host = nullptr;
+        ctx->bucket_host_bytes = 0;
+        DSORT_HIP(ctx, hipHostMalloc(&ctx->bucket_host, (size_t)BK_MAXB * 8 + 8, hipHostMallocDefault));
+        ctx->bucket_host_bytes = (size_t)BK_MAXB * 8 + 8;
+    }
+    if (!ctx->bucket_ev && hipEventCreateWithFlags(&ctx->bucket_ev, hipEventDisableTiming) != hipSuccess)
+        return set_err(ctx, DSORT_EHIP, "hipEventCreate");
+
+    // 1. splitters from a regular sample, sorted in (key, index) order by the int64 sort
+    hipLaunchKernelGGL(bucket_sample_kernel, dim3(ceil_div(S, 256)), dim3(256), 0, s, d_in, (uint64_t)n, smp, S);
+    DSORT_HIP(ctx, hipGetLastError());
+    rc = sort_device<int64_t>(ctx, smp, smp, S, s, false);
+    if (rc) return rc;
+    // (the int64 sort reset the statistics and events; the int32 sort's start from here)
+    ctx->stats = dsort_stats{};
+    ctx->stats.keys_in = ctx->stats.keys_out = n;
+    ctx->stats.tile_keys = TILE;
+    ctx->ev_mask = 0;
+    ctx->kev_used = 0;
+    ctx->last_stream = s;
+    if (timed && ctx->ev_ok) {
+        DSORT_HIP(ctx, hipEventRecord(ctx->ev[0], s));
+        ctx->ev_mask |= 1u;
+    }
+    hipLaunchKernelGGL(bucket_splitter_kernel, dim3(1), dim3(BK_MAXB), 0, s, smp, B, BP, spl);
+    // 2. histograms, their scan, the scatter
+    hipLaunchKernelGGL(bucket_hist_kernel, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, B, BP, cnt);
+    hipLaunchKernelGGL(bucket_colsum_kernel, dim3((unsigned)nchunk), dim3(BK_MAXB), 0, s, cnt, (uint32_t)G, B, part);
+    hipLaunchKernelGGL(bucket_scan_kernel, dim3(1), dim3(BK_MAXB), 0, s, part, (uint32_t)nchunk, B, bst, tpre, tt, ntl);
+    hipLaunchKernelGGL(bucket_offsets_kernel, dim3((unsigned)nchunk), dim3(BK_MAXB), 0, s, cnt, part, bst, (uint32_t)G, B, offs);
+    DSORT_HIP(ctx, hipGetLastError());
+    // bucket starts to the host (the pass plan depends on the bucket sizes)
+    uint64_t *hb = static_cast<uint64_t *>(ctx->bucket_host);
+    DSORT_HIP(ctx, hipMemcpyAsync(hb, bst, (size_t)(B + 1) * 8, hipMemcpyDeviceToHost, s));
+    DSORT_HIP(ctx, hipEventRecord(ctx->bucket_ev, s));
+    // the scatter goes to the buffer the tile sort reads; choose it once the pass count is
+    // known (the host waits for the bucket starts while the scatter runs)
+    DSORT_HIP(ctx, hipEventSynchronize(ctx->bucket_ev));
+    std::vector<uint64_t> bsz(B);
+    for (int b = 0; b < B; ++b) bsz[b] = hb[b + 1] - hb[b];
+    if (hb[B] != n) return set_err(ctx, DSORT_EHIP, "bucket partition lost keys");
+    // pass plan: runs per bucket, merged 16 at a time inside each bucket
+    constexpr int MAXF = 16;
+    std::vector<std::vector<uint64_t>> runs(B);
+    int passes = 0;
+    for (int b = 0; b < B; ++b) {
+        // the tile sort's runs of bucket b (bucket_tiles: a 0..3-key head, then TILE-key tiles)
+        const uint64_t h = bucket_head(hb[b], bsz[b]);
+        if (h) runs[b].push_back(h);
+        for (uint64_t o = h; o < bsz[b]; o += TILE) runs[b].push_back(bsz[b] - o < (uint64_t)TILE ? bsz[b] - o : TILE);
+        int p = 0;
+        for (uint64_t r = runs[b].size(); r > 1; r = ceil_div(r, MAXF)) ++p;
+        passes = p > passes ? p : passes;
+    }
+    ctx->stats.merge_passes = passes;
+    int32_t *bufs[2] = {d_keys, scratch};
+    int cur = (passes % 2 == 0) ? 0 : 1;  // tile sort output; the passes end in d_keys
+    // scatter into the tile sort's buffer unless that is the input (in-place sort)
+    int32_t *part_out = (bufs[cur] == d_in) ? bufs[cur ^ 1] : bufs[cur];
+    hipLaunchKernelGGL(bucket_scatter_kernel, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, B, BP, offs, part_out);
+    DSORT_HIP(ctx, hipGetLastError());
+    // 3. tile sort inside the buckets
+    hipLaunchKernelGGL(block_sort_w_kernel, dim3((unsigned)tmax), dim3(THREADS), 0, s, part_out,
+                       bufs[cur], (uint64_t)n, reinterpret_cast<const uint4 *>(tt), ntl);
+    DSORT_HIP(ctx, hipGetLastError());
+    if (timed && ctx->ev_ok) {
+        DSORT_HIP(ctx, hipEventRecord(ctx->ev[1], s));
+        ctx->ev_mask |= 2u;
+    }
+    // 4. group tables of every pass (one staging buffer, one copy)
+    std::vector<BucketPass> plan;
+    std::vector<GroupK> groups;
+    std::vector<uint32_t> tgroup;
+    for (int p = 0; p < passes; ++p) {
+        BucketPass bp{1, 0, 0, groups.size(), tgroup.size()};
+        int maxr = 1;
+        uint64_t base = 0, tiles = 0;
+        for (int b = 0; b < B; ++b) {
+            std::vector<uint64_t> next;
+            const size_t nr = runs[b].size();
+            for (size_t r0 = 0; r0 < nr; r0 += MAXF) {
+                GroupK gk{};
+                gk.base = base;
+                gk.first_tile = tiles;
+                gk.roff[0] = 0;
+                uint64_t tot = 0;
+                for (size_t r = r0; r < nr && r < r0 + MAXF; ++r) {
+                    tot += runs[b][r];
+                    gk.roff[++gk.nruns] = tot;
+                }
+                for (int r = (int)gk.nruns + 1; r <= kMaxF; ++r) gk.roff[r] = tot;
+                gk.total = tot;
+                maxr = (int)gk.nruns > maxr ? (int)gk.nruns : maxr;
+                const uint64_t gt = ceil_div(tot, (uint64_t)TNOM);
+                for (uint64_t k = 0; k < gt; ++k) tgroup.push_back((uint32_t)(groups.size() - bp.group_off));
+                tiles += gt;
+                base += tot;
+                next.push_back(tot);
+                groups.push_back(gk);
+            }
+            runs[b].swap(next);
+        }
+        bp.logf = ceil_log2((uint64_t)maxr) < 1 ? 1 : ceil_log2((uint64_t)maxr);
+        bp.ngroups = groups.size() - bp.group_off;
+        bp.ntiles = tiles;
+        plan.push_back(bp);
+    }
+    if (passes > 0) {
+        const size_t gbytes = groups.size() * sizeof(GroupK), tbytes = tgroup.size() * sizeof(uint32_t);
+        const size_t tb_off = (gbytes + 255) & ~(size_t)255;
+        if (ctx->groups_ev_pending) DSORT_HIP(ctx, hipEventSynchronize(ctx->groups_ev));
+        ctx->groups_ev_pending = false;
+        if (ctx->groups_host_bytes < tb_off + tbytes) {
+            if (ctx->groups_host) (void)hipHostFree(ctx->groups_host);
+            ctx->groups_host = nullptr;
+            ctx->groups_host_bytes = 0;
+            DSORT_HIP(ctx, hipHostMalloc(&ctx->groups_host, tb_off + tbytes, hipHostMallocDefault));
+            ctx->groups_host_bytes = tb_off + tbytes;
+        }
+        rc = ensure(ctx, &ctx->groups, &ctx->groups_bytes, tb_off + tbytes, "group table");
+        if (rc) return rc;
+        std::memcpy(ctx->groups_host, groups.data(), gbytes);
+        std::memcpy(static_cast<char *>(ctx->groups_host) + tb_off, tgroup.data(), tbytes);
+        DSORT_HIP(ctx, hipMemcpyAsync(ctx->groups, ctx->groups_host, tb_off + tbytes, hipMemcpyHostToDevice, s));
+        if (!ctx->groups_ev && hipEventCreateWithFlags(&ctx->groups_ev, hipEventDisableTiming) != hipSuccess)
+            return set_err(ctx, DSORT_EHIP, "hipEventCreate");
+        DSORT_HIP(ctx, hipEventRecord(ctx->groups_ev, s));
+        ctx->groups_ev_pending = true;
+        const GroupK *dg = static_cast<const GroupK *>(ctx->groups);
+        const uint32_t *dt = reinterpret_cast<const uint32_t *>(static_cast<const char *>(ctx->groups) + tb_off);
+        for (int p = 0; p < passes; ++p) {
+            PassDesc pd{(uint64_t)n, 0, 1 << plan[p].logf, (int)plan[p].ngroups, dg + plan[p].group_off};
+            pd.tile_group = dt + plan[p].tile_off;
+            rc = launch_pass_w<false>(ctx, bufs[cur], bufs[cur ^ 1], pd, plan[p].logf, plan[p].ntiles, s, timed);
+            if (rc) return rc;
+            cur ^= 1;
+            fault_point(s, p);
+        }
+    }
+    if (timed && ctx->ev_ok) {
+        DSORT_HIP(ctx, hipEventRecord(ctx->ev[2], s));
+        ctx->ev_mask |= 4u;
+    }
+    return DSORT_OK;
+}
+
 }  // namespace wv
 
 #ifdef DSORT_STAMPS
@@ -739,6 +953,7 @@ int wave_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys, size_t n
             DSORT_HIP(ctx, hipMemcpyAsync(d_keys, d_in, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
         return DSORT_OK;
     }
+    if (const int B = bucket_count(n)) return bucket_sort_i32(ctx, d_in, d_keys, n, s, timed, B);
     const uint64_t tiles = ceil_div(n, TILE);
     const std::vector<int> plan = plan_passes(tiles);
     const int passes = (int)plan.size();
@@ -756,7 +971,7 @@ int wave_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys, size_t n
         ctx->ev_mask |= 1u;
     }
     hipLaunchKernelGGL(block_sort_w_kernel, dim3((unsigned)tiles), dim3(THREADS), 0, s, d_in,
-                       bufs[cur], (uint64_t)n);
+                       bufs[cur], (uint64_t)n, nullptr, nullptr);
     DSORT_HIP(ctx, hipGetLastError());
     if (timed && ctx->ev_ok) {
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[1], s));

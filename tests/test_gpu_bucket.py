@@ -1,0 +1,82 @@
+"""The bucketed int32 sort (dsort_bucket.h: sample-splitter partition pass, then the tile sort and
+the k-way merge passes inside every bucket) against numpy on the MI355X.  DSORT_BUCKETS forces a
+bucket count at any size (the library reads it per call), so small inputs exercise the same
+kernels as the 2^30-key bench: empty buckets, single-run buckets, 0..3-key head tiles, heavy
+duplicates split across buckets by the (key, index) composite."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+INT_MIN, INT_MAX = -(2**31), 2**31 - 1
+TILE = 16384
+
+
+def _keys(rng, kind, n):
+    if kind == "uniform":
+        return rng.integers(INT_MIN, INT_MAX, n, endpoint=True).astype(np.int32)
+    if kind == "equal":
+        return np.full(n, 7, np.int32)
+    if kind == "few":
+        return (rng.integers(0, 4, n) * 1000 - 1500).astype(np.int32)
+    if kind == "sorted":
+        return np.sort(rng.integers(INT_MIN, INT_MAX, n, endpoint=True).astype(np.int32))
+    if kind == "reverse":
+        return np.sort(rng.integers(INT_MIN, INT_MAX, n, endpoint=True).astype(np.int32))[::-1].copy()
+    if kind == "extremes":
+        return rng.choice(np.array([INT_MIN, INT_MIN + 1, -1, 0, 1, INT_MAX - 1, INT_MAX], np.int32), n)
+    if kind == "narrow":  # every key inside one radix slot of the bucket lookup
+        return rng.integers(1000, 1064, n).astype(np.int32)
+    raise ValueError(kind)
+
+
+def _sort(ctx, a, inplace):
+    import torch
+    t = torch.from_numpy(a).cuda()
+    if inplace:
+        ctx.sort_dev(t)
+        out = t
+    else:
+        out = torch.empty_like(t)
+        ctx.sort_dev(t, out)
+        assert np.array_equal(t.cpu().numpy(), a)  # the input is left alone
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
+
+
+@pytest.mark.parametrize("kind", ["uniform", "equal", "few", "sorted", "reverse", "extremes", "narrow"])
+@pytest.mark.parametrize("B,n", [(2, 100_003), (3, 17), (7, 3 * TILE + 5), (33, 1_000_003),
+                                 (64, 4 * TILE), (1024, 500_000)])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_bucketed_sort_vs_numpy(gpu_ctx, monkeypatch, kind, B, n, inplace):
+    monkeypatch.setenv("DSORT_BUCKETS", str(B))
+    a = _keys(np.random.default_rng(B * 131 + n), kind, n)
+    assert np.array_equal(_sort(gpu_ctx, a, inplace), np.sort(a))
+
+
+@pytest.mark.parametrize("tiles,passes", [(200, 2), (300, 3)])
+def test_bucketed_sort_multi_pass_buckets(gpu_ctx, monkeypatch, tiles, passes):
+    """Few buckets of many tiles: more than 16 (256) runs per bucket -> 2 (3) merge passes."""
+    monkeypatch.setenv("DSORT_BUCKETS", "2")
+    a = _keys(np.random.default_rng(tiles), "uniform", 2 * tiles * TILE + 777)
+    assert np.array_equal(_sort(gpu_ctx, a, False), np.sort(a))
+    assert gpu_ctx.stats()["merge_passes"] == passes
+
+
+def test_bucketed_default_at_2p26_matches_regular_path(gpu_ctx, monkeypatch):
+    """Default bucket count at 2^26 (32 buckets) and DSORT_BUCKETS=0 (regular passes): same
+    output, no descents, same multiset."""
+    import torch
+    n = 1 << 26
+    t = torch.empty(n, dtype=torch.int32, device="cuda")
+    gpu_ctx.gen_uniform(t, 0x5EED2026)
+    fp = gpu_ctx.fingerprint(t)
+    o1, o2 = torch.empty_like(t), torch.empty_like(t)
+    monkeypatch.delenv("DSORT_BUCKETS", raising=False)
+    gpu_ctx.sort_dev(t, o1)
+    assert gpu_ctx.stats()["merge_passes"] == 2  # 32 buckets of ~2^21 keys: ~128 runs each
+    monkeypatch.setenv("DSORT_BUCKETS", "0")
+    gpu_ctx.sort_dev(t, o2)
+    torch.cuda.synchronize()
+    assert gpu_ctx.descents(o1) == 0 and gpu_ctx.fingerprint(o1) == fp
+    assert torch.equal(o1, o2)
