@@ -401,7 +401,7 @@ def main():
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": pmc_traffic("mergew_kernel", n, k["w"]), "avg_launch_ms": round(avg_launch_ms, 4),
             "algorithmic_bytes_per_launch": bytes_per_launch,
-            "block_sort_ms": round(k["block_ms"] / args.steps, 3),
+            "partition_and_tile_sort_ms": round(k["block_ms"] / args.steps, 3),
             "whole_sort_single_pass_bound_frac": round(2 * k["w"] * n / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
         }
         if not args.no_cpu_baseline and args.dtype == "i32":
