@@ -1,5 +1,6 @@
-// dsort_bucket.h -- the int32 sort with a sample-splitter partition pass in front (included by
-// dsort_wave.hip inside namespace dsort::wv; uses its tile sort and k-way pass kernels).
+// dsort_bucket.h -- the sample-splitter partition pass in front of the sorts (namespace
+// dsort::bk; included by dsort_wave.hip for int32 and dsort_sort.hip for int64, whose drivers run
+// their own tile sort and k-way passes inside the buckets).
 //
 // The multi-GPU design cuts the keys into key ranges with sample-sort splitters and sorts every
 // range on its own GPU.  The same idea inside one GPU's HBM: B buckets (about
@@ -22,30 +23,74 @@
 //   bucket_scatter_kernel  per 16384-key sub-tile: keys grouped by bucket in LDS, then written
 //                          to their buckets (consecutive lanes on consecutive keys of a bucket)
 #pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dsort {
+namespace bk {
 
 constexpr int BK_T = 1024;               // threads of the partition kernels
-constexpr int BK_K = 16;                 // keys per thread per sub-tile
-constexpr int BK_SUB = BK_T * BK_K;      // 16384 keys per sub-tile
-constexpr int BK_SUBS = 4;               // sub-tiles per workgroup
-constexpr int BK_WG = BK_SUB * BK_SUBS;  // 65536 keys per partition workgroup
+constexpr int BK_WG = 65536;             // keys per partition workgroup
 constexpr int BK_MAXB = 1024;            // buckets at most (<= threads, one bucket per thread)
 constexpr int BK_OS = 32;                // samples per bucket
 constexpr int BK_CHUNK = 64;             // workgroups per column-sum chunk
 
+// Scatter sub-tile per key width: KPT keys per thread, SUB = BK_T * KPT keys staged in LDS.
+template <typename T> struct Geo;
+template <> struct Geo<int32_t> { static constexpr int KPT = 16; };
+template <> struct Geo<int64_t> { static constexpr int KPT = 8; };
+
 struct TileRef {
     uint64_t base;   // first key of the tile
-    uint32_t valid;  // keys in the tile (<= TILE)
+    uint32_t valid;  // keys in the tile (<= the tile size)
     uint32_t pad;
 };
 
-__device__ __forceinline__ int64_t composite(int32_t key, uint64_t idx) {
-    return (int64_t)((uint64_t)(int64_t)key << 32 | (uint32_t)idx);
-}
+// The composite order (key, input index): unique per key, so duplicates spread over buckets.
+// int32: packed in one int64 (key * 2^32 + index); int64: a (key, index) pair.
+struct Pair {
+    int64_t k;
+    uint32_t i, pad;
+};
+template <typename T> struct Comp;
+template <> struct Comp<int32_t> {
+    using C = int64_t;
+    __host__ __device__ static C make(int32_t key, uint64_t idx) {
+        return (int64_t)((uint64_t)(int64_t)key << 32 | (uint32_t)idx);
+    }
+    __host__ __device__ static bool lt(C a, C b) { return a < b; }
+    __host__ __device__ static C inf() { return INT64_MAX; }
+    // composite (key of the slot start, index 0) of sign-flipped key prefix `u`
+    __host__ __device__ static C slot_start(uint64_t ubias) {
+        return (int64_t)(((uint64_t)((uint32_t)ubias ^ 0x80000000u)) << 32);
+    }
+    __host__ __device__ static uint32_t slot_of(int32_t key, int bits) {
+        return ((uint32_t)key ^ 0x80000000u) >> (32 - bits);
+    }
+    static constexpr int KB = 32;  // key bits
+};
+template <> struct Comp<int64_t> {
+    using C = Pair;
+    __host__ __device__ static C make(int64_t key, uint64_t idx) { return Pair{key, (uint32_t)idx, 0}; }
+    __host__ __device__ static bool lt(const C &a, const C &b) {
+        return a.k < b.k || (a.k == b.k && a.i < b.i);
+    }
+    __host__ __device__ static C inf() { return Pair{INT64_MAX, 0xFFFFFFFFu, 0}; }
+    __host__ __device__ static C slot_start(uint64_t ubias) {
+        return Pair{(int64_t)(ubias ^ 0x8000000000000000ull), 0, 0};
+    }
+    __host__ __device__ static uint32_t slot_of(int64_t key, int bits) {
+        return (uint32_t)(((uint64_t)key ^ 0x8000000000000000ull) >> (64 - bits));
+    }
+    static constexpr int KB = 64;
+};
 
 // bucket of composite c: the number of splitters below c (spl holds BP entries, +inf padded)
-__device__ __forceinline__ int bucket_of(const int64_t *spl, int BP, int64_t c) {
+template <typename T>
+__device__ __forceinline__ int bucket_of(const typename Comp<T>::C *spl, int BP,
+                                         const typename Comp<T>::C &c) {
     int lo = 0;
-    for (int st = BP >> 1; st >= 1; st >>= 1) lo += spl[lo + st - 1] < c ? st : 0;
+    for (int st = BP >> 1; st >= 1; st >>= 1) lo += Comp<T>::lt(spl[lo + st - 1], c) ? st : 0;
     return lo;
 }
 
@@ -56,81 +101,90 @@ __device__ __forceinline__ int bucket_of(const int64_t *spl, int BP, int64_t c) 
 constexpr int BK_SLOTB = 12;
 constexpr int BK_SLOTS = 1 << BK_SLOTB;
 
-__device__ __forceinline__ void build_slots(const int64_t *spl, int BP, uint32_t *rng) {
+template <typename T>
+__device__ __forceinline__ void build_slots(const typename Comp<T>::C *spl, int BP, uint32_t *rng) {
+    using CT = Comp<T>;
     for (int i = threadIdx.x; i < BK_SLOTS; i += blockDim.x) {
         uint32_t cnt[2];
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
-            // splitters with key < (slot i + e) start, as a composite: key * 2^32 + 0
-            const uint64_t su = (uint64_t)(i + e) << (32 - BK_SLOTB);  // biased key of the start
-            const int64_t c = i + e == BK_SLOTS ? INT64_MAX
-                                                : (int64_t)((uint64_t)((uint32_t)su ^ 0x80000000u) << 32);
-            cnt[e] = (uint32_t)bucket_of(spl, BP, c);
+            // splitters whose key lies below the start of slot i + e
+            const uint64_t su = (uint64_t)(i + e) << (CT::KB - BK_SLOTB);  // sign-flipped key
+            const typename CT::C c = i + e == BK_SLOTS ? CT::inf() : CT::slot_start(su);
+            cnt[e] = (uint32_t)bucket_of<T>(spl, BP, c);
         }
         rng[i] = cnt[0] | (cnt[1] << 16);
     }
 }
 
-__device__ __forceinline__ int bucket_fast(const int64_t *spl, const uint32_t *rng, int32_t key,
-                                           int64_t c) {
-    const uint32_t r = rng[((uint32_t)key ^ 0x80000000u) >> (32 - BK_SLOTB)];
+template <typename T>
+__device__ __forceinline__ int bucket_fast(const typename Comp<T>::C *spl, const uint32_t *rng,
+                                           T key, const typename Comp<T>::C &c) {
+    const uint32_t r = rng[Comp<T>::slot_of(key, BK_SLOTB)];
     int lo = (int)(r & 0xFFFF), hi = (int)(r >> 16);
     while (lo < hi) {  // lower bound among the splitters of the slot
         const int mid = (lo + hi) >> 1;
-        if (spl[mid] < c) lo = mid + 1;
+        if (Comp<T>::lt(spl[mid], c)) lo = mid + 1;
         else hi = mid;
     }
     return lo;
 }
 
-__global__ void __launch_bounds__(256) bucket_sample_kernel(const int32_t *__restrict__ in,
-                                                            uint64_t n, int64_t *__restrict__ smp,
+template <typename T>
+__global__ void __launch_bounds__(256) bucket_sample_kernel(const T *__restrict__ in, uint64_t n,
+                                                            typename Comp<T>::C *__restrict__ smp,
                                                             uint32_t s) {
     const uint32_t k = blockIdx.x * 256 + threadIdx.x;
     if (k >= s) return;
     const uint64_t pos = ((2 * (uint64_t)k + 1) * n) / (2 * (uint64_t)s);
-    smp[k] = composite(in[pos], pos);
+    smp[k] = Comp<T>::make(in[pos], pos);
 }
 
-__global__ void __launch_bounds__(BK_MAXB) bucket_splitter_kernel(const int64_t *__restrict__ smp,
+// splitter b = sample (b+1)*BK_OS - 1 of the sorted samples, b < B-1; +inf up to BP
+template <typename T>
+__global__ void __launch_bounds__(BK_MAXB) bucket_splitter_kernel(const typename Comp<T>::C *__restrict__ smp,
                                                                  int B, int BP,
-                                                                 int64_t *__restrict__ spl) {
+                                                                 typename Comp<T>::C *__restrict__ spl) {
     const int b = threadIdx.x;
-    if (b < BP) spl[b] = b < B - 1 ? smp[(uint64_t)(b + 1) * BK_OS - 1] : INT64_MAX;
+    if (b < BP) spl[b] = b < B - 1 ? smp[(uint64_t)(b + 1) * BK_OS - 1] : Comp<T>::inf();
 }
 
-__device__ __forceinline__ void load_splitters(const int64_t *spl_g, int BP, int64_t *spl) {
+template <typename T>
+__device__ __forceinline__ void load_splitters(const typename Comp<T>::C *spl_g, int BP,
+                                               typename Comp<T>::C *spl) {
     for (int b = threadIdx.x; b < BP; b += BK_T) spl[b] = spl_g[b];
 }
 
-// counts[g * B + b] = keys of workgroup g's 65536 keys in bucket b
-__global__ void __launch_bounds__(BK_T) bucket_hist_kernel(const int32_t *__restrict__ in,
-                                                           uint64_t n,
-                                                           const int64_t *__restrict__ spl_g,
+// counts[g * B + b] = keys of workgroup g's BK_WG keys in bucket b
+template <typename T>
+__global__ void __launch_bounds__(BK_T) bucket_hist_kernel(const T *__restrict__ in, uint64_t n,
+                                                           const typename Comp<T>::C *__restrict__ spl_g,
                                                            int B, int BP,
                                                            uint32_t *__restrict__ counts) {
-    __shared__ int64_t spl[BK_MAXB];
+    using CT = Comp<T>;
+    constexpr int KPT = Geo<T>::KPT, SUB = BK_T * KPT;
+    __shared__ typename CT::C spl[BK_MAXB];
     __shared__ uint32_t rng[BK_SLOTS];
     __shared__ uint32_t hist[BK_MAXB];
-    load_splitters(spl_g, BP, spl);
+    load_splitters<T>(spl_g, BP, spl);
     for (int b = threadIdx.x; b < B; b += BK_T) hist[b] = 0;
     __syncthreads();
-    build_slots(spl, BP, rng);
+    build_slots<T>(spl, BP, rng);
     __syncthreads();
     const uint64_t g0 = (uint64_t)blockIdx.x * BK_WG;
 #pragma unroll 1
-    for (int sub = 0; sub < BK_SUBS; ++sub) {
-        const uint64_t b0 = g0 + (uint64_t)sub * BK_SUB + threadIdx.x;
-        int32_t key[BK_K];
+    for (int sub = 0; sub < BK_WG / SUB; ++sub) {
+        const uint64_t b0 = g0 + (uint64_t)sub * SUB + threadIdx.x;
+        T key[KPT];
 #pragma unroll
-        for (int k = 0; k < BK_K; ++k) {
+        for (int k = 0; k < KPT; ++k) {
             const uint64_t i = b0 + (uint64_t)k * BK_T;
-            key[k] = i < n ? in[i] : 0;
+            key[k] = i < n ? in[i] : T(0);
         }
 #pragma unroll
-        for (int k = 0; k < BK_K; ++k) {
+        for (int k = 0; k < KPT; ++k) {
             const uint64_t i = b0 + (uint64_t)k * BK_T;
-            if (i < n) atomicAdd(&hist[bucket_fast(spl, rng, key[k], composite(key[k], i))], 1u);
+            if (i < n) atomicAdd(&hist[bucket_fast<T>(spl, rng, key[k], CT::make(key[k], i))], 1u);
         }
     }
     __syncthreads();
@@ -138,7 +192,7 @@ __global__ void __launch_bounds__(BK_T) bucket_hist_kernel(const int32_t *__rest
 }
 
 // part[c * B + b] = sum of counts[g * B + b] over the BK_CHUNK workgroups g of chunk c
-__global__ void __launch_bounds__(BK_MAXB) bucket_colsum_kernel(const uint32_t *__restrict__ counts,
+static __global__ void __launch_bounds__(BK_MAXB) bucket_colsum_kernel(const uint32_t *__restrict__ counts,
                                                                uint32_t G, int B,
                                                                uint64_t *__restrict__ part) {
     const int b = threadIdx.x;
@@ -150,16 +204,17 @@ __global__ void __launch_bounds__(BK_MAXB) bucket_colsum_kernel(const uint32_t *
     part[(uint64_t)blockIdx.x * B + b] = sum;
 }
 
-// Tiles of a bucket [sk, sk + len): a head tile up to the next 4-key boundary (0..3 keys), then
-// TILE-key tiles from there, so every other tile starts 16-byte aligned (the tile sort's
-// 16-byte loads).  The host plans the merge passes with the same rule (bucket_tiles).
-__host__ __device__ __forceinline__ uint64_t bucket_head(uint64_t sk, uint64_t len) {
-    const uint64_t h = (4 - (sk & 3)) & 3;
+// Tiles of a bucket [sk, sk + len) for a tile sort of TILE-key tiles with 16-byte loads of
+// ALIGN keys: a head tile up to the next ALIGN-key boundary (0..ALIGN-1 keys), then TILE-key
+// tiles from there.  The host plans the merge passes with the same rule.
+__host__ __device__ __forceinline__ uint64_t bucket_head(uint64_t sk, uint64_t len, uint64_t align) {
+    const uint64_t h = (align - (sk & (align - 1))) & (align - 1);
     return h < len ? h : len;
 }
-__host__ __device__ __forceinline__ uint64_t bucket_tiles(uint64_t sk, uint64_t len) {
-    const uint64_t h = bucket_head(sk, len);
-    return (h ? 1 : 0) + (len - h + TILE - 1) / TILE;
+__host__ __device__ __forceinline__ uint64_t bucket_tiles(uint64_t sk, uint64_t len, uint64_t tile,
+                                                          uint64_t align) {
+    const uint64_t h = bucket_head(sk, len, align);
+    return (h ? 1 : 0) + (len - h + tile - 1) / tile;
 }
 
 // exclusive scan of one value per thread over a BK_MAXB-thread workgroup; `all` = total
@@ -184,10 +239,10 @@ __device__ __forceinline__ uint64_t scan_excl_u64(uint64_t v, uint64_t *wsum, ui
 
 // One workgroup: part -> exclusive prefix over chunks (in place); bucket starts bstart[0..B];
 // the tile table of the tile sort (every bucket cut into tiles, bucket_tiles) and its size.
-__global__ void __launch_bounds__(BK_MAXB) bucket_scan_kernel(uint64_t *__restrict__ part,
-                                                             uint32_t nchunk, int B,
+static __global__ void __launch_bounds__(BK_MAXB) bucket_scan_kernel(uint64_t *__restrict__ part,
+                                                             uint32_t nchunk, int B, uint32_t tile,
+                                                             uint32_t align,
                                                              uint64_t *__restrict__ bstart,
-                                                             uint32_t *__restrict__ tpre,
                                                              TileRef *__restrict__ tt,
                                                              uint32_t *__restrict__ ntiles) {
     __shared__ uint64_t wsum[BK_MAXB / 64];
@@ -202,28 +257,26 @@ __global__ void __launch_bounds__(BK_MAXB) bucket_scan_kernel(uint64_t *__restri
     }
     uint64_t allk, allt;
     const uint64_t sk = scan_excl_u64(tot, wsum, allk);
-    const uint64_t nt = b < B ? bucket_tiles(sk, tot) : 0;
+    const uint64_t nt = b < B ? bucket_tiles(sk, tot, tile, align) : 0;
     const uint64_t st = scan_excl_u64(nt, wsum, allt);
     if (b < B) {
         bstart[b] = sk;
-        tpre[b] = (uint32_t)st;
-        const uint64_t h = bucket_head(sk, tot);
+        const uint64_t h = bucket_head(sk, tot, align);
         uint64_t k = st;
         if (h) tt[k++] = TileRef{sk, (uint32_t)h, 0};
-        for (uint64_t base = sk + h; base < sk + tot; base += TILE) {
+        for (uint64_t base = sk + h; base < sk + tot; base += tile) {
             const uint64_t rem = sk + tot - base;
-            tt[k++] = TileRef{base, (uint32_t)(rem < (uint64_t)TILE ? rem : TILE), 0};
+            tt[k++] = TileRef{base, (uint32_t)(rem < (uint64_t)tile ? rem : tile), 0};
         }
     }
     if (b == 0) {
         bstart[B] = allk;
-        tpre[B] = (uint32_t)allt;
         *ntiles = (uint32_t)allt;
     }
 }
 
 // offs[g * B + b] = global position of workgroup g's first key of bucket b
-__global__ void __launch_bounds__(BK_MAXB) bucket_offsets_kernel(const uint32_t *__restrict__ counts,
+static __global__ void __launch_bounds__(BK_MAXB) bucket_offsets_kernel(const uint32_t *__restrict__ counts,
                                                                 const uint64_t *__restrict__ part,
                                                                 const uint64_t *__restrict__ bstart,
                                                                 uint32_t G, int B,
@@ -239,60 +292,62 @@ __global__ void __launch_bounds__(BK_MAXB) bucket_offsets_kernel(const uint32_t 
     }
 }
 
-// Per 16384-key sub-tile: every key takes a slot of its bucket in LDS (atomic on the sub-tile
-// histogram), the sub-tile is laid out bucket by bucket, and consecutive threads write
+// Per sub-tile (BK_T * KPT keys): every key takes a slot of its bucket in LDS (atomic on the
+// sub-tile histogram), the sub-tile is laid out bucket by bucket, and consecutive threads write
 // consecutive keys of a bucket to its global range.  The order of keys inside a bucket is not
-// kept (the bucket is sorted afterwards; the keys carry no payload).
-__global__ void __launch_bounds__(BK_T) bucket_scatter_kernel(const int32_t *__restrict__ in,
-                                                              uint64_t n,
-                                                              const int64_t *__restrict__ spl_g,
+// kept (the bucket is sorted afterwards; the keys carry no payload).  The next sub-tile's keys
+// are loaded while the current one is placed.
+template <typename T>
+__global__ void __launch_bounds__(BK_T) bucket_scatter_kernel(const T *__restrict__ in, uint64_t n,
+                                                              const typename Comp<T>::C *__restrict__ spl_g,
                                                               int B, int BP,
                                                               const uint64_t *__restrict__ offs,
-                                                              int32_t *__restrict__ out) {
-    __shared__ int64_t spl[BK_MAXB];
+                                                              T *__restrict__ out) {
+    using CT = Comp<T>;
+    constexpr int KPT = Geo<T>::KPT, SUB = BK_T * KPT, SUBS = BK_WG / SUB;
+    __shared__ typename CT::C spl[BK_MAXB];
     __shared__ uint32_t rng[BK_SLOTS];
     __shared__ uint64_t goff[BK_MAXB];   // next global position of each bucket (this workgroup)
     __shared__ uint32_t hist[BK_MAXB];   // sub-tile histogram, then its exclusive scan
     __shared__ uint32_t wsum[BK_T / 64];
-    __shared__ int32_t lk[BK_SUB];       // the sub-tile grouped by bucket
-    __shared__ uint16_t lb[BK_SUB];      // bucket of every LDS slot
-    load_splitters(spl_g, BP, spl);
+    __shared__ T lk[SUB];                // the sub-tile grouped by bucket
+    __shared__ uint16_t lb[SUB];         // bucket of every LDS slot
+    load_splitters<T>(spl_g, BP, spl);
     for (int b = threadIdx.x; b < B; b += BK_T) goff[b] = offs[(uint64_t)blockIdx.x * B + b];
     __syncthreads();
-    build_slots(spl, BP, rng);
+    build_slots<T>(spl, BP, rng);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t g0 = (uint64_t)blockIdx.x * BK_WG;
-    // keys of the next sub-tile are loaded while the current one is placed (software pipeline)
-    int32_t nxt[BK_K];
+    T nxt[KPT];
 #pragma unroll
-    for (int k = 0; k < BK_K; ++k) {
+    for (int k = 0; k < KPT; ++k) {
         const uint64_t i = g0 + threadIdx.x + (uint64_t)k * BK_T;
-        nxt[k] = i < n ? in[i] : 0;
+        nxt[k] = i < n ? in[i] : T(0);
     }
 #pragma unroll 1
-    for (int sub = 0; sub < BK_SUBS; ++sub) {
-        const uint64_t s0 = g0 + (uint64_t)sub * BK_SUB;
+    for (int sub = 0; sub < SUBS; ++sub) {
+        const uint64_t s0 = g0 + (uint64_t)sub * SUB;
         if (s0 >= n) break;  // workgroup-uniform
         for (int b = threadIdx.x; b < B; b += BK_T) hist[b] = 0;
         __syncthreads();
-        int32_t key[BK_K];
-        int bk[BK_K];
-        uint32_t slot[BK_K];
+        T key[KPT];
+        int bk[KPT];
+        uint32_t slot[KPT];
 #pragma unroll
-        for (int k = 0; k < BK_K; ++k) key[k] = nxt[k];
-        if (sub + 1 < BK_SUBS) {
+        for (int k = 0; k < KPT; ++k) key[k] = nxt[k];
+        if (sub + 1 < SUBS) {
 #pragma unroll
-            for (int k = 0; k < BK_K; ++k) {
-                const uint64_t i = s0 + BK_SUB + threadIdx.x + (uint64_t)k * BK_T;
-                nxt[k] = i < n ? in[i] : 0;
+            for (int k = 0; k < KPT; ++k) {
+                const uint64_t i = s0 + SUB + threadIdx.x + (uint64_t)k * BK_T;
+                nxt[k] = i < n ? in[i] : T(0);
             }
         }
 #pragma unroll
-        for (int k = 0; k < BK_K; ++k) {
+        for (int k = 0; k < KPT; ++k) {
             const uint64_t i = s0 + threadIdx.x + (uint64_t)k * BK_T;
             bk[k] = -1;
             if (i < n) {
-                bk[k] = bucket_fast(spl, rng, key[k], composite(key[k], i));
+                bk[k] = bucket_fast<T>(spl, rng, key[k], CT::make(key[k], i));
                 slot[k] = atomicAdd(&hist[bk[k]], 1u);
             }
         }
@@ -311,7 +366,7 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_kernel(const int32_t *__r
         if (threadIdx.x < (unsigned)B) hist[threadIdx.x] = woff + incl - hv;
         __syncthreads();
 #pragma unroll
-        for (int k = 0; k < BK_K; ++k) {
+        for (int k = 0; k < KPT; ++k) {
             if (bk[k] >= 0) {
                 const uint32_t p = hist[bk[k]] + slot[k];
                 lk[p] = key[k];
@@ -319,9 +374,9 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_kernel(const int32_t *__r
             }
         }
         __syncthreads();
-        const uint32_t cnt = s0 + BK_SUB <= n ? BK_SUB : (uint32_t)(n - s0);
+        const uint32_t cnt = s0 + SUB <= n ? SUB : (uint32_t)(n - s0);
 #pragma unroll
-        for (int k = 0; k < BK_K; ++k) {
+        for (int k = 0; k < KPT; ++k) {
             const uint32_t p = threadIdx.x + k * BK_T;
             if (p < cnt) {
                 const int b = lb[p];
@@ -331,9 +386,12 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_kernel(const int32_t *__r
         __syncthreads();
         // advance every bucket's global position by this sub-tile's keys
         if (threadIdx.x < (unsigned)B) {
-            const uint32_t nxt = threadIdx.x + 1 < (unsigned)B ? hist[threadIdx.x + 1] : cnt;
-            goff[threadIdx.x] += nxt - hist[threadIdx.x];
+            const uint32_t nx = threadIdx.x + 1 < (unsigned)B ? hist[threadIdx.x + 1] : cnt;
+            goff[threadIdx.x] += nx - hist[threadIdx.x];
         }
         __syncthreads();
     }
 }
+
+}  // namespace bk
+}  // namespace dsort

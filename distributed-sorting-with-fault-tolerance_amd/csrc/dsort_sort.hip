@@ -29,11 +29,13 @@
 #include <algorithm>
 #include <climits>
 #include <cstdlib>
+#include <cstring>
 #include <csignal>
 #include <string>
 #include <type_traits>
 #include <vector>
 
+#include "dsort_bucket.h"
 #include "dsort_internal.h"
 #include "dsort_part.h"
 
@@ -209,8 +211,12 @@ __device__ __forceinline__ void store_tile(const T *s, T *out, int valid) {
 // ---------------------------------------------------------------------------------------
 // 1. Tile sort.
 // ---------------------------------------------------------------------------------------
+// tiles: NULL = tile j is keys [j * TILE, (j + 1) * TILE) of n; else tile j = tiles[j] (the
+// bucketed sort's tiles, which never cross a bucket; bk::TileRef), j < *ntiles.
 template <typename T, int THREADS, int K>
-__global__ void __launch_bounds__(THREADS) block_sort_kernel(const T *in, T *out, uint64_t n) {
+__global__ void __launch_bounds__(THREADS) block_sort_kernel(const T *in, T *out, uint64_t n,
+                                                             const uint4 *tiles,
+                                                             const uint32_t *ntiles) {
     // `in` may alias `out` (in-place sort): every workgroup reads its whole tile first.
     constexpr int TILE = THREADS * K;
     using V = typename Vec16<T>::type;
@@ -218,12 +224,21 @@ __global__ void __launch_bounds__(THREADS) block_sort_kernel(const T *in, T *out
     __shared__ __attribute__((aligned(16))) T s[lds_keys<T>(TILE)];
 
     const int t = threadIdx.x;
-    const uint64_t base = (uint64_t)blockIdx.x * TILE;
-    const uint64_t rem = n - base;
-    const int valid = rem < (uint64_t)TILE ? (int)rem : TILE;
+    uint64_t base;
+    int valid;
+    if (tiles) {
+        if (blockIdx.x >= *ntiles) return;  // the grid is an upper bound
+        const uint4 r = tiles[blockIdx.x];
+        base = (uint64_t)r.x | ((uint64_t)r.y << 32);
+        valid = (int)r.z;
+    } else {
+        base = (uint64_t)blockIdx.x * TILE;
+        const uint64_t rem = n - base;
+        valid = rem < (uint64_t)TILE ? (int)rem : TILE;
+    }
 
     T v[K];
-    if (valid == TILE) {
+    if (valid == TILE && (reinterpret_cast<uintptr_t>(in + base) & 15) == 0) {
         const V *src = reinterpret_cast<const V *>(in + base);
 #pragma unroll
         for (int i = 0; i < K / VN; ++i) {
@@ -455,10 +470,209 @@ bool use_legacy_kernels() {
     return v == 1;
 }
 
+// ---- bucketed int64 sort (dsort_bucket.h) --------------------------------------------------
+// As the int32 one (dsort_wave.hip): B ~ n / 2^21 buckets by (key, index) splitters, one
+// partition pass, then the tile sort (4096-key tiles) and the k-way passes inside every bucket
+// (groups of <= 2^max_logf runs): 2 merge passes at 2^30 keys instead of 4.  The 32*B samples
+// are sorted on the host (16-byte (key, index) pairs).  DSORT_BUCKETS as for int32.
+static int bucket_count_i64(uint64_t n) {
+    const char *e = getenv("DSORT_BUCKETS");
+    const int forced = e ? atoi(e) : -1;
+    if (forced == 0) return 0;
+    uint64_t B = forced > 0 ? (uint64_t)forced : (n >> 21);
+    if (forced < 0 && n < (1ull << 25)) return 0;
+    if (n >= (1ull << 32)) return 0;
+    if (B > (uint64_t)bk::BK_MAXB) B = bk::BK_MAXB;
+    return B >= 2 ? (int)B : 0;
+}
+
+static int bucket_sort_i64(dsort_ctx *ctx, const int64_t *d_in, int64_t *d_keys, size_t n,
+                           hipStream_t s, bool timed, int B) {
+    using namespace bk;
+    using T = int64_t;
+    using C = Comp<T>::C;
+    constexpr int THREADS = Geom<T>::THREADS, K = Geom<T>::K, TILE = Geom<T>::TILE;
+    constexpr uint64_t ALIGN = 16 / sizeof(T);
+    const int BP = 1 << ceil_log2((uint64_t)B);
+    const uint64_t G = ceil_div(n, BK_WG);
+    const uint64_t nchunk = ceil_div(G, BK_CHUNK);
+    const uint32_t S = (uint32_t)B * BK_OS;
+    const uint64_t tmax = ceil_div(n, TILE) + 2 * (uint64_t)B;
+    ctx->stats = dsort_stats{};
+    ctx->stats.keys_in = ctx->stats.keys_out = n;
+    ctx->stats.tile_keys = TILE;
+    ctx->ev_mask = 0;
+    ctx->kev_used = 0;
+    ctx->last_stream = s;
+    size_t off = 0;
+    auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
+    const size_t o_smp = take((size_t)S * sizeof(C)), o_spl = take((size_t)BP * sizeof(C)),
+                 o_cnt = take((size_t)G * B * 4), o_part = take((size_t)nchunk * B * 8),
+                 o_offs = take((size_t)G * B * 8), o_bst = take((size_t)(B + 1) * 8),
+                 o_tt = take((size_t)tmax * sizeof(TileRef)), o_nt = take(4);
+    int rc = ensure(ctx, &ctx->bucket, &ctx->bucket_bytes, off, "bucket partition");
+    if (rc) return rc;
+    char *a = static_cast<char *>(ctx->bucket);
+    C *smp = reinterpret_cast<C *>(a + o_smp);
+    C *spl = reinterpret_cast<C *>(a + o_spl);
+    uint32_t *cnt = reinterpret_cast<uint32_t *>(a + o_cnt);
+    uint64_t *part = reinterpret_cast<uint64_t *>(a + o_part);
+    uint64_t *offs = reinterpret_cast<uint64_t *>(a + o_offs);
+    uint64_t *bst = reinterpret_cast<uint64_t *>(a + o_bst);
+    TileRef *tt = reinterpret_cast<TileRef *>(a + o_tt);
+    uint32_t *ntl = reinterpret_cast<uint32_t *>(a + o_nt);
+    rc = ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, n * sizeof(T), "sort scratch");
+    if (rc) return rc;
+    T *scratch = static_cast<T *>(ctx->scratch);
+    const size_t hbytes = (size_t)BK_MAXB * BK_OS * sizeof(C) + (size_t)(BK_MAXB + 1) * 8;
+    if (ctx->bucket_host_bytes < hbytes) {
+        if (ctx->bucket_host) (void)hipHostFree(ctx->bucket_host);
+        ctx->bucket_host = nullptr;
+        ctx->bucket_host_bytes = 0;
+        DSORT_HIP(ctx, hipHostMalloc(&ctx->bucket_host, hbytes, hipHostMallocDefault));
+        ctx->bucket_host_bytes = hbytes;
+    }
+    if (!ctx->bucket_ev && hipEventCreateWithFlags(&ctx->bucket_ev, hipEventDisableTiming) != hipSuccess)
+        return set_err(ctx, DSORT_EHIP, "hipEventCreate");
+    if (timed && ctx->ev_ok) {
+        DSORT_HIP(ctx, hipEventRecord(ctx->ev[0], s));
+        ctx->ev_mask |= 1u;
+    }
+    // 1. splitters: samples to the host, sorted in (key, index) order, every BK_OS-th back
+    C *hs = static_cast<C *>(ctx->bucket_host);
+    hipLaunchKernelGGL(bucket_sample_kernel<T>, dim3(ceil_div(S, 256)), dim3(256), 0, s, d_in, (uint64_t)n, smp, S);
+    DSORT_HIP(ctx, hipGetLastError());
+    DSORT_HIP(ctx, hipMemcpyAsync(hs, smp, (size_t)S * sizeof(C), hipMemcpyDeviceToHost, s));
+    DSORT_HIP(ctx, hipStreamSynchronize(s));
+    std::sort(hs, hs + S, [](const C &x, const C &y) { return Comp<T>::lt(x, y); });
+    for (int b = 0; b < BP; ++b) hs[b] = b < B - 1 ? hs[(size_t)(b + 1) * BK_OS - 1] : Comp<T>::inf();
+    DSORT_HIP(ctx, hipMemcpyAsync(spl, hs, (size_t)BP * sizeof(C), hipMemcpyHostToDevice, s));
+    // 2. histograms, their scan, bucket starts to the host
+    hipLaunchKernelGGL(bucket_hist_kernel<T>, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, B, BP, cnt);
+    hipLaunchKernelGGL(bucket_colsum_kernel, dim3((unsigned)nchunk), dim3(BK_MAXB), 0, s, cnt, (uint32_t)G, B, part);
+    hipLaunchKernelGGL(bucket_scan_kernel, dim3(1), dim3(BK_MAXB), 0, s, part, (uint32_t)nchunk, B,
+                       (uint32_t)TILE, (uint32_t)ALIGN, bst, tt, ntl);
+    hipLaunchKernelGGL(bucket_offsets_kernel, dim3((unsigned)nchunk), dim3(BK_MAXB), 0, s, cnt, part, bst, (uint32_t)G, B, offs);
+    DSORT_HIP(ctx, hipGetLastError());
+    uint64_t *hb = reinterpret_cast<uint64_t *>(hs + BK_MAXB * BK_OS);
+    DSORT_HIP(ctx, hipMemcpyAsync(hb, bst, (size_t)(B + 1) * 8, hipMemcpyDeviceToHost, s));
+    DSORT_HIP(ctx, hipEventRecord(ctx->bucket_ev, s));
+    DSORT_HIP(ctx, hipEventSynchronize(ctx->bucket_ev));
+    if (hb[B] != n) return set_err(ctx, DSORT_EHIP, "bucket partition lost keys");
+    // pass plan: the tile sort's runs of every bucket, merged 2^max_logf at a time
+    const int MAXF = 1 << max_logf();
+    std::vector<std::vector<uint64_t>> runs(B);
+    int passes = 0;
+    for (int b = 0; b < B; ++b) {
+        const uint64_t len = hb[b + 1] - hb[b], h = bucket_head(hb[b], len, ALIGN);
+        if (h) runs[b].push_back(h);
+        for (uint64_t o = h; o < len; o += TILE) runs[b].push_back(len - o < (uint64_t)TILE ? len - o : TILE);
+        int p = 0;
+        for (uint64_t r = runs[b].size(); r > 1; r = ceil_div(r, MAXF)) ++p;
+        passes = p > passes ? p : passes;
+    }
+    ctx->stats.merge_passes = passes;
+    T *bufs[2] = {d_keys, scratch};
+    int cur = (passes % 2 == 0) ? 0 : 1;
+    T *part_out = (bufs[cur] == d_in) ? bufs[cur ^ 1] : bufs[cur];
+    hipLaunchKernelGGL(bucket_scatter_kernel<T>, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, B, BP, offs, part_out);
+    DSORT_HIP(ctx, hipGetLastError());
+    // 3. tile sort inside the buckets
+    hipLaunchKernelGGL((block_sort_kernel<T, THREADS, K>), dim3((unsigned)tmax), dim3(THREADS), 0, s,
+                       part_out, bufs[cur], (uint64_t)n, reinterpret_cast<const uint4 *>(tt), ntl);
+    DSORT_HIP(ctx, hipGetLastError());
+    if (timed && ctx->ev_ok) {
+        DSORT_HIP(ctx, hipEventRecord(ctx->ev[1], s));
+        ctx->ev_mask |= 2u;
+    }
+    // 4. group tables of every pass (one staging buffer, one copy), then the passes
+    struct PassPlan { int logf; uint64_t ngroups, ntiles; size_t group_off, tile_off; };
+    std::vector<PassPlan> plan;
+    std::vector<GroupK> groups;
+    std::vector<uint32_t> tgroup;
+    for (int p = 0; p < passes; ++p) {
+        int maxr = 1;
+        for (int b = 0; b < B; ++b)
+            for (size_t r0 = 0; r0 < runs[b].size(); r0 += MAXF) {
+                const int nr = (int)std::min<size_t>(MAXF, runs[b].size() - r0);
+                maxr = nr > maxr ? nr : maxr;
+            }
+        PassPlan pp{ceil_log2((uint64_t)maxr) < 1 ? 1 : ceil_log2((uint64_t)maxr), 0, 0, groups.size(), tgroup.size()};
+        const uint64_t tn = (uint64_t)tnom_of<T>(pp.logf);
+        uint64_t base = 0, tiles = 0;
+        for (int b = 0; b < B; ++b) {
+            std::vector<uint64_t> next;
+            const size_t nr = runs[b].size();
+            for (size_t r0 = 0; r0 < nr; r0 += MAXF) {
+                GroupK gk{};
+                gk.base = base;
+                gk.first_tile = tiles;
+                uint64_t tot = 0;
+                for (size_t r = r0; r < nr && r < r0 + MAXF; ++r) {
+                    tot += runs[b][r];
+                    gk.roff[++gk.nruns] = tot;
+                }
+                for (int r = (int)gk.nruns + 1; r <= kMaxF; ++r) gk.roff[r] = tot;
+                gk.total = tot;
+                const uint64_t gt = ceil_div(tot, tn);
+                for (uint64_t k = 0; k < gt; ++k) tgroup.push_back((uint32_t)(groups.size() - pp.group_off));
+                tiles += gt;
+                base += tot;
+                next.push_back(tot);
+                groups.push_back(gk);
+            }
+            runs[b].swap(next);
+        }
+        pp.ngroups = groups.size() - pp.group_off;
+        pp.ntiles = tiles;
+        plan.push_back(pp);
+    }
+    if (passes > 0) {
+        const size_t gbytes = groups.size() * sizeof(GroupK), tbytes = tgroup.size() * sizeof(uint32_t);
+        const size_t tb_off = (gbytes + 255) & ~(size_t)255;
+        if (ctx->groups_ev_pending) DSORT_HIP(ctx, hipEventSynchronize(ctx->groups_ev));
+        ctx->groups_ev_pending = false;
+        if (ctx->groups_host_bytes < tb_off + tbytes) {
+            if (ctx->groups_host) (void)hipHostFree(ctx->groups_host);
+            ctx->groups_host = nullptr;
+            ctx->groups_host_bytes = 0;
+            DSORT_HIP(ctx, hipHostMalloc(&ctx->groups_host, tb_off + tbytes, hipHostMallocDefault));
+            ctx->groups_host_bytes = tb_off + tbytes;
+        }
+        rc = ensure(ctx, &ctx->groups, &ctx->groups_bytes, tb_off + tbytes, "group table");
+        if (rc) return rc;
+        std::memcpy(ctx->groups_host, groups.data(), gbytes);
+        std::memcpy(static_cast<char *>(ctx->groups_host) + tb_off, tgroup.data(), tbytes);
+        DSORT_HIP(ctx, hipMemcpyAsync(ctx->groups, ctx->groups_host, tb_off + tbytes, hipMemcpyHostToDevice, s));
+        if (!ctx->groups_ev && hipEventCreateWithFlags(&ctx->groups_ev, hipEventDisableTiming) != hipSuccess)
+            return set_err(ctx, DSORT_EHIP, "hipEventCreate");
+        DSORT_HIP(ctx, hipEventRecord(ctx->groups_ev, s));
+        ctx->groups_ev_pending = true;
+        const GroupK *dg = static_cast<const GroupK *>(ctx->groups);
+        const uint32_t *dt = reinterpret_cast<const uint32_t *>(static_cast<const char *>(ctx->groups) + tb_off);
+        for (int p = 0; p < passes; ++p) {
+            PassDesc pd{(uint64_t)n, 0, 1 << plan[p].logf, (int)plan[p].ngroups, dg + plan[p].group_off};
+            pd.tile_group = dt + plan[p].tile_off;
+            rc = launch_pass<T, THREADS, K, false>(ctx, bufs[cur], bufs[cur ^ 1], pd, plan[p].logf,
+                                                   plan[p].ntiles, s, timed);
+            if (rc) return rc;
+            cur ^= 1;
+            fault_point(s, p);
+        }
+    }
+    if (timed && ctx->ev_ok) {
+        DSORT_HIP(ctx, hipEventRecord(ctx->ev[2], s));
+        ctx->ev_mask |= 4u;
+    }
+    return DSORT_OK;
+}
+
 template <typename T>
 int sort_device(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipStream_t s, bool timed) {
     if constexpr (std::is_same<T, int32_t>::value) {
         if (!use_legacy_kernels()) return wave_sort_i32(ctx, d_in, d_keys, n, s, timed);
+    } else {
+        if (const int B = bucket_count_i64(n)) return bucket_sort_i64(ctx, d_in, d_keys, n, s, timed, B);
     }
     constexpr int THREADS = Geom<T>::THREADS, K = Geom<T>::K, TILE = Geom<T>::TILE;
     ctx->stats = dsort_stats{};
@@ -492,7 +706,7 @@ int sort_device(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipStream_t 
         ctx->ev_mask |= 1u;
     }
     hipLaunchKernelGGL((block_sort_kernel<T, THREADS, K>), dim3((unsigned)tiles), dim3(THREADS), 0,
-                       s, d_in, bufs[cur], (uint64_t)n);
+                       s, d_in, bufs[cur], (uint64_t)n, nullptr, nullptr);
     DSORT_HIP(ctx, hipGetLastError());
     if (timed && ctx->ev_ok) {
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[1], s));

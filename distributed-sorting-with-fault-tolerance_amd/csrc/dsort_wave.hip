@@ -35,6 +35,7 @@
 #include <cstring>
 #include <vector>
 
+#include "dsort_bucket.h"
 #include "dsort_internal.h"
 #include "dsort_part.h"
 
@@ -672,8 +673,6 @@ __global__ void __launch_bounds__(THREADS, 8) mergew_kernel(const int *__restric
     }
 }
 
-#include "dsort_bucket.h"
-
 // ------------------------------------------------------------------------------------------
 // Host side
 // ------------------------------------------------------------------------------------------
@@ -740,7 +739,8 @@ static int bucket_count(uint64_t n) {
     if (forced == 0) return 0;
     uint64_t B = forced > 0 ? (uint64_t)forced : (n >> 21);
     if (forced < 0 && n < (1ull << 25)) return 0;
-    if (B > (uint64_t)BK_MAXB) B = BK_MAXB;
+    if (n >= (1ull << 32)) return 0;  // 32-bit bucket positions in the scatter
+    if (B > (uint64_t)bk::BK_MAXB) B = bk::BK_MAXB;
     return B >= 2 ? (int)B : 0;
 }
 
@@ -754,6 +754,7 @@ struct BucketPass {
 
 static int bucket_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys, size_t n,
                            hipStream_t s, bool timed, int B) {
+    using namespace bk;
     const int BP = 1 << ceil_log2((uint64_t)B);
     const uint64_t G = ceil_div(n, BK_WG);
     const uint64_t nchunk = ceil_div(G, BK_CHUNK);
@@ -765,8 +766,7 @@ static int bucket_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys,
     const size_t o_smp = take((size_t)S * 8), o_spl = take((size_t)BP * 8),
                  o_cnt = take((size_t)G * B * 4), o_part = take((size_t)nchunk * B * 8),
                  o_offs = take((size_t)G * B * 8), o_bst = take((size_t)(B + 1) * 8),
-                 o_tpre = take((size_t)(B + 1) * 4), o_tt = take((size_t)tmax * sizeof(TileRef)),
-                 o_nt = take(4);
+                 o_tt = take((size_t)tmax * sizeof(TileRef)), o_nt = take(4);
     int rc = ensure(ctx, &ctx->bucket, &ctx->bucket_bytes, off, "bucket partition");
     if (rc) return rc;
     char *a = static_cast<char *>(ctx->bucket);
@@ -776,7 +776,6 @@ static int bucket_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys,
     uint64_t *part = reinterpret_cast<uint64_t *>(a + o_part);
     uint64_t *offs = reinterpret_cast<uint64_t *>(a + o_offs);
     uint64_t *bst = reinterpret_cast<uint64_t *>(a + o_bst);
-    uint32_t *tpre = reinterpret_cast<uint32_t *>(a + o_tpre);
     TileRef *tt = reinterpret_cast<TileRef *>(a + o_tt);
     uint32_t *ntl = reinterpret_cast<uint32_t *>(a + o_nt);
     rc = ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, n * sizeof(int32_t), "sort scratch");
@@ -793,7 +792,7 @@ static int bucket_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys,
         return set_err(ctx, DSORT_EHIP, "hipEventCreate");
 
     // 1. splitters from a regular sample, sorted in (key, index) order by the int64 sort
-    hipLaunchKernelGGL(bucket_sample_kernel, dim3(ceil_div(S, 256)), dim3(256), 0, s, d_in, (uint64_t)n, smp, S);
+    hipLaunchKernelGGL(bucket_sample_kernel<int32_t>, dim3(ceil_div(S, 256)), dim3(256), 0, s, d_in, (uint64_t)n, smp, S);
     DSORT_HIP(ctx, hipGetLastError());
     rc = sort_device<int64_t>(ctx, smp, smp, S, s, false);
     if (rc) return rc;
@@ -808,11 +807,12 @@ static int bucket_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys,
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[0], s));
         ctx->ev_mask |= 1u;
     }
-    hipLaunchKernelGGL(bucket_splitter_kernel, dim3(1), dim3(BK_MAXB), 0, s, smp, B, BP, spl);
+    hipLaunchKernelGGL(bucket_splitter_kernel<int32_t>, dim3(1), dim3(BK_MAXB), 0, s, smp, B, BP, spl);
     // 2. histograms, their scan, the scatter
-    hipLaunchKernelGGL(bucket_hist_kernel, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, B, BP, cnt);
+    hipLaunchKernelGGL(bucket_hist_kernel<int32_t>, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, B, BP, cnt);
     hipLaunchKernelGGL(bucket_colsum_kernel, dim3((unsigned)nchunk), dim3(BK_MAXB), 0, s, cnt, (uint32_t)G, B, part);
-    hipLaunchKernelGGL(bucket_scan_kernel, dim3(1), dim3(BK_MAXB), 0, s, part, (uint32_t)nchunk, B, bst, tpre, tt, ntl);
+    hipLaunchKernelGGL(bucket_scan_kernel, dim3(1), dim3(BK_MAXB), 0, s, part, (uint32_t)nchunk, B,
+                       (uint32_t)TILE, 4u, bst, tt, ntl);
     hipLaunchKernelGGL(bucket_offsets_kernel, dim3((unsigned)nchunk), dim3(BK_MAXB), 0, s, cnt, part, bst, (uint32_t)G, B, offs);
     DSORT_HIP(ctx, hipGetLastError());
     // bucket starts to the host (the pass plan depends on the bucket sizes)
@@ -831,7 +831,7 @@ static int bucket_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys,
     int passes = 0;
     for (int b = 0; b < B; ++b) {
         // the tile sort's runs of bucket b (bucket_tiles: a 0..3-key head, then TILE-key tiles)
-        const uint64_t h = bucket_head(hb[b], bsz[b]);
+        const uint64_t h = bucket_head(hb[b], bsz[b], 4);
         if (h) runs[b].push_back(h);
         for (uint64_t o = h; o < bsz[b]; o += TILE) runs[b].push_back(bsz[b] - o < (uint64_t)TILE ? bsz[b] - o : TILE);
         int p = 0;
@@ -843,7 +843,7 @@ static int bucket_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys,
     int cur = (passes % 2 == 0) ? 0 : 1;  // tile sort output; the passes end in d_keys
     // scatter into the tile sort's buffer unless that is the input (in-place sort)
     int32_t *part_out = (bufs[cur] == d_in) ? bufs[cur ^ 1] : bufs[cur];
-    hipLaunchKernelGGL(bucket_scatter_kernel, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, B, BP, offs, part_out);
+    hipLaunchKernelGGL(bucket_scatter_kernel<int32_t>, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, B, BP, offs, part_out);
     DSORT_HIP(ctx, hipGetLastError());
     // 3. tile sort inside the buckets
     hipLaunchKernelGGL(block_sort_w_kernel, dim3((unsigned)tmax), dim3(THREADS), 0, s, part_out,

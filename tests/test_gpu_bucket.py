@@ -80,3 +80,47 @@ def test_bucketed_default_at_2p26_matches_regular_path(gpu_ctx, monkeypatch):
     torch.cuda.synchronize()
     assert gpu_ctx.descents(o1) == 0 and gpu_ctx.fingerprint(o1) == fp
     assert torch.equal(o1, o2)
+
+
+I64_MIN, I64_MAX = -(2**63), 2**63 - 1
+
+
+def _keys64(rng, kind, n):
+    if kind == "uniform":
+        return rng.integers(I64_MIN, I64_MAX, n, endpoint=True, dtype=np.int64)
+    if kind == "equal":
+        return np.full(n, -5, np.int64)
+    if kind == "few":
+        return rng.integers(0, 3, n).astype(np.int64) * (1 << 40) - (1 << 41)
+    if kind == "extremes":
+        return rng.choice(np.array([I64_MIN, I64_MIN + 1, -1, 0, 1, I64_MAX - 1, I64_MAX], np.int64), n)
+    if kind == "small":  # all keys inside one lookup slot (top 12 bits equal)
+        return rng.integers(0, 1 << 20, n).astype(np.int64)
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("kind", ["uniform", "equal", "few", "extremes", "small"])
+@pytest.mark.parametrize("B,n", [(2, 50_001), (5, 4096 * 3 + 1), (64, 1_000_003), (1024, 300_000)])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_bucketed_sort_i64_vs_numpy(gpu_ctx, monkeypatch, kind, B, n, inplace):
+    monkeypatch.setenv("DSORT_BUCKETS", str(B))
+    a = _keys64(np.random.default_rng(B * 7 + n), kind, n)
+    assert np.array_equal(_sort(gpu_ctx, a, inplace), np.sort(a))
+
+
+def test_bucketed_zipf_i64_2p26(gpu_ctx, monkeypatch):
+    """Default bucket count on the BASELINE config-4 distribution (heavy duplicates): sorted,
+    same multiset, identical to the regular passes."""
+    import torch
+    n = 1 << 26
+    t = torch.empty(n, dtype=torch.int64, device="cuda")
+    gpu_ctx.gen_zipf_i64(t, 0x5EED2026)
+    fp = gpu_ctx.fingerprint(t)
+    o1, o2 = torch.empty_like(t), torch.empty_like(t)
+    monkeypatch.delenv("DSORT_BUCKETS", raising=False)
+    gpu_ctx.sort_dev(t, o1)
+    monkeypatch.setenv("DSORT_BUCKETS", "0")
+    gpu_ctx.sort_dev(t, o2)
+    torch.cuda.synchronize()
+    assert gpu_ctx.descents(o1) == 0 and gpu_ctx.fingerprint(o1) == fp
+    assert torch.equal(o1, o2)
