@@ -30,14 +30,16 @@ namespace dsort {
 namespace bk {
 
 constexpr int BK_T = 1024;               // threads of the partition kernels
-constexpr int BK_WG = 65536;             // keys per partition workgroup
 constexpr int BK_MAXB = 1024;            // buckets at most (<= threads, one bucket per thread)
 constexpr int BK_OS = 32;                // samples per bucket
 constexpr int BK_CHUNK = 64;             // workgroups per column-sum chunk
 
 // Scatter sub-tile per key width: KPT keys per thread, SUB = BK_T * KPT keys staged in LDS.
 template <typename T> struct Geo;
-template <> struct Geo<int32_t> { static constexpr int KPT = 16; };
+#ifndef DSORT_BK_KPT32
+#define DSORT_BK_KPT32 16
+#endif
+template <> struct Geo<int32_t> { static constexpr int KPT = DSORT_BK_KPT32; };
 template <> struct Geo<int64_t> { static constexpr int KPT = 8; };
 
 struct TileRef {
@@ -98,7 +100,10 @@ __device__ __forceinline__ int bucket_of(const typename Comp<T>::C *spl, int BP,
 // the number of splitters whose key lies below the slot (low 16 bits) and below the next slot
 // (high 16 bits).  Only splitters inside the key's slot need a comparison -- usually none or
 // one -- instead of a log2(B)-step search with bank conflicts on every step.
-constexpr int BK_SLOTB = 12;
+#ifndef DSORT_BK_SLOTB
+#define DSORT_BK_SLOTB 11
+#endif
+constexpr int BK_SLOTB = DSORT_BK_SLOTB;
 constexpr int BK_SLOTS = 1 << BK_SLOTB;
 
 template <typename T>
@@ -140,13 +145,14 @@ __global__ void __launch_bounds__(256) bucket_sample_kernel(const T *__restrict_
     smp[k] = Comp<T>::make(in[pos], pos);
 }
 
-// splitter b = sample (b+1)*BK_OS - 1 of the sorted samples, b < B-1; +inf up to BP
+// splitter b = sample (b+1)*os - 1 of the sorted samples (os samples per bucket), b < B-1;
+// +inf up to BP
 template <typename T>
 __global__ void __launch_bounds__(BK_MAXB) bucket_splitter_kernel(const typename Comp<T>::C *__restrict__ smp,
-                                                                 int B, int BP,
+                                                                 int B, int BP, int os,
                                                                  typename Comp<T>::C *__restrict__ spl) {
     const int b = threadIdx.x;
-    if (b < BP) spl[b] = b < B - 1 ? smp[(uint64_t)(b + 1) * BK_OS - 1] : Comp<T>::inf();
+    if (b < BP) spl[b] = b < B - 1 ? smp[(uint64_t)(b + 1) * os - 1] : Comp<T>::inf();
 }
 
 template <typename T>
@@ -155,11 +161,20 @@ __device__ __forceinline__ void load_splitters(const typename Comp<T>::C *spl_g,
     for (int b = threadIdx.x; b < BP; b += BK_T) spl[b] = spl_g[b];
 }
 
-// counts[g * B + b] = keys of workgroup g's BK_WG keys in bucket b
+// Keys per partition workgroup: `subs` sub-tiles of BK_T * KPT keys, 4..16 so that a large
+// input gets >= ~2048 workgroups with long per-bucket runs and a small one still fills the chip.
+template <typename T>
+__host__ __forceinline__ int bucket_wg_subs(uint64_t n) {
+    const uint64_t sub = (uint64_t)BK_T * Geo<T>::KPT;
+    const uint64_t v = n / (2048 * sub);
+    return v < 4 ? 4 : (v > 16 ? 16 : (int)v);
+}
+
+// counts[g * B + b] = keys of workgroup g's subs sub-tiles in bucket b
 template <typename T>
 __global__ void __launch_bounds__(BK_T) bucket_hist_kernel(const T *__restrict__ in, uint64_t n,
                                                            const typename Comp<T>::C *__restrict__ spl_g,
-                                                           int B, int BP,
+                                                           int B, int BP, int subs,
                                                            uint32_t *__restrict__ counts) {
     using CT = Comp<T>;
     constexpr int KPT = Geo<T>::KPT, SUB = BK_T * KPT;
@@ -171,9 +186,9 @@ __global__ void __launch_bounds__(BK_T) bucket_hist_kernel(const T *__restrict__
     __syncthreads();
     build_slots<T>(spl, BP, rng);
     __syncthreads();
-    const uint64_t g0 = (uint64_t)blockIdx.x * BK_WG;
+    const uint64_t g0 = (uint64_t)blockIdx.x * subs * SUB;
 #pragma unroll 1
-    for (int sub = 0; sub < BK_WG / SUB; ++sub) {
+    for (int sub = 0; sub < subs; ++sub) {
         const uint64_t b0 = g0 + (uint64_t)sub * SUB + threadIdx.x;
         T key[KPT];
 #pragma unroll
@@ -292,32 +307,34 @@ static __global__ void __launch_bounds__(BK_MAXB) bucket_offsets_kernel(const ui
     }
 }
 
-// Per sub-tile (BK_T * KPT keys): every key takes a slot of its bucket in LDS (atomic on the
-// sub-tile histogram), the sub-tile is laid out bucket by bucket, and consecutive threads write
-// consecutive keys of a bucket to its global range.  The order of keys inside a bucket is not
-// kept (the bucket is sorted afterwards; the keys carry no payload).  The next sub-tile's keys
-// are loaded while the current one is placed.
+// Per sub-tile (BK_T * KPT keys): every key takes a slot of its bucket (atomic on the sub-tile
+// histogram), which gives both its global position (the bucket's next position in this
+// workgroup's range + slot) and its LDS position in the sub-tile laid out bucket by bucket
+// (scan + slot).  Key and global position go to LDS there; then consecutive threads write
+// consecutive LDS entries, i.e. consecutive keys of a bucket to consecutive addresses.  The order
+// of keys inside a bucket is not kept (the bucket is sorted afterwards; the keys carry no
+// payload).  The next sub-tile's keys are loaded while the current one is placed.
 template <typename T>
 __global__ void __launch_bounds__(BK_T) bucket_scatter_kernel(const T *__restrict__ in, uint64_t n,
                                                               const typename Comp<T>::C *__restrict__ spl_g,
-                                                              int B, int BP,
+                                                              int B, int BP, int subs,
                                                               const uint64_t *__restrict__ offs,
                                                               T *__restrict__ out) {
     using CT = Comp<T>;
-    constexpr int KPT = Geo<T>::KPT, SUB = BK_T * KPT, SUBS = BK_WG / SUB;
+    constexpr int KPT = Geo<T>::KPT, SUB = BK_T * KPT;
     __shared__ typename CT::C spl[BK_MAXB];
     __shared__ uint32_t rng[BK_SLOTS];
-    __shared__ uint64_t goff[BK_MAXB];   // next global position of each bucket (this workgroup)
-    __shared__ uint32_t hist[BK_MAXB];   // sub-tile histogram, then its exclusive scan
+    __shared__ uint2 sgo[BK_MAXB];       // (sub-tile scan, next global position) per bucket; n < 2^32
+    __shared__ uint32_t hist[BK_MAXB];   // sub-tile histogram
     __shared__ uint32_t wsum[BK_T / 64];
     __shared__ T lk[SUB];                // the sub-tile grouped by bucket
-    __shared__ uint16_t lb[SUB];         // bucket of every LDS slot
+    __shared__ uint32_t lg[SUB];         // global position of every LDS entry
     load_splitters<T>(spl_g, BP, spl);
-    for (int b = threadIdx.x; b < B; b += BK_T) goff[b] = offs[(uint64_t)blockIdx.x * B + b];
+    for (int b = threadIdx.x; b < B; b += BK_T) sgo[b] = make_uint2(0u, (uint32_t)offs[(uint64_t)blockIdx.x * B + b]);
     __syncthreads();
     build_slots<T>(spl, BP, rng);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint64_t g0 = (uint64_t)blockIdx.x * BK_WG;
+    const uint64_t g0 = (uint64_t)blockIdx.x * subs * SUB;
     T nxt[KPT];
 #pragma unroll
     for (int k = 0; k < KPT; ++k) {
@@ -325,7 +342,7 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_kernel(const T *__restric
         nxt[k] = i < n ? in[i] : T(0);
     }
 #pragma unroll 1
-    for (int sub = 0; sub < SUBS; ++sub) {
+    for (int sub = 0; sub < subs; ++sub) {
         const uint64_t s0 = g0 + (uint64_t)sub * SUB;
         if (s0 >= n) break;  // workgroup-uniform
         for (int b = threadIdx.x; b < B; b += BK_T) hist[b] = 0;
@@ -335,7 +352,7 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_kernel(const T *__restric
         uint32_t slot[KPT];
 #pragma unroll
         for (int k = 0; k < KPT; ++k) key[k] = nxt[k];
-        if (sub + 1 < SUBS) {
+        if (sub + 1 < subs) {
 #pragma unroll
             for (int k = 0; k < KPT; ++k) {
                 const uint64_t i = s0 + SUB + threadIdx.x + (uint64_t)k * BK_T;
@@ -363,14 +380,14 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_kernel(const T *__restric
         __syncthreads();
         uint32_t woff = 0;
         for (int i = 0; i < w; ++i) woff += wsum[i];
-        if (threadIdx.x < (unsigned)B) hist[threadIdx.x] = woff + incl - hv;
+        if (threadIdx.x < (unsigned)B) sgo[threadIdx.x].x = woff + incl - hv;
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < KPT; ++k) {
             if (bk[k] >= 0) {
-                const uint32_t p = hist[bk[k]] + slot[k];
-                lk[p] = key[k];
-                lb[p] = (uint16_t)bk[k];
+                const uint2 so = sgo[bk[k]];
+                lk[so.x + slot[k]] = key[k];
+                lg[so.x + slot[k]] = so.y + slot[k];
             }
         }
         __syncthreads();
@@ -378,18 +395,15 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_kernel(const T *__restric
 #pragma unroll
         for (int k = 0; k < KPT; ++k) {
             const uint32_t p = threadIdx.x + k * BK_T;
-            if (p < cnt) {
-                const int b = lb[p];
-                out[goff[b] + (p - hist[b])] = lk[p];
-            }
+#if defined(DSORT_ABL_SEQSTORE)
+            if (p < cnt) out[s0 + p] = lk[p] + (T)(lg[p] & 1);  // ablation: coalesced stores
+#else
+            if (p < cnt) out[lg[p]] = lk[p];
+#endif
         }
-        __syncthreads();
-        // advance every bucket's global position by this sub-tile's keys
-        if (threadIdx.x < (unsigned)B) {
-            const uint32_t nx = threadIdx.x + 1 < (unsigned)B ? hist[threadIdx.x + 1] : cnt;
-            goff[threadIdx.x] += nx - hist[threadIdx.x];
-        }
-        __syncthreads();
+        // advance every bucket's global position by this sub-tile's keys (sgo.x is not read
+        // again before the next scan, which follows two barriers)
+        if (threadIdx.x < (unsigned)B) sgo[threadIdx.x].y += hv;
     }
 }
 

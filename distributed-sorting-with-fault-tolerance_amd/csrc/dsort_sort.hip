@@ -494,7 +494,8 @@ static int bucket_sort_i64(dsort_ctx *ctx, const int64_t *d_in, int64_t *d_keys,
     constexpr int THREADS = Geom<T>::THREADS, K = Geom<T>::K, TILE = Geom<T>::TILE;
     constexpr uint64_t ALIGN = 16 / sizeof(T);
     const int BP = 1 << ceil_log2((uint64_t)B);
-    const uint64_t G = ceil_div(n, BK_WG);
+    const int subs = bucket_wg_subs<T>(n);
+    const uint64_t G = ceil_div(n, (uint64_t)subs * BK_T * Geo<T>::KPT);
     const uint64_t nchunk = ceil_div(G, BK_CHUNK);
     const uint32_t S = (uint32_t)B * BK_OS;
     const uint64_t tmax = ceil_div(n, TILE) + 2 * (uint64_t)B;
@@ -548,7 +549,7 @@ static int bucket_sort_i64(dsort_ctx *ctx, const int64_t *d_in, int64_t *d_keys,
     for (int b = 0; b < BP; ++b) hs[b] = b < B - 1 ? hs[(size_t)(b + 1) * BK_OS - 1] : Comp<T>::inf();
     DSORT_HIP(ctx, hipMemcpyAsync(spl, hs, (size_t)BP * sizeof(C), hipMemcpyHostToDevice, s));
     // 2. histograms, their scan, bucket starts to the host
-    hipLaunchKernelGGL(bucket_hist_kernel<T>, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, B, BP, cnt);
+    hipLaunchKernelGGL(bucket_hist_kernel<T>, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, B, BP, subs, cnt);
     hipLaunchKernelGGL(bucket_colsum_kernel, dim3((unsigned)nchunk), dim3(BK_MAXB), 0, s, cnt, (uint32_t)G, B, part);
     hipLaunchKernelGGL(bucket_scan_kernel, dim3(1), dim3(BK_MAXB), 0, s, part, (uint32_t)nchunk, B,
                        (uint32_t)TILE, (uint32_t)ALIGN, bst, tt, ntl);
@@ -575,7 +576,7 @@ static int bucket_sort_i64(dsort_ctx *ctx, const int64_t *d_in, int64_t *d_keys,
     T *bufs[2] = {d_keys, scratch};
     int cur = (passes % 2 == 0) ? 0 : 1;
     T *part_out = (bufs[cur] == d_in) ? bufs[cur ^ 1] : bufs[cur];
-    hipLaunchKernelGGL(bucket_scatter_kernel<T>, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, B, BP, offs, part_out);
+    hipLaunchKernelGGL(bucket_scatter_kernel<T>, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, B, BP, subs, offs, part_out);
     DSORT_HIP(ctx, hipGetLastError());
     // 3. tile sort inside the buckets
     hipLaunchKernelGGL((block_sort_kernel<T, THREADS, K>), dim3((unsigned)tmax), dim3(THREADS), 0, s,

@@ -731,17 +731,30 @@ static int launch_pass_w(dsort_ctx *ctx, const int *src, int *dst, const PassDes
 }
 
 // ---- bucketed sort (dsort_bucket.h) ------------------------------------------------------
-// Buckets of about 2^21 keys: at most 1024, and none below 2^25 keys (DSORT_BUCKETS=0 turns the
-// partition off, DSORT_BUCKETS=<B> forces B buckets).
+// Buckets of about 1.4 M keys (2^21 / 1.5): at most 1024, and none below 2^25 keys
+// (DSORT_BUCKETS=0 turns the partition off, DSORT_BUCKETS=<B> forces B buckets,
+// DSORT_BUCKET_KEYS=<k> sets the nominal bucket size).  The nominal size leaves room for the
+// sampling spread: at 2^30 keys the largest of the 768 buckets stays below 128 tiles, so the
+// merge inside the buckets needs 7 levels (F = 16, then F = 8), not 8.
 static int bucket_count(uint64_t n) {
     const char *e = getenv("DSORT_BUCKETS");  // read per call: tests force small bucket counts
     const int forced = e ? atoi(e) : -1;
     if (forced == 0) return 0;
-    uint64_t B = forced > 0 ? (uint64_t)forced : (n >> 21);
+    const char *k = getenv("DSORT_BUCKET_KEYS");
+    const uint64_t tk = k && atoll(k) > 0 ? (uint64_t)atoll(k) : (1ull << 22) / 3;
+    uint64_t B = forced > 0 ? (uint64_t)forced : ceil_div(n, tk);
     if (forced < 0 && n < (1ull << 25)) return 0;
     if (n >= (1ull << 32)) return 0;  // 32-bit bucket positions in the scatter
     if (B > (uint64_t)bk::BK_MAXB) B = bk::BK_MAXB;
     return B >= 2 ? (int)B : 0;
+}
+
+// Samples per bucket for the int32 splitters (sorted on the GPU): the relative spread of the
+// bucket sizes is about 1/sqrt(os).  DSORT_BUCKET_OS overrides.
+static int bucket_os() {
+    const char *e = getenv("DSORT_BUCKET_OS");
+    const int v = e ? atoi(e) : 256;
+    return v < 1 ? 1 : (v > 4096 ? 4096 : v);
 }
 
 // Group tables of the merge passes inside buckets: pass p merges groups of up to 16
@@ -756,9 +769,11 @@ static int bucket_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys,
                            hipStream_t s, bool timed, int B) {
     using namespace bk;
     const int BP = 1 << ceil_log2((uint64_t)B);
-    const uint64_t G = ceil_div(n, BK_WG);
+    const int subs = bucket_wg_subs<int32_t>(n);
+    const uint64_t G = ceil_div(n, (uint64_t)subs * BK_T * Geo<int32_t>::KPT);
     const uint64_t nchunk = ceil_div(G, BK_CHUNK);
-    const uint32_t S = (uint32_t)B * BK_OS;
+    const int os = bucket_os();
+    const uint32_t S = (uint32_t)B * (uint32_t)os;
     const uint64_t tmax = ceil_div(n, TILE) + 2 * (uint64_t)B;  // + a head and a tail per bucket
     // device arena: samples, splitters, counts, chunk sums, offsets, bucket starts, tile table
     size_t off = 0;
@@ -807,44 +822,45 @@ static int bucket_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys,
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[0], s));
         ctx->ev_mask |= 1u;
     }
-    hipLaunchKernelGGL(bucket_splitter_kernel<int32_t>, dim3(1), dim3(BK_MAXB), 0, s, smp, B, BP, spl);
+    hipLaunchKernelGGL(bucket_splitter_kernel<int32_t>, dim3(1), dim3(BK_MAXB), 0, s, smp, B, BP, os, spl);
     // 2. histograms, their scan, the scatter
-    hipLaunchKernelGGL(bucket_hist_kernel<int32_t>, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, B, BP, cnt);
+    hipLaunchKernelGGL(bucket_hist_kernel<int32_t>, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, B, BP, subs, cnt);
     hipLaunchKernelGGL(bucket_colsum_kernel, dim3((unsigned)nchunk), dim3(BK_MAXB), 0, s, cnt, (uint32_t)G, B, part);
     hipLaunchKernelGGL(bucket_scan_kernel, dim3(1), dim3(BK_MAXB), 0, s, part, (uint32_t)nchunk, B,
                        (uint32_t)TILE, 4u, bst, tt, ntl);
     hipLaunchKernelGGL(bucket_offsets_kernel, dim3((unsigned)nchunk), dim3(BK_MAXB), 0, s, cnt, part, bst, (uint32_t)G, B, offs);
     DSORT_HIP(ctx, hipGetLastError());
-    // bucket starts to the host (the pass plan depends on the bucket sizes)
+    // bucket starts to the host (the pass plan depends on the bucket sizes); the host waits for
+    // them while the scatter runs.  The scatter always writes the scratch buffer (never the
+    // input: the context owns it); the tile sort then writes whichever buffer makes the last
+    // pass land in d_keys.
     uint64_t *hb = static_cast<uint64_t *>(ctx->bucket_host);
     DSORT_HIP(ctx, hipMemcpyAsync(hb, bst, (size_t)(B + 1) * 8, hipMemcpyDeviceToHost, s));
     DSORT_HIP(ctx, hipEventRecord(ctx->bucket_ev, s));
-    // the scatter goes to the buffer the tile sort reads; choose it once the pass count is
-    // known (the host waits for the bucket starts while the scatter runs)
+    int32_t *part_out = scratch;
+    hipLaunchKernelGGL(bucket_scatter_kernel<int32_t>, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, B, BP, subs, offs, part_out);
+    DSORT_HIP(ctx, hipGetLastError());
     DSORT_HIP(ctx, hipEventSynchronize(ctx->bucket_ev));
     std::vector<uint64_t> bsz(B);
     for (int b = 0; b < B; ++b) bsz[b] = hb[b + 1] - hb[b];
     if (hb[B] != n) return set_err(ctx, DSORT_EHIP, "bucket partition lost keys");
-    // pass plan: runs per bucket, merged 16 at a time inside each bucket
-    constexpr int MAXF = 16;
+    // pass plan: the runs of every bucket; the largest bucket's run count R sets the merge
+    // levels L = ceil(log2 R), split into the fewest passes of <= max_logf levels (larger passes
+    // first).  Pass p merges groups of 2^bits[p] consecutive runs inside each bucket.
     std::vector<std::vector<uint64_t>> runs(B);
-    int passes = 0;
+    uint64_t maxruns = 1;
     for (int b = 0; b < B; ++b) {
         // the tile sort's runs of bucket b (bucket_tiles: a 0..3-key head, then TILE-key tiles)
         const uint64_t h = bucket_head(hb[b], bsz[b], 4);
         if (h) runs[b].push_back(h);
         for (uint64_t o = h; o < bsz[b]; o += TILE) runs[b].push_back(bsz[b] - o < (uint64_t)TILE ? bsz[b] - o : TILE);
-        int p = 0;
-        for (uint64_t r = runs[b].size(); r > 1; r = ceil_div(r, MAXF)) ++p;
-        passes = p > passes ? p : passes;
+        maxruns = runs[b].size() > maxruns ? runs[b].size() : maxruns;
     }
+    const std::vector<int> pbits = plan_passes(maxruns);
+    const int passes = (int)pbits.size();
     ctx->stats.merge_passes = passes;
     int32_t *bufs[2] = {d_keys, scratch};
     int cur = (passes % 2 == 0) ? 0 : 1;  // tile sort output; the passes end in d_keys
-    // scatter into the tile sort's buffer unless that is the input (in-place sort)
-    int32_t *part_out = (bufs[cur] == d_in) ? bufs[cur ^ 1] : bufs[cur];
-    hipLaunchKernelGGL(bucket_scatter_kernel<int32_t>, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, B, BP, offs, part_out);
-    DSORT_HIP(ctx, hipGetLastError());
     // 3. tile sort inside the buckets
     hipLaunchKernelGGL(block_sort_w_kernel, dim3((unsigned)tmax), dim3(THREADS), 0, s, part_out,
                        bufs[cur], (uint64_t)n, reinterpret_cast<const uint4 *>(tt), ntl);
@@ -859,6 +875,7 @@ static int bucket_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys,
     std::vector<uint32_t> tgroup;
     for (int p = 0; p < passes; ++p) {
         BucketPass bp{1, 0, 0, groups.size(), tgroup.size()};
+        const size_t MAXF = (size_t)1 << pbits[p];
         int maxr = 1;
         uint64_t base = 0, tiles = 0;
         for (int b = 0; b < B; ++b) {

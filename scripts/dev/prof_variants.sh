@@ -1,0 +1,13 @@
+#!/bin/bash
+# rocprofv3 kernel traces of scripts/dev/ktime.py for several library variants / env settings.
+# usage: scripts/dev/prof_variants.sh "<tag>:<env assignments>" ...   (tag "x:DSORT_LIB=... K=V")
+set -e
+REPO="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}"
+cd /tmp; export TMPDIR=/tmp; cd "$REPO"
+for spec in "$@"; do
+  tag=${spec%%:*}; envs=${spec#*:}
+  mkdir -p "$REPO/gpurun_out/pv_$tag"
+  env $envs timeout -k 10 120 rocprofv3 --kernel-trace -d "$REPO/gpurun_out/pv_$tag" -o run -- \
+    python3 -u "$REPO/scripts/dev/ktime.py" --reps ${REPS:-3} $KTIME_ARGS > "$REPO/gpurun_out/pv_$tag/ktime.log" 2>&1
+  grep total "$REPO/gpurun_out/pv_$tag/ktime.log" | grep -v SQLite
+done
