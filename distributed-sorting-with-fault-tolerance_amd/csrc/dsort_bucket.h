@@ -33,11 +33,21 @@ constexpr int BK_T = 1024;               // threads of the partition kernels
 constexpr int BK_MAXB = 1024;            // buckets at most (<= threads, one bucket per thread)
 constexpr int BK_OS = 32;                // samples per bucket
 constexpr int BK_CHUNK = 64;             // workgroups per column-sum chunk
+#ifndef DSORT_BK_BID
+#define DSORT_BK_BID 0                   // scatter: LDS holds bucket ids, not global positions
+#endif
 
 // Scatter sub-tile per key width: KPT keys per thread, SUB = BK_T * KPT keys staged in LDS.
 template <typename T> struct Geo;
+#ifndef DSORT_BK_LINES
+#define DSORT_BK_LINES 1                 // int32 scatter writes whole 64-byte lines (carry in LDS)
+#endif
 #ifndef DSORT_BK_KPT32
+#if DSORT_BK_LINES
+#define DSORT_BK_KPT32 14                // 56 KiB sub-tile + 64 KiB line carry
+#else
 #define DSORT_BK_KPT32 16
+#endif
 #endif
 template <> struct Geo<int32_t> { static constexpr int KPT = DSORT_BK_KPT32; };
 template <> struct Geo<int64_t> { static constexpr int KPT = 8; };
@@ -328,9 +338,15 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_kernel(const T *__restric
     __shared__ uint32_t hist[BK_MAXB];   // sub-tile histogram
     __shared__ uint32_t wsum[BK_T / 64];
     __shared__ T lk[SUB];                // the sub-tile grouped by bucket
+#if DSORT_BK_BID
+    __shared__ uint16_t lb[SUB];         // bucket of every LDS entry
+    // thread b keeps bucket b's next global position in a register (B <= BK_T)
+    uint32_t gy = threadIdx.x < (unsigned)B ? (uint32_t)offs[(uint64_t)blockIdx.x * B + threadIdx.x] : 0u;
+#else
     __shared__ uint32_t lg[SUB];         // global position of every LDS entry
-    load_splitters<T>(spl_g, BP, spl);
     for (int b = threadIdx.x; b < B; b += BK_T) sgo[b] = make_uint2(0u, (uint32_t)offs[(uint64_t)blockIdx.x * B + b]);
+#endif
+    load_splitters<T>(spl_g, BP, spl);
     __syncthreads();
     build_slots<T>(spl, BP, rng);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -380,6 +396,30 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_kernel(const T *__restric
         __syncthreads();
         uint32_t woff = 0;
         for (int i = 0; i < w; ++i) woff += wsum[i];
+#if DSORT_BK_BID
+        // (LDS start - global start) of bucket b in this sub-tile; written after the barrier
+        // that follows the previous sub-tile's stores, read after the next one
+        if (threadIdx.x < (unsigned)B) {
+            sgo[threadIdx.x] = make_uint2(woff + incl - hv, gy - (woff + incl - hv));
+            gy += hv;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < KPT; ++k) {
+            if (bk[k] >= 0) {
+                const uint32_t lp = sgo[bk[k]].x + slot[k];
+                lk[lp] = key[k];
+                lb[lp] = (uint16_t)bk[k];
+            }
+        }
+        __syncthreads();
+        const uint32_t cnt = s0 + SUB <= n ? SUB : (uint32_t)(n - s0);
+#pragma unroll
+        for (int k = 0; k < KPT; ++k) {
+            const uint32_t p = threadIdx.x + k * BK_T;
+            if (p < cnt) out[sgo[lb[p]].y + p] = lk[p];
+        }
+#else
         if (threadIdx.x < (unsigned)B) sgo[threadIdx.x].x = woff + incl - hv;
         __syncthreads();
 #pragma unroll
@@ -404,6 +444,182 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_kernel(const T *__restric
         // advance every bucket's global position by this sub-tile's keys (sgo.x is not read
         // again before the next scan, which follows two barriers)
         if (threadIdx.x < (unsigned)B) sgo[threadIdx.x].y += hv;
+#endif
+    }
+}
+
+
+// The int32 scatter with whole-line writes.  The per-sub-tile scatter above writes every
+// bucket's ~20 keys of a sub-tile as a piece of a 128-byte line: the rest of that line comes
+// from the neighbouring sub-tiles, so most lines reach memory in several partial writes, and
+// the scattered stores cost 1.3 of its 3.7 ms at 2^30 keys (measured against an ablation with
+// coalesced stores).  Here every bucket of the workgroup's range is a stream of 64-byte lines
+// (16 keys, aligned in memory): a sub-tile writes only the whole lines of each bucket (the
+// bucket's carried keys + its new keys) and carries the rest (< 16 keys per bucket) in LDS to
+// the next sub-tile.  Only the first and last line of each bucket in the workgroup's range can
+// be partial; the first is padded at the front with "phantom" entries up to the line boundary
+// (never written).  The lines are written by 4 lanes each (16-byte stores), consecutive lanes on
+// consecutive 16-byte pieces; a lane finds its line's bucket in a line->bucket map built by a
+// max-scan over the buckets' first lines.
+constexpr int BK_LK = 16;      // int32 keys per 64-byte line
+constexpr int BK_MAXC = 3072;  // lines per sub-tile at most: (SUB + 30 * BK_MAXB) / 16
+static __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const int32_t *__restrict__ in, uint64_t n,
+                                                                    const int64_t *__restrict__ spl_g,
+                                                                    int B, int BP, int subs,
+                                                                    const uint64_t *__restrict__ offs,
+                                                                    int32_t *__restrict__ out) {
+    using CT = Comp<int32_t>;
+    constexpr int KPT = Geo<int32_t>::KPT, SUB = BK_T * KPT;
+    static_assert((SUB + 30 * BK_MAXB) / BK_LK <= BK_MAXC, "line map too small");
+    static_assert(SUB < (1 << 15), "packed scan fields");
+    __shared__ int64_t spl[BK_MAXB];
+    __shared__ uint32_t rng[BK_SLOTS];
+    __shared__ uint4 st[BK_MAXB];  // per bucket: LDS start, carry|phantom|new keys, first line, line base
+    __shared__ union {
+        uint32_t hist[BK_MAXB];   // sub-tile histogram (until the scan)
+        uint16_t map[BK_MAXC];    // line -> bucket + 1 (after the scan)
+    } hm;
+    __shared__ uint32_t wsum[BK_T / 64];
+    __shared__ int32_t lk[SUB];                  // the sub-tile's new keys grouped by bucket
+    __shared__ int32_t carry[BK_MAXB * BK_LK];   // per bucket: keys not yet written (< 16)
+    const int tb = threadIdx.x, lane = tb & 63, w = tb >> 6;
+    const bool owner = tb < B;  // thread b owns bucket b's line stream
+    uint32_t vc = 0, ph = 0, gb = 0;
+    if (owner) {
+        const uint32_t o = (uint32_t)offs[(uint64_t)blockIdx.x * B + tb];
+        ph = (uint32_t)(((uintptr_t)(out + o) >> 2) & (BK_LK - 1));
+        vc = ph;
+        gb = o - ph;  // (mod 2^32) the first line of the stream starts ph entries before o
+    }
+    load_splitters<int32_t>(spl_g, BP, spl);
+    __syncthreads();
+    build_slots<int32_t>(spl, BP, rng);
+    const uint64_t g0 = (uint64_t)blockIdx.x * subs * SUB;
+    int32_t nxt[KPT];
+#pragma unroll
+    for (int k = 0; k < KPT; ++k) {
+        const uint64_t i = g0 + tb + (uint64_t)k * BK_T;
+        nxt[k] = i < n ? in[i] : 0;
+    }
+#pragma unroll 1
+    for (int sub = 0; sub < subs; ++sub) {
+        const uint64_t s0 = g0 + (uint64_t)sub * SUB;
+        if (s0 >= n) break;  // workgroup-uniform
+        const bool last = sub + 1 == subs || s0 + SUB >= n;
+        if (owner) hm.hist[tb] = 0;
+        __syncthreads();
+        int32_t key[KPT];
+        int bk[KPT];
+        uint32_t slot[KPT];
+#pragma unroll
+        for (int k = 0; k < KPT; ++k) key[k] = nxt[k];
+        if (!last) {
+#pragma unroll
+            for (int k = 0; k < KPT; ++k) {
+                const uint64_t i = s0 + SUB + tb + (uint64_t)k * BK_T;
+                nxt[k] = i < n ? in[i] : 0;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < KPT; ++k) {
+            const uint64_t i = s0 + tb + (uint64_t)k * BK_T;
+            bk[k] = -1;
+            if (i < n) {
+                bk[k] = bucket_fast<int32_t>(spl, rng, key[k], CT::make(key[k], i));
+                slot[k] = atomicAdd(&hm.hist[bk[k]], 1u);
+            }
+        }
+        __syncthreads();
+        // one scan of (new keys, lines to write) per bucket, packed in 16-bit halves
+        const uint32_t hv = owner ? hm.hist[tb] : 0;
+        const uint32_t L = vc + hv;  // entries of the stream not yet written
+        const uint32_t nl = !owner ? 0 : last ? (L > ph ? (L + BK_LK - 1) / BK_LK : 0) : L / BK_LK;
+        const uint32_t pv = hv | nl << 16;
+        uint32_t incl = pv;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) wsum[w] = incl;
+        __syncthreads();
+        uint32_t woff = 0, all = 0;
+#pragma unroll
+        for (int i = 0; i < BK_T / 64; ++i) {
+            const uint32_t v = wsum[i];
+            woff += i < w ? v : 0;
+            all += v;
+        }
+        const uint32_t ex = woff + incl - pv;
+        const uint32_t lks = ex & 0xFFFF, p0 = ex >> 16, C = all >> 16;
+        if (owner) st[tb] = make_uint4(lks, vc | ph << 5 | hv << 10, p0, gb);
+        for (uint32_t i = tb; i < C; i += BK_T) hm.map[i] = 0;  // the histogram is dead
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < KPT; ++k)
+            if (bk[k] >= 0) lk[st[bk[k]].x + slot[k]] = key[k];
+        if (nl) hm.map[p0] = (uint16_t)(tb + 1);
+        __syncthreads();
+        // max-scan of the map: every line gets the bucket of the last first-line at or before it
+        uint32_t m[3];
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            const uint32_t i = 3 * tb + t;
+            m[t] = i < C ? hm.map[i] : 0;
+            if (t) m[t] = m[t] > m[t - 1] ? m[t] : m[t - 1];
+        }
+        uint32_t mx = m[2];
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(mx, o);
+            if (lane >= o) mx = y > mx ? y : mx;
+        }
+        const uint32_t below = __shfl_up(mx, 1);
+        if (lane == 63) wsum[w] = mx;
+        __syncthreads();
+        uint32_t pre = lane ? below : 0;
+        for (int i = 0; i < w; ++i) pre = wsum[i] > pre ? wsum[i] : pre;
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            const uint32_t i = 3 * tb + t;
+            if (i < C) hm.map[i] = (uint16_t)(m[t] > pre ? m[t] : pre);
+        }
+        __syncthreads();
+        // whole lines: 4 lanes per line, 4 keys (16 bytes) per lane
+        for (uint32_t it = tb; it < 4 * C; it += BK_T) {
+            const uint32_t j = it >> 2, q = it & 3;
+            const int b = (int)hm.map[j] - 1;
+            const uint4 sb = st[b];
+            const uint32_t cv = sb.y & 31, cp = (sb.y >> 5) & 31, cL = cv + (sb.y >> 10);
+            const uint32_t e0 = (j - sb.z) * BK_LK + 4 * q;
+            int32_t v[4];
+            bool ok[4];
+            bool full = true;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const uint32_t e = e0 + t;
+                ok[t] = e >= cp && e < cL;
+                full = full && ok[t];
+                v[t] = !ok[t] ? 0 : e < cv ? carry[b * BK_LK + e] : lk[sb.x + e - cv];
+            }
+            const uint32_t gi = sb.w + e0;  // mod 2^32
+            if (full) {
+                *reinterpret_cast<int4 *>(out + gi) = make_int4(v[0], v[1], v[2], v[3]);
+            } else {
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    if (ok[t]) out[(uint32_t)(gi + t)] = v[t];
+            }
+        }
+        if (last) break;
+        __syncthreads();
+        // carry the tail of every stream: entries [16 nl, L) -> carry[0, L - 16 nl)
+        if (owner) {
+            const uint32_t nv = L - nl * BK_LK;
+            for (uint32_t e2 = nl ? 0 : vc; e2 < nv; ++e2)
+                carry[tb * BK_LK + e2] = lk[lks + nl * BK_LK + e2 - vc];
+            if (nl) ph = 0;
+            gb += nl * BK_LK;
+            vc = nv;
+        }
     }
 }
 

@@ -838,7 +838,11 @@ static int bucket_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys,
     DSORT_HIP(ctx, hipMemcpyAsync(hb, bst, (size_t)(B + 1) * 8, hipMemcpyDeviceToHost, s));
     DSORT_HIP(ctx, hipEventRecord(ctx->bucket_ev, s));
     int32_t *part_out = scratch;
+#if DSORT_BK_LINES
+    hipLaunchKernelGGL(bucket_scatter_lines_kernel, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, B, BP, subs, offs, part_out);
+#else
     hipLaunchKernelGGL(bucket_scatter_kernel<int32_t>, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, B, BP, subs, offs, part_out);
+#endif
     DSORT_HIP(ctx, hipGetLastError());
     DSORT_HIP(ctx, hipEventSynchronize(ctx->bucket_ev));
     std::vector<uint64_t> bsz(B);

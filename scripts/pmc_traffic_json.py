@@ -10,7 +10,8 @@ import json
 import sys
 
 NAMES = {"block_sort_w_kernel": "block_sort_w_kernel", "mergew_kernel": "mergew_kernel",
-         "partk_kernel": "partk_kernel"}
+         "partk_kernel": "partk_kernel", "bucket_hist_kernel": "bucket_hist_kernel",
+         "bucket_scatter": "bucket_scatter"}
 
 
 def per_kernel(path, counter):
