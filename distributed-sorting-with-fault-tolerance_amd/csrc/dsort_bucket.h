@@ -461,6 +461,23 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_kernel(const T *__restric
 // (never written).  The lines are written by 4 lanes each (16-byte stores), consecutive lanes on
 // consecutive 16-byte pieces; a lane finds its line's bucket in a line->bucket map built by a
 // max-scan over the buckets' first lines.
+#ifndef DSORT_BK_XCD
+#define DSORT_BK_XCD 0
+#endif
+// Workgroup -> key range.  Workgroups are dispatched round-robin over the 8 XCDs; with
+// DSORT_BK_XCD every XCD takes a contiguous block of ranges instead, so the workgroups sharing
+// an L2 write adjacent pieces of every bucket (a bijection on [0, G) for any G).
+__device__ __forceinline__ uint32_t wg_order(uint32_t bid, uint32_t G) {
+#if DSORT_BK_XCD
+    constexpr uint32_t NX = 8;
+    const uint32_t q = G / NX, r = G % NX, x = bid % NX, i = bid / NX;
+    return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
+#else
+    (void)G;
+    return bid;
+#endif
+}
+
 constexpr int BK_LK = 16;      // int32 keys per 64-byte line
 constexpr int BK_MAXC = 3072;  // lines per sub-tile at most: (SUB + 30 * BK_MAXB) / 16
 static __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const int32_t *__restrict__ in, uint64_t n,
@@ -483,10 +500,11 @@ static __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const
     __shared__ int32_t lk[SUB];                  // the sub-tile's new keys grouped by bucket
     __shared__ int32_t carry[BK_MAXB * BK_LK];   // per bucket: keys not yet written (< 16)
     const int tb = threadIdx.x, lane = tb & 63, w = tb >> 6;
+    const uint32_t g = wg_order(blockIdx.x, gridDim.x);
     const bool owner = tb < B;  // thread b owns bucket b's line stream
     uint32_t vc = 0, ph = 0, gb = 0;
     if (owner) {
-        const uint32_t o = (uint32_t)offs[(uint64_t)blockIdx.x * B + tb];
+        const uint32_t o = (uint32_t)offs[(uint64_t)g * B + tb];
         ph = (uint32_t)(((uintptr_t)(out + o) >> 2) & (BK_LK - 1));
         vc = ph;
         gb = o - ph;  // (mod 2^32) the first line of the stream starts ph entries before o
@@ -494,7 +512,7 @@ static __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const
     load_splitters<int32_t>(spl_g, BP, spl);
     __syncthreads();
     build_slots<int32_t>(spl, BP, rng);
-    const uint64_t g0 = (uint64_t)blockIdx.x * subs * SUB;
+    const uint64_t g0 = (uint64_t)g * subs * SUB;
     int32_t nxt[KPT];
 #pragma unroll
     for (int k = 0; k < KPT; ++k) {

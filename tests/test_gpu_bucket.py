@@ -124,3 +124,44 @@ def test_bucketed_zipf_i64_2p26(gpu_ctx, monkeypatch):
     torch.cuda.synchronize()
     assert gpu_ctx.descents(o1) == 0 and gpu_ctx.fingerprint(o1) == fp
     assert torch.equal(o1, o2)
+
+
+@pytest.mark.parametrize("dtype", ["i32", "i64"])
+@pytest.mark.parametrize("shift_in,shift_out", [(1, 3), (3, 0), (0, 5), (2, 2)])
+@pytest.mark.parametrize("B,n", [(5, 300_001), (700, 2_000_003)])
+def test_bucketed_sort_unaligned_views(gpu_ctx, monkeypatch, dtype, shift_in, shift_out, B, n):
+    """Input and output tensors that start at element offsets (not 16-byte aligned): the 16-byte
+    loads of the tile sort and the line-aligned bucket scatter must not assume aligned caller
+    buffers."""
+    import torch
+    monkeypatch.setenv("DSORT_BUCKETS", str(B))
+    rng = np.random.default_rng(B + shift_in * 7 + shift_out)
+    a = _keys(rng, "uniform", n) if dtype == "i32" else _keys64(rng, "uniform", n)
+    tdt = torch.int32 if dtype == "i32" else torch.int64
+    src = torch.empty(n + 8, dtype=tdt, device="cuda")
+    dst = torch.full((n + 8,), 77, dtype=tdt, device="cuda")
+    src[shift_in:shift_in + n] = torch.from_numpy(a).cuda()
+    gpu_ctx.sort_dev(src[shift_in:shift_in + n], dst[shift_out:shift_out + n])
+    torch.cuda.synchronize()
+    d = dst.cpu().numpy()
+    assert np.array_equal(d[shift_out:shift_out + n], np.sort(a))
+    assert (d[:shift_out] == 77).all() and (d[shift_out + n:] == 77).all()  # nothing written outside
+    assert np.array_equal(src[shift_in:shift_in + n].cpu().numpy(), a)
+
+
+@pytest.mark.parametrize("dtype", ["i32", "i64"])
+@pytest.mark.parametrize("shift", [1, 2, 3])
+def test_bucketed_sort_unaligned_view_in_place(gpu_ctx, monkeypatch, dtype, shift):
+    import torch
+    monkeypatch.setenv("DSORT_BUCKETS", "37")
+    n = 1_500_007
+    rng = np.random.default_rng(shift)
+    a = _keys(rng, "few", n) if dtype == "i32" else _keys64(rng, "few", n)
+    tdt = torch.int32 if dtype == "i32" else torch.int64
+    buf = torch.full((n + 8,), 5, dtype=tdt, device="cuda")
+    buf[shift:shift + n] = torch.from_numpy(a).cuda()
+    gpu_ctx.sort_dev(buf[shift:shift + n])
+    torch.cuda.synchronize()
+    d = buf.cpu().numpy()
+    assert np.array_equal(d[shift:shift + n], np.sort(a))
+    assert (d[:shift] == 5).all() and (d[shift + n:] == 5).all()
