@@ -25,9 +25,15 @@ template <> struct Geom<int32_t> {
     static constexpr int K = 16;
     static constexpr int TILE = THREADS * K;
 };
+#ifndef DSORT_T64
+#define DSORT_T64 512
+#endif
+#ifndef DSORT_K64
+#define DSORT_K64 8
+#endif
 template <> struct Geom<int64_t> {
-    static constexpr int THREADS = 512;
-    static constexpr int K = 8;
+    static constexpr int THREADS = DSORT_T64;
+    static constexpr int K = DSORT_K64;
     static constexpr int TILE = THREADS * K;
 };
 
