@@ -173,11 +173,35 @@ __device__ __forceinline__ void load_splitters(const typename Comp<T>::C *spl_g,
 
 // Keys per partition workgroup: `subs` sub-tiles of BK_T * KPT keys, 4..16 so that a large
 // input gets >= ~2048 workgroups with long per-bucket runs and a small one still fills the chip.
+// The scatter holds one workgroup per CU (its LDS), so it runs in rounds of BK_CUS workgroups:
+// among subs values up to that cap the one with the fewest sub-tiles per CU over all rounds wins
+// (2^30 int32: 14 sub-tiles, 21 rounds = 294 sub-tiles per CU, instead of 16 with 18.3 rounds =
+// 19 x 16 = 304).
+#ifndef DSORT_BK_BALANCE
+#define DSORT_BK_BALANCE 1
+#endif
+constexpr uint64_t BK_CUS = 256;  // MI355X compute units
 template <typename T>
 __host__ __forceinline__ int bucket_wg_subs(uint64_t n) {
     const uint64_t sub = (uint64_t)BK_T * Geo<T>::KPT;
     const uint64_t v = n / (2048 * sub);
-    return v < 4 ? 4 : (v > 16 ? 16 : (int)v);
+    const int cap = v < 4 ? 4 : (v > 16 ? 16 : (int)v);
+#if DSORT_BK_BALANCE
+    if (cap > 4) {
+        const uint64_t nsub = (n + sub - 1) / sub;
+        int best = cap;
+        uint64_t bcost = ~0ull;
+        for (int s = cap; s >= (cap + 1) / 2; --s) {
+            const uint64_t rounds = ((nsub + s - 1) / s + BK_CUS - 1) / BK_CUS;
+            if (rounds * s < bcost) {
+                bcost = rounds * s;
+                best = s;
+            }
+        }
+        return best;
+    }
+#endif
+    return cap;
 }
 
 // counts[g * B + b] = keys of workgroup g's subs sub-tiles in bucket b
