@@ -33,6 +33,7 @@
 #include <climits>
 #include <cstdlib>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #include "dsort_bucket.h"
@@ -731,17 +732,18 @@ static int launch_pass_w(dsort_ctx *ctx, const int *src, int *dst, const PassDes
 }
 
 // ---- bucketed sort (dsort_bucket.h) ------------------------------------------------------
-// Buckets of about 1.4 M keys (2^21 / 1.5): at most 1024, and none below 2^25 keys
+// Buckets of about 2^20 keys (64 tiles): at most 1024, and none below 2^25 keys
 // (DSORT_BUCKETS=0 turns the partition off, DSORT_BUCKETS=<B> forces B buckets,
-// DSORT_BUCKET_KEYS=<k> sets the nominal bucket size).  The nominal size leaves room for the
-// sampling spread: at 2^30 keys the largest of the 768 buckets stays below 128 tiles, so the
-// merge inside the buckets needs 7 levels (F = 16, then F = 8), not 8.
+// DSORT_BUCKET_KEYS=<k> sets the nominal bucket size).  At 2^30 keys the largest of the 1024
+// buckets stays below 128 tiles (7 merge levels: F = 16, then F = 8), and the buckets of <= 64
+// runs take F = 8 twice (per-bucket fan-in, below).  768 buckets of 1.4 M keys: 15.49-15.53 ms;
+// 1024: 15.32-15.37 ms (profiles/r1_bucket_fanin_ab.txt).
 static int bucket_count(uint64_t n) {
     const char *e = getenv("DSORT_BUCKETS");  // read per call: tests force small bucket counts
     const int forced = e ? atoi(e) : -1;
     if (forced == 0) return 0;
     const char *k = getenv("DSORT_BUCKET_KEYS");
-    const uint64_t tk = k && atoll(k) > 0 ? (uint64_t)atoll(k) : (1ull << 22) / 3;
+    const uint64_t tk = k && atoll(k) > 0 ? (uint64_t)atoll(k) : (1ull << 20);
     uint64_t B = forced > 0 ? (uint64_t)forced : ceil_div(n, tk);
     if (forced < 0 && n < (1ull << 25)) return 0;
     if (n >= (1ull << 32)) return 0;  // 32-bit bucket positions in the scatter
@@ -873,22 +875,37 @@ static int bucket_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys,
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[1], s));
         ctx->ev_mask |= 2u;
     }
-    // 4. group tables of every pass (one staging buffer, one copy)
-    std::vector<BucketPass> plan;
+    // 4. group tables of every pass (one staging buffer, one copy).  Every bucket gets its own
+    // fan-in per pass: the passes after the first keep the global plan's fan-in and the first
+    // takes only the levels the bucket still needs (a bucket of <= 64 runs merges F = 8 twice
+    // instead of F = 16 then F = 8).  A pass is then one launch per kernel fan-in among its
+    // groups (DSORT_BUCKET_FANIN=global keeps the global fan-in for every bucket).
+    const bool per_bucket = !(getenv("DSORT_BUCKET_FANIN") && std::string(getenv("DSORT_BUCKET_FANIN")) == "global");
+    std::vector<BucketPass> plan;  // one entry per launch
+    std::vector<int> plan_pass;    // the pass of every launch
     std::vector<GroupK> groups;
     std::vector<uint32_t> tgroup;
+    std::vector<int> tail(passes + 1, 0);  // tail[p] = levels of the global plan from pass p on
+    for (int p = passes - 1; p >= 0; --p) tail[p] = tail[p + 1] + pbits[p];
+    std::vector<int> blev(B);
+    for (int b = 0; b < B; ++b) blev[b] = ceil_log2((uint64_t)runs[b].size());
     for (int p = 0; p < passes; ++p) {
-        BucketPass bp{1, 0, 0, groups.size(), tgroup.size()};
-        const size_t MAXF = (size_t)1 << pbits[p];
-        int maxr = 1;
-        uint64_t base = 0, tiles = 0;
+        std::vector<GroupK> pg;       // this pass's groups (base = global key position)
+        std::vector<int> pk;          // kernel log2 fan-in of every group
+        uint64_t base = 0;
         for (int b = 0; b < B; ++b) {
+            int fb = pbits[p];
+            if (per_bucket) {
+                const int need = blev[b] - tail[p + 1];  // levels this pass must resolve
+                fb = need < 0 ? 0 : (need < pbits[p] ? need : pbits[p]);
+                blev[b] -= fb;
+            }
+            const size_t MAXF = (size_t)1 << fb;
             std::vector<uint64_t> next;
             const size_t nr = runs[b].size();
             for (size_t r0 = 0; r0 < nr; r0 += MAXF) {
                 GroupK gk{};
                 gk.base = base;
-                gk.first_tile = tiles;
                 gk.roff[0] = 0;
                 uint64_t tot = 0;
                 for (size_t r = r0; r < nr && r < r0 + MAXF; ++r) {
@@ -897,20 +914,40 @@ static int bucket_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys,
                 }
                 for (int r = (int)gk.nruns + 1; r <= kMaxF; ++r) gk.roff[r] = tot;
                 gk.total = tot;
-                maxr = (int)gk.nruns > maxr ? (int)gk.nruns : maxr;
-                const uint64_t gt = ceil_div(tot, (uint64_t)TNOM);
-                for (uint64_t k = 0; k < gt; ++k) tgroup.push_back((uint32_t)(groups.size() - bp.group_off));
-                tiles += gt;
                 base += tot;
                 next.push_back(tot);
-                groups.push_back(gk);
+                pg.push_back(gk);
+                const int kl = ceil_log2((uint64_t)gk.nruns);
+                pk.push_back(kl < 1 ? 1 : kl);
             }
             runs[b].swap(next);
         }
-        bp.logf = ceil_log2((uint64_t)maxr) < 1 ? 1 : ceil_log2((uint64_t)maxr);
-        bp.ngroups = groups.size() - bp.group_off;
-        bp.ntiles = tiles;
-        plan.push_back(bp);
+        // launch classes: the fan-ins of the groups that merge >= 3 runs; groups of 1-2 runs ride
+        // with the smallest class (or form the only one)
+        int lmin = 99, lmax = 1;
+        for (size_t g = 0; g < pg.size(); ++g)
+            if (pk[g] >= 2) { lmin = pk[g] < lmin ? pk[g] : lmin; lmax = pk[g] > lmax ? pk[g] : lmax; }
+        if (lmin == 99) lmin = lmax = 1;
+        for (size_t g = 0; g < pg.size(); ++g) pk[g] = pk[g] < lmin ? lmin : pk[g];
+        for (int l = lmin; l <= lmax; ++l) {
+            BucketPass bp{l, 0, 0, groups.size(), tgroup.size()};
+            uint64_t tiles = 0;
+            for (size_t g = 0; g < pg.size(); ++g) {
+                if (pk[g] != l) continue;
+                GroupK gk = pg[g];
+                gk.first_tile = tiles;
+                const uint64_t gt = ceil_div(gk.total, (uint64_t)TNOM);
+                for (uint64_t k = 0; k < gt; ++k) tgroup.push_back((uint32_t)(groups.size() - bp.group_off));
+                tiles += gt;
+                groups.push_back(gk);
+            }
+            bp.ngroups = groups.size() - bp.group_off;
+            bp.ntiles = tiles;
+            if (bp.ngroups) {
+                plan.push_back(bp);
+                plan_pass.push_back(p);
+            }
+        }
     }
     if (passes > 0) {
         const size_t gbytes = groups.size() * sizeof(GroupK), tbytes = tgroup.size() * sizeof(uint32_t);
@@ -935,13 +972,15 @@ static int bucket_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys,
         ctx->groups_ev_pending = true;
         const GroupK *dg = static_cast<const GroupK *>(ctx->groups);
         const uint32_t *dt = reinterpret_cast<const uint32_t *>(static_cast<const char *>(ctx->groups) + tb_off);
-        for (int p = 0; p < passes; ++p) {
-            PassDesc pd{(uint64_t)n, 0, 1 << plan[p].logf, (int)plan[p].ngroups, dg + plan[p].group_off};
-            pd.tile_group = dt + plan[p].tile_off;
-            rc = launch_pass_w<false>(ctx, bufs[cur], bufs[cur ^ 1], pd, plan[p].logf, plan[p].ntiles, s, timed);
+        for (size_t q = 0; q < plan.size(); ++q) {
+            PassDesc pd{(uint64_t)n, 0, 1 << plan[q].logf, (int)plan[q].ngroups, dg + plan[q].group_off};
+            pd.tile_group = dt + plan[q].tile_off;
+            rc = launch_pass_w<false>(ctx, bufs[cur], bufs[cur ^ 1], pd, plan[q].logf, plan[q].ntiles, s, timed);
             if (rc) return rc;
-            cur ^= 1;
-            fault_point(s, p);
+            if (q + 1 == plan.size() || plan_pass[q + 1] != plan_pass[q]) {  // pass complete
+                cur ^= 1;
+                fault_point(s, plan_pass[q]);
+            }
         }
     }
     if (timed && ctx->ev_ok) {

@@ -8,6 +8,6 @@ for L in ${LOGFS:-3 4 5 6}; do
 import json,sys
 L=sys.argv[1]
 d=json.loads(open(f"gpurun_out/sweep_{L}.log").read().strip().splitlines()[-1])
-print(f"logf={L} value={d['value']/1e9:.2f} Gkeys/s ms={d['ms_per_step']:.2f} merge_kernel_ms={d['roofline']['avg_launch_ms']} frac={d['roofline']['frac']} block_ms={d['roofline']['block_sort_ms']} cfg={d['config']['workload']}")
+print(f"logf={L} value={d['value']/1e9:.2f} Gkeys/s ms={d['ms_per_step']:.2f} merge_kernel_ms={d['roofline']['avg_pass_ms']} frac={d['roofline']['frac']} block_ms={d['roofline']['block_sort_ms']} cfg={d['config']['workload']}")
 PY
 done

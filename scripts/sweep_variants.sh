@@ -8,6 +8,6 @@ for V in $VARIANTS; do
 import json,sys
 V=sys.argv[1]
 d=json.loads(open(f"gpurun_out/var_{V}.log").read().strip().splitlines()[-1])
-print(f"{V}: value={d['value']/1e9:.2f} Gkeys/s ms={d['ms_per_step']:.2f} merge_kernel_ms={d['roofline']['avg_launch_ms']} block_ms={d['roofline']['block_sort_ms']}")
+print(f"{V}: value={d['value']/1e9:.2f} Gkeys/s ms={d['ms_per_step']:.2f} merge_kernel_ms={d['roofline']['avg_pass_ms']} block_ms={d['roofline']['block_sort_ms']}")
 PY
 done
