@@ -146,7 +146,7 @@ def pmc_traffic(kernel, n, w):
         return None
     if w != 4:
         return None
-    return round(rec["traffic_bytes"] * n / (1 << 30))
+    return round(rec.get("traffic_bytes_per_pass", rec["traffic_bytes"]) * n / (1 << 30))
 
 
 # ------------------------------------------------------------------------- GPU runs

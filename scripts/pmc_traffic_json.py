@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """profiles/r1_pmc_traffic.json from two rocprofv3 PMC passes (FETCH_SIZE and WRITE_SIZE runs of
 scripts/pmc.sh over scripts/kdriver.py at 2^30 uniform int32):
-   pmc_traffic_json.py <fetch counter_collection.csv> <write counter_collection.csv> [note]
+   pmc_traffic_json.py <fetch counter_collection.csv> <write counter_collection.csv> [note] [passes]
 Per-launch bytes: FETCH_SIZE (KB) x 2 (MI355X_MICROARCH.md HBM section: wide streaming reads
 report half their bytes) + WRITE_SIZE (KB)."""
 import collections
@@ -23,7 +23,7 @@ def per_kernel(path, counter):
             if key in r["Kernel_Name"]:
                 tot[key] += float(r["Counter_Value"])
                 disp[key].add(r["Dispatch_Id"])
-    return {k: (tot[k] / len(disp[k]) * 1024, len(disp[k])) for k in tot}
+    return {k: (tot[k] / len(disp[k]) * 1024, len(disp[k]), tot[k] * 1024) for k in tot}
 
 
 fetch = per_kernel(sys.argv[1], "FETCH_SIZE")
@@ -38,11 +38,17 @@ out = {
                    + (sys.argv[3] if len(sys.argv) > 3 else ""),
     "kernels": {},
 }
+# a merge pass may be several launches (one per kernel fan-in): per-pass bytes = all merge
+# launches / (sorts x passes), sorts = tile-sort launches
+passes = int(sys.argv[4]) if len(sys.argv) > 4 else 0
+sorts = fetch.get("block_sort_w_kernel", (0, 0, 0))[1]
 for k in NAMES:
     if k in fetch and k in write:
-        f, n = fetch[k]
-        wb, _ = write[k]
+        f, n, ft = fetch[k]
+        wb, _, wt = write[k]
         out["kernels"][k] = {"launches": n, "fetch_bytes": 2 * f, "write_bytes": wb,
                              "traffic_bytes": 2 * f + wb}
+        if k == "mergew_kernel" and passes and sorts:
+            out["kernels"][k]["traffic_bytes_per_pass"] = (2 * ft + wt) / (sorts * passes)
 json.dump(out, sys.stdout, indent=1)
 print()
