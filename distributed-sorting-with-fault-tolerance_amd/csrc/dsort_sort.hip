@@ -560,18 +560,18 @@ static int bucket_sort_i64(dsort_ctx *ctx, const int64_t *d_in, int64_t *d_keys,
     DSORT_HIP(ctx, hipEventRecord(ctx->bucket_ev, s));
     DSORT_HIP(ctx, hipEventSynchronize(ctx->bucket_ev));
     if (hb[B] != n) return set_err(ctx, DSORT_EHIP, "bucket partition lost keys");
-    // pass plan: the tile sort's runs of every bucket, merged 2^max_logf at a time
-    const int MAXF = 1 << max_logf();
+    // pass plan: the tile sort's runs of every bucket; the largest bucket's run count sets the
+    // levels, spread over the fewest passes of <= max_logf levels (as the int32 driver)
     std::vector<std::vector<uint64_t>> runs(B);
-    int passes = 0;
+    uint64_t maxruns = 1;
     for (int b = 0; b < B; ++b) {
         const uint64_t len = hb[b + 1] - hb[b], h = bucket_head(hb[b], len, ALIGN);
         if (h) runs[b].push_back(h);
         for (uint64_t o = h; o < len; o += TILE) runs[b].push_back(len - o < (uint64_t)TILE ? len - o : TILE);
-        int p = 0;
-        for (uint64_t r = runs[b].size(); r > 1; r = ceil_div(r, MAXF)) ++p;
-        passes = p > passes ? p : passes;
+        maxruns = runs[b].size() > maxruns ? runs[b].size() : maxruns;
     }
+    const std::vector<int> pbits = plan_passes(maxruns);
+    const int passes = (int)pbits.size();
     ctx->stats.merge_passes = passes;
     T *bufs[2] = {d_keys, scratch};
     int cur = (passes % 2 == 0) ? 0 : 1;
@@ -586,28 +586,35 @@ static int bucket_sort_i64(dsort_ctx *ctx, const int64_t *d_in, int64_t *d_keys,
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[1], s));
         ctx->ev_mask |= 2u;
     }
-    // 4. group tables of every pass (one staging buffer, one copy), then the passes
-    struct PassPlan { int logf; uint64_t ngroups, ntiles; size_t group_off, tile_off; };
-    std::vector<PassPlan> plan;
+    // 4. group tables of every pass (one staging buffer, one copy), then the passes.  Per-bucket
+    // fan-in as in the int32 driver: the passes after the first keep the global fan-in, the first
+    // resolves only the levels the bucket still needs; one launch per kernel fan-in of a pass.
+    const bool per_bucket = !(getenv("DSORT_BUCKET_FANIN") && std::string(getenv("DSORT_BUCKET_FANIN")) == "global");
+    struct PassPlan { int logf; uint64_t ngroups, ntiles; size_t group_off, tile_off; int pass; };
+    std::vector<PassPlan> plan;  // one entry per launch
     std::vector<GroupK> groups;
     std::vector<uint32_t> tgroup;
+    std::vector<int> tail(passes + 1, 0);
+    for (int p = passes - 1; p >= 0; --p) tail[p] = tail[p + 1] + pbits[p];
+    std::vector<int> blev(B);
+    for (int b = 0; b < B; ++b) blev[b] = ceil_log2((uint64_t)runs[b].size());
     for (int p = 0; p < passes; ++p) {
-        int maxr = 1;
-        for (int b = 0; b < B; ++b)
-            for (size_t r0 = 0; r0 < runs[b].size(); r0 += MAXF) {
-                const int nr = (int)std::min<size_t>(MAXF, runs[b].size() - r0);
-                maxr = nr > maxr ? nr : maxr;
-            }
-        PassPlan pp{ceil_log2((uint64_t)maxr) < 1 ? 1 : ceil_log2((uint64_t)maxr), 0, 0, groups.size(), tgroup.size()};
-        const uint64_t tn = (uint64_t)tnom_of<T>(pp.logf);
-        uint64_t base = 0, tiles = 0;
+        std::vector<GroupK> pg;
+        std::vector<int> pk;
+        uint64_t base = 0;
         for (int b = 0; b < B; ++b) {
+            int fb = pbits[p];
+            if (per_bucket) {
+                const int need = blev[b] - tail[p + 1];
+                fb = need < 0 ? 0 : (need < pbits[p] ? need : pbits[p]);
+                blev[b] -= fb;
+            }
+            const size_t MAXF = (size_t)1 << fb;
             std::vector<uint64_t> next;
             const size_t nr = runs[b].size();
             for (size_t r0 = 0; r0 < nr; r0 += MAXF) {
                 GroupK gk{};
                 gk.base = base;
-                gk.first_tile = tiles;
                 uint64_t tot = 0;
                 for (size_t r = r0; r < nr && r < r0 + MAXF; ++r) {
                     tot += runs[b][r];
@@ -615,18 +622,36 @@ static int bucket_sort_i64(dsort_ctx *ctx, const int64_t *d_in, int64_t *d_keys,
                 }
                 for (int r = (int)gk.nruns + 1; r <= kMaxF; ++r) gk.roff[r] = tot;
                 gk.total = tot;
-                const uint64_t gt = ceil_div(tot, tn);
-                for (uint64_t k = 0; k < gt; ++k) tgroup.push_back((uint32_t)(groups.size() - pp.group_off));
-                tiles += gt;
                 base += tot;
                 next.push_back(tot);
-                groups.push_back(gk);
+                pg.push_back(gk);
+                const int kl = ceil_log2((uint64_t)gk.nruns);
+                pk.push_back(kl < 1 ? 1 : kl);
             }
             runs[b].swap(next);
         }
-        pp.ngroups = groups.size() - pp.group_off;
-        pp.ntiles = tiles;
-        plan.push_back(pp);
+        int lmin = 99, lmax = 1;
+        for (size_t g = 0; g < pg.size(); ++g)
+            if (pk[g] >= 2) { lmin = pk[g] < lmin ? pk[g] : lmin; lmax = pk[g] > lmax ? pk[g] : lmax; }
+        if (lmin == 99) lmin = lmax = 1;
+        for (size_t g = 0; g < pg.size(); ++g) pk[g] = pk[g] < lmin ? lmin : pk[g];
+        for (int l = lmin; l <= lmax; ++l) {
+            PassPlan pp{l, 0, 0, groups.size(), tgroup.size(), p};
+            const uint64_t tn = (uint64_t)tnom_of<T>(l);
+            uint64_t tiles = 0;
+            for (size_t g = 0; g < pg.size(); ++g) {
+                if (pk[g] != l) continue;
+                GroupK gk = pg[g];
+                gk.first_tile = tiles;
+                const uint64_t gt = ceil_div(gk.total, tn);
+                for (uint64_t k = 0; k < gt; ++k) tgroup.push_back((uint32_t)(groups.size() - pp.group_off));
+                tiles += gt;
+                groups.push_back(gk);
+            }
+            pp.ngroups = groups.size() - pp.group_off;
+            pp.ntiles = tiles;
+            if (pp.ngroups) plan.push_back(pp);
+        }
     }
     if (passes > 0) {
         const size_t gbytes = groups.size() * sizeof(GroupK), tbytes = tgroup.size() * sizeof(uint32_t);
@@ -651,14 +676,16 @@ static int bucket_sort_i64(dsort_ctx *ctx, const int64_t *d_in, int64_t *d_keys,
         ctx->groups_ev_pending = true;
         const GroupK *dg = static_cast<const GroupK *>(ctx->groups);
         const uint32_t *dt = reinterpret_cast<const uint32_t *>(static_cast<const char *>(ctx->groups) + tb_off);
-        for (int p = 0; p < passes; ++p) {
-            PassDesc pd{(uint64_t)n, 0, 1 << plan[p].logf, (int)plan[p].ngroups, dg + plan[p].group_off};
-            pd.tile_group = dt + plan[p].tile_off;
-            rc = launch_pass<T, THREADS, K, false>(ctx, bufs[cur], bufs[cur ^ 1], pd, plan[p].logf,
-                                                   plan[p].ntiles, s, timed);
+        for (size_t q = 0; q < plan.size(); ++q) {
+            PassDesc pd{(uint64_t)n, 0, 1 << plan[q].logf, (int)plan[q].ngroups, dg + plan[q].group_off};
+            pd.tile_group = dt + plan[q].tile_off;
+            rc = launch_pass<T, THREADS, K, false>(ctx, bufs[cur], bufs[cur ^ 1], pd, plan[q].logf,
+                                                   plan[q].ntiles, s, timed);
             if (rc) return rc;
-            cur ^= 1;
-            fault_point(s, p);
+            if (q + 1 == plan.size() || plan[q + 1].pass != plan[q].pass) {  // pass complete
+                cur ^= 1;
+                fault_point(s, plan[q].pass);
+            }
         }
     }
     if (timed && ctx->ev_ok) {
