@@ -116,9 +116,10 @@ __device__ __forceinline__ int bucket_of(const typename Comp<T>::C *spl, int BP,
 constexpr int BK_SLOTB = DSORT_BK_SLOTB;
 constexpr int BK_SLOTS = 1 << BK_SLOTB;
 
-template <typename T>
+template <typename T, int SB = BK_SLOTB>
 __device__ __forceinline__ void build_slots(const typename Comp<T>::C *spl, int BP, uint32_t *rng) {
     using CT = Comp<T>;
+    constexpr int BK_SLOTB = SB, BK_SLOTS = 1 << SB;
     for (int i = threadIdx.x; i < BK_SLOTS; i += blockDim.x) {
         uint32_t cnt[2];
 #pragma unroll
@@ -132,10 +133,10 @@ __device__ __forceinline__ void build_slots(const typename Comp<T>::C *spl, int 
     }
 }
 
-template <typename T>
+template <typename T, int SB = BK_SLOTB>
 __device__ __forceinline__ int bucket_fast(const typename Comp<T>::C *spl, const uint32_t *rng,
                                            T key, const typename Comp<T>::C &c) {
-    const uint32_t r = rng[Comp<T>::slot_of(key, BK_SLOTB)];
+    const uint32_t r = rng[Comp<T>::slot_of(key, SB)];
     int lo = (int)(r & 0xFFFF), hi = (int)(r >> 16);
     while (lo < hi) {  // lower bound among the splitters of the slot
         const int mid = (lo + hi) >> 1;
@@ -204,7 +205,11 @@ __host__ __forceinline__ int bucket_wg_subs(uint64_t n) {
     return cap;
 }
 
-// counts[g * B + b] = keys of workgroup g's subs sub-tiles in bucket b
+// counts[g * B + b] = keys of workgroup g's subs sub-tiles in bucket b.  The histogram has LDS to
+// spare, so its slot table can be finer than the scatter's (DSORT_BK_HSLOTB bits).
+#ifndef DSORT_BK_HSLOTB
+#define DSORT_BK_HSLOTB BK_SLOTB
+#endif
 template <typename T>
 __global__ void __launch_bounds__(BK_T) bucket_hist_kernel(const T *__restrict__ in, uint64_t n,
                                                            const typename Comp<T>::C *__restrict__ spl_g,
@@ -212,13 +217,14 @@ __global__ void __launch_bounds__(BK_T) bucket_hist_kernel(const T *__restrict__
                                                            uint32_t *__restrict__ counts) {
     using CT = Comp<T>;
     constexpr int KPT = Geo<T>::KPT, SUB = BK_T * KPT;
+    constexpr int HSB = DSORT_BK_HSLOTB;
     __shared__ typename CT::C spl[BK_MAXB];
-    __shared__ uint32_t rng[BK_SLOTS];
+    __shared__ uint32_t rng[1 << HSB];
     __shared__ uint32_t hist[BK_MAXB];
     load_splitters<T>(spl_g, BP, spl);
     for (int b = threadIdx.x; b < B; b += BK_T) hist[b] = 0;
     __syncthreads();
-    build_slots<T>(spl, BP, rng);
+    build_slots<T, HSB>(spl, BP, rng);
     __syncthreads();
     const uint64_t g0 = (uint64_t)blockIdx.x * subs * SUB;
 #pragma unroll 1
@@ -233,7 +239,7 @@ __global__ void __launch_bounds__(BK_T) bucket_hist_kernel(const T *__restrict__
 #pragma unroll
         for (int k = 0; k < KPT; ++k) {
             const uint64_t i = b0 + (uint64_t)k * BK_T;
-            if (i < n) atomicAdd(&hist[bucket_fast<T>(spl, rng, key[k], CT::make(key[k], i))], 1u);
+            if (i < n) atomicAdd(&hist[bucket_fast<T, HSB>(spl, rng, key[k], CT::make(key[k], i))], 1u);
         }
     }
     __syncthreads();
