@@ -63,8 +63,36 @@ def test_bucketed_sort_multi_pass_buckets(gpu_ctx, monkeypatch, tiles, passes):
     assert gpu_ctx.stats()["merge_passes"] == passes
 
 
+@pytest.mark.parametrize("dtype", ["i32", "i64"])
+@pytest.mark.parametrize("fanin", ["per-bucket", "global"])
+@pytest.mark.parametrize("B", [3, 9])
+def test_bucketed_sort_mixed_fanin(gpu_ctx, monkeypatch, dtype, fanin, B):
+    """Buckets whose mean size sits at a power-of-two run count (64 int32 tiles, 256 int64
+    tiles), so the sampling spread puts some buckets above it and some below: a pass mixes
+    per-bucket fan-ins (one launch per kernel fan-in).  DSORT_BUCKET_FANIN=global plans every
+    bucket with the largest bucket's fan-in.  Both must sort exactly (keys: a dense duplicate-heavy
+    cluster plus the full int range)."""
+    import torch
+    monkeypatch.setenv("DSORT_BUCKETS", str(B))
+    if fanin == "global":
+        monkeypatch.setenv("DSORT_BUCKET_FANIN", "global")
+    else:
+        monkeypatch.delenv("DSORT_BUCKET_FANIN", raising=False)
+    rng = np.random.default_rng(B * 7 + len(fanin))
+    n = B * 64 * TILE + 333
+    dense = rng.integers(-1000, 1000, n // 2)
+    tail = rng.integers(INT_MIN, INT_MAX, n - n // 2, endpoint=True)
+    a = rng.permutation(np.concatenate([dense, tail])).astype(np.int32 if dtype == "i32" else np.int64)
+    t = torch.from_numpy(a).cuda()
+    out = torch.empty_like(t)
+    gpu_ctx.sort_dev(t, out)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), np.sort(a))
+    assert gpu_ctx.stats()["merge_passes"] >= 1
+
+
 def test_bucketed_default_at_2p26_matches_regular_path(gpu_ctx, monkeypatch):
-    """Default bucket count at 2^26 (32 buckets) and DSORT_BUCKETS=0 (regular passes): same
+    """Default bucket count at 2^26 (64 buckets) and DSORT_BUCKETS=0 (regular passes): same
     output, no descents, same multiset."""
     import torch
     n = 1 << 26
@@ -74,7 +102,7 @@ def test_bucketed_default_at_2p26_matches_regular_path(gpu_ctx, monkeypatch):
     o1, o2 = torch.empty_like(t), torch.empty_like(t)
     monkeypatch.delenv("DSORT_BUCKETS", raising=False)
     gpu_ctx.sort_dev(t, o1)
-    assert gpu_ctx.stats()["merge_passes"] == 2  # 32 buckets of ~2^21 keys: ~128 runs each
+    assert gpu_ctx.stats()["merge_passes"] == 2  # 64 buckets of ~2^20 keys: ~64 runs each
     monkeypatch.setenv("DSORT_BUCKETS", "0")
     gpu_ctx.sort_dev(t, o2)
     torch.cuda.synchronize()
