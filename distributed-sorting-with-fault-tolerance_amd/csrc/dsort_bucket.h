@@ -157,13 +157,17 @@ __global__ void __launch_bounds__(256) bucket_sample_kernel(const T *__restrict_
 }
 
 // splitter b = sample (b+1)*os - 1 of the sorted samples (os samples per bucket), b < B-1;
-// +inf up to BP
+// +inf up to BP.  With k > 0 the first k buckets take kos samples each and the rest los each
+// (skewed bucket sizes, see bucket_skew in dsort_wave.hip).
 template <typename T>
 __global__ void __launch_bounds__(BK_MAXB) bucket_splitter_kernel(const typename Comp<T>::C *__restrict__ smp,
                                                                  int B, int BP, int os,
-                                                                 typename Comp<T>::C *__restrict__ spl) {
+                                                                 typename Comp<T>::C *__restrict__ spl,
+                                                                 int k = 0, int kos = 0, int los = 0) {
     const int b = threadIdx.x;
-    if (b < BP) spl[b] = b < B - 1 ? smp[(uint64_t)(b + 1) * os - 1] : Comp<T>::inf();
+    const uint64_t idx = k == 0 ? (uint64_t)(b + 1) * os
+                       : b < k ? (uint64_t)(b + 1) * kos : (uint64_t)k * kos + (uint64_t)(b + 1 - k) * los;
+    if (b < BP) spl[b] = b < B - 1 ? smp[idx - 1] : Comp<T>::inf();
 }
 
 template <typename T>

@@ -759,6 +759,28 @@ static int bucket_os() {
     return v < 1 ? 1 : (v > 4096 ? 4096 : v);
 }
 
+// Skewed bucket sizes.  When the mean bucket holds about 64 tiles (2^30 keys in 1024 buckets),
+// about half the buckets land above 64 runs and merge F = 16 then F = 8, the rest F = 8 twice.
+// Instead the first k buckets get 56 tiles' worth of samples (below 64 runs despite the sampling
+// spread) and the others share the rest, about 104 tiles each (below 128): most keys then take
+// the cheaper F = 8 first pass.  Returns k and the samples per small / large bucket;
+// DSORT_BUCKET_SKEW=0 turns it off.
+struct Skew { int k, kos, los; };
+static Skew bucket_skew(uint64_t n, int B, int os) {
+    const char *e = getenv("DSORT_BUCKET_SKEW");
+    if (e && atoi(e) == 0) return Skew{0, 0, 0};
+    const double R = (double)n / ((double)B * TILE);  // mean tiles per bucket
+    if (B < 16 || R <= 56.0 || R > 72.0) return Skew{0, 0, 0};
+    const double small = 56.0, large = 104.0;
+    const int k = (int)((double)B * (large - R) / (large - small));
+    if (k <= 0 || k >= B) return Skew{0, 0, 0};
+    const int kos = (int)((double)os * small / R);
+    const uint64_t S = (uint64_t)B * os, rem = S - (uint64_t)k * kos;
+    const int los = (int)((rem + (B - k) - 1) / (uint64_t)(B - k));  // the last bucket gets less
+    if (kos < 1 || los < kos || (uint64_t)k * kos + (uint64_t)(B - 1 - k) * los >= S) return Skew{0, 0, 0};
+    return Skew{k, kos, los};
+}
+
 // Group tables of the merge passes inside buckets: pass p merges groups of up to 16
 // consecutive runs of one bucket; a bucket with a single run left is carried as a 1-run group.
 struct BucketPass {
@@ -824,7 +846,9 @@ static int bucket_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys,
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[0], s));
         ctx->ev_mask |= 1u;
     }
-    hipLaunchKernelGGL(bucket_splitter_kernel<int32_t>, dim3(1), dim3(BK_MAXB), 0, s, smp, B, BP, os, spl);
+    const Skew sk = bucket_skew(n, B, os);
+    hipLaunchKernelGGL(bucket_splitter_kernel<int32_t>, dim3(1), dim3(BK_MAXB), 0, s, smp, B, BP, os, spl,
+                       sk.k, sk.kos, sk.los);
     // 2. histograms, their scan, the scatter
     hipLaunchKernelGGL(bucket_hist_kernel<int32_t>, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, B, BP, subs, cnt);
     hipLaunchKernelGGL(bucket_colsum_kernel, dim3((unsigned)nchunk), dim3(BK_MAXB), 0, s, cnt, (uint32_t)G, B, part);
