@@ -771,7 +771,12 @@ static Skew bucket_skew(uint64_t n, int B, int os) {
     if (e && atoi(e) == 0) return Skew{0, 0, 0};
     const double R = (double)n / ((double)B * TILE);  // mean tiles per bucket
     if (B < 16 || R <= 56.0 || R > 72.0) return Skew{0, 0, 0};
-    const double small = 56.0, large = 104.0;
+    double small = 56.0, large = 104.0;  // DSORT_BUCKET_SKEW=<small>:<large> overrides (experiments)
+    if (e && strchr(e, ':')) {
+        small = atof(e);
+        large = atof(strchr(e, ':') + 1);
+        if (!(small > 0 && large > small)) return Skew{0, 0, 0};
+    }
     const int k = (int)((double)B * (large - R) / (large - small));
     if (k <= 0 || k >= B) return Skew{0, 0, 0};
     const int kos = (int)((double)os * small / R);
