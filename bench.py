@@ -1,28 +1,39 @@
 #!/usr/bin/env python3
-"""Benchmark of the MI355X sort path (BASELINE.json metric: sorted keys/sec, int32, 2^30 keys).
+"""Benchmark of the MI355X sort path (BASELINE.json metric: sorted keys/sec, int32, 2^30 keys,
+at 1/2/4/8 GPUs, with the HBM / xGMI roofline fraction).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--keys N_TOTAL] [--dtype i32|i64]
-                    [--dist uniform|zipf] [--no-cpu-baseline]
+                    [--dist uniform|zipf] [--path single|samplesort] [--no-cpu-baseline]
 
-One step = one full sort of the synthetic batch with the input already resident in HBM:
-  N = 1: dsort_sort_dev_copy (tile sort + merge-path passes) of all keys on one GPU.
-  N > 1: launched by torch.distributed.run, one process per GPU; every rank holds an equal
-         contiguous chunk (server.c:185-216 partitioning) and the step is the sample sort
-         (local sort + splitters + RCCL all-to-all over xGMI + merge of the received runs).
-         The total key count stays fixed (strong scaling), as the metric is quoted on 2^30 keys.
-The sorted output is verified outside the timed region (ascending + multiset fingerprint).
+One step = one full sort of the synthetic batch, input already resident in HBM:
+  single      (default at N = 1) dsort_sort_dev_copy: partition, tile sort and merge-path passes
+              of all keys on one GPU;
+  samplesort  (default at N > 1; --path samplesort forces it at N = 1) one process per GPU, every
+              rank holding an equal contiguous chunk (server.c:185-216), the step being the sample
+              sort: local sort + splitters + RCCL all-to-all over xGMI + merge of the received runs
+              (replaces the gather at server.c:414-415).  The total key count stays fixed (strong
+              scaling: the metric is quoted on 2^30 keys); --keys 2**32 is config C3.
+Ranks: `python bench.py --gpus N` spawns the N rank processes itself (subprocess, before any GPU
+call, rendezvous on 127.0.0.1); under torch.distributed.run it is one of them.  --gpus must equal
+the number of rank processes, and N GPUs must be visible.
+The sorted output is verified outside the timed region (ascending + multiset fingerprint + rank
+boundaries).
 
-Prints ONE JSON line on rank 0 (contract in the task statement) with two extra objects:
-  roofline      live HIP-event timing of the dominant kernel (the merge-path merge kernel) and
-                its algorithmic bytes (2*w bytes per key per launch) against 8 TB/s;
+Rank 0 prints ONE JSON line with two extra objects:
+  roofline      live HIP-event timing of the dominant kernel (the merge-path merge pass; at N > 1
+                the local sort's, slowest rank) against 8 TB/s, and at N > 1 the key exchange's
+                bytes over xGMI against (N-1) links x 153 GB/s;
   cpu_baseline  the reference's own algorithm (client.c merge_sort on 4 threads + server.c
                 merge_chunks, compiled from the reference sources into oracle/_ref) on a bounded
-                sample, timed on this host's cores.
+                sample, plus the reference's TCP server + 4 clients on input.txt (config C1),
+                timed on this host's cores.
 """
 import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import tempfile
 import threading
@@ -34,47 +45,194 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(REPO, "distributed-sorting-with-fault-tolerance_amd")
 sys.path.insert(0, PKG)
 
-import torch  # noqa: E402  (before dsort: one HIP runtime)
-import dsort  # noqa: E402
-
 SEED = 0x5EED2026
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+XGMI_LINK_GBS = 153.0   # one xGMI link (7 per MI355X, one to every peer of an 8-GPU node)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--keys", type=lambda s: int(eval(s, {}, {})), default=1 << 30,
-                    help="total keys (e.g. 2**30)")
+                    help="total keys over all GPUs (e.g. 2**30)")
     ap.add_argument("--dtype", choices=["i32", "i64"], default="i32")
     ap.add_argument("--dist", choices=["uniform", "zipf"], default="uniform")
+    ap.add_argument("--path", choices=["auto", "single", "samplesort"], default="auto")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-keys", type=lambda s: int(eval(s, {}, {})), default=1 << 25)
+    ap.add_argument("--cpu-sample-keys", type=lambda s: int(eval(s, {}, {})), default=1 << 27)
     ap.add_argument("--kill-rank", type=int, default=None,
                     help="BASELINE config C5: fault-tolerance run (launch WITHOUT torchrun: the master "
                          "spawns one worker per GPU); this worker dies mid-sort")
     ap.add_argument("--kill-after-pass", type=int, default=1,
                     help="the dying worker SIGKILLs itself after this merge pass of its local sort")
+    ap.add_argument("--kill-stage", choices=["sort", "exchange"], default="sort",
+                    help="C5: die in the local sort (after --kill-after-pass) or inside the key exchange")
     ap.add_argument("--reassign", choices=["first-live", "next-live"], default="first-live")
     ap.add_argument("--codec", action="store_true",
                     help="time the GPU text codec (output.txt format + %%d parse) on --keys sorted keys")
-    return ap.parse_args()
+    ap.add_argument("--launcher-selftest", action="store_true", help=argparse.SUPPRESS)
+    return ap.parse_args(argv)
+
+
+# ------------------------------------------------------------------------- rank launcher
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def rank_envs(n, port, base=None):
+    """The environment of each of n rank processes (torch.distributed.run's variables)."""
+    base = dict(os.environ if base is None else base)
+    out = []
+    for r in range(n):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                 HSA_ENABLE_IPC_MODE_LEGACY="0")
+        out.append(e)
+    return out
+
+
+def launch_ranks(n, argv, check_devices=True, timeout_s=1800):
+    """Spawns n copies of this script as ranks 0..n-1 (children, never exec; no GPU call in this
+    process: torch.cuda.device_count() does not initialise the GPU on this image).  Returns the
+    first non-zero exit code, else 0; a failing rank takes the others down."""
+    if check_devices:
+        import torch
+
+        ndev = torch.cuda.device_count()
+        if n > ndev:
+            print(f"bench: --gpus {n} needs {n} visible GPUs (one rank per GPU), found {ndev}",
+                  file=sys.stderr, flush=True)
+            return 2
+    envs = rank_envs(n, free_port())
+    procs = [subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), *argv], env=e) for e in envs]
+    rc, t_end = 0, time.time() + timeout_s
+    try:
+        while any(p.poll() is None for p in procs):
+            bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+            if bad or time.time() > t_end:
+                rc = bad[0] if bad else 124
+                break
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+            p.wait()
+    if rc == 0:
+        rc = next((p.returncode for p in procs if p.returncode), 0)
+    return rc
+
+
+def launcher_selftest():
+    """--launcher-selftest: one line per rank with the plumbing it received (CPU test)."""
+    print(json.dumps({"rank": int(os.environ["RANK"]), "world": int(os.environ["WORLD_SIZE"]),
+                      "local_rank": int(os.environ["LOCAL_RANK"]), "master": os.environ["MASTER_ADDR"],
+                      "port": int(os.environ["MASTER_PORT"])}), flush=True)
 
 
 # ------------------------------------------------------------------------- CPU baseline
-def cpu_baseline(sample_keys):
+def host_info():
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        usable = os.cpu_count()
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": usable}
+
+
+def reference_tcp_c1(reps=5, timeout=60.0):
+    """Config C1 on the reference itself: oracle/_ref/server + 4 oracle/_ref/client processes on
+    127.0.0.1 (server.c:120-157 accepts exactly 4), the reference's input.txt (10 000 keys,
+    tests/golden/ref_input.txt) sorted `reps` times in one session; wall time from the file name
+    on the server's stdin to its "Sorting completed" line (server.c:265-270).  None when the
+    reference build is absent."""
+    ref = os.path.join(REPO, "oracle", "_ref")
+    server, client = os.path.join(ref, "server"), os.path.join(ref, "client")
+    src = os.path.join(REPO, "tests", "golden", "ref_input.txt")
+    if not (os.path.exists(server) and os.path.exists(client) and os.path.exists(src)):
+        return None
+    with tempfile.TemporaryDirectory() as d:
+        port = free_port()
+        with open(os.path.join(d, "server.conf"), "w") as f:
+            f.write(f"SERVER_PORT={port}\n")
+        with open(os.path.join(d, "client.conf"), "w") as f:
+            f.write(f"SERVER_IP=127.0.0.1\nSERVER_PORT={port}\n")
+        with open(src, "rb") as fi, open(os.path.join(d, "input.txt"), "wb") as fo:
+            fo.write(fi.read())
+        srv = subprocess.Popen([server, "server.conf"], cwd=d, stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                               stderr=subprocess.STDOUT, bufsize=0)
+        clients = []
+        try:
+            lines = []
+
+            def reader():
+                for raw in iter(srv.stdout.readline, b""):
+                    lines.append((time.perf_counter(), raw))
+
+            th = threading.Thread(target=reader, daemon=True)
+            th.start()
+            t0 = time.time()
+            while not any(b"waiting for worker" in ln for _, ln in lines):
+                if time.time() - t0 > timeout or srv.poll() is not None:
+                    return None
+                time.sleep(0.01)
+            for _ in range(4):
+                clients.append(subprocess.Popen([client, "client.conf"], cwd=d, stdout=subprocess.DEVNULL,
+                                                stderr=subprocess.DEVNULL))
+            while sum(b"connected" in ln.lower() for _, ln in lines) < 4:
+                if time.time() - t0 > timeout or srv.poll() is not None:
+                    return None
+                time.sleep(0.01)
+            times = []
+            for _ in range(reps):
+                seen = sum(b"Sorting completed" in ln for _, ln in lines)
+                ts = time.perf_counter()
+                srv.stdin.write(b"input.txt\n")
+                while sum(b"Sorting completed" in ln for _, ln in lines) <= seen:
+                    if time.time() - t0 > timeout or srv.poll() is not None:
+                        return None
+                    time.sleep(0.0005)
+                te = [t for t, ln in lines if b"Sorting completed" in ln][seen]
+                times.append(te - ts)
+            srv.stdin.write(b"exit\n")
+            ok = open(os.path.join(d, "output.txt"), "rb").read() == \
+                open(os.path.join(REPO, "tests", "golden", "ref_output.txt"), "rb").read()
+        finally:
+            for p in clients + [srv]:
+                if p.poll() is None:
+                    p.kill()
+                p.wait()
+    med = sorted(times)[len(times) // 2]
+    return {"keys": 10000, "files": reps, "first_file_ms": round(1e3 * times[0], 3),
+            "median_file_ms": round(1e3 * med, 3), "keys_per_s_median": 10000 / med,
+            "output_matches_reference_output_txt": ok}
+
+
+def cpu_baseline(sample_keys, target_keys):
     """The reference algorithm on the host: 4 worker threads each run the reference's
     merge_sort (client.c:166) on an equal contiguous chunk (server.c:185-216), then the
     reference's merge_chunks (server.c:481, linear argmin 4-way merge + output.txt text write).
     Uses oracle/_ref (reference compiled from its sources); falls back to the oracle restatement
-    (kind "port") when that build is absent."""
+    (kind "port") when that build is absent.  Also times the reference's TCP path on input.txt
+    (config C1)."""
     ref_dir = os.path.join(REPO, "oracle", "_ref")
     workers = 4
     keys = np.empty(sample_keys, np.int32)
-    orc_path = os.path.join(REPO, "oracle", "liboracle.so")
-    orc = ctypes.CDLL(orc_path)
+    orc = ctypes.CDLL(os.path.join(REPO, "oracle", "liboracle.so"))
     orc.oracle_gen_uniform_i32.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_void_p]
     orc.oracle_gen_uniform_i32(SEED, 0, sample_keys, keys.ctypes.data)
     sz = [sample_keys // workers + (1 if i < sample_keys % workers else 0) for i in range(workers)]
@@ -126,31 +284,47 @@ def cpu_baseline(sample_keys):
         finally:
             os.chdir(cwd)
     ok = all(np.all(c[:-1] <= c[1:]) for c in chunks)
+    # merge_sort is n log n per chunk, merge_chunks linear: the sample's time scaled to the metric size
+    import math
+    scale_sort = (target_keys / sample_keys) * math.log2(target_keys / workers) / math.log2(sample_keys / workers)
+    est = (t1 - t0) * scale_sort + (t2 - t1) * target_keys / sample_keys
+    hi = host_info()
     return {
         "value": sample_keys / (t2 - t0), "unit": "sorted keys/s", "cores": workers, "kind": kind,
         "sample": (f"{sample_keys} uniform int32 keys (seed {SEED:#x}); 4 threads x reference merge_sort "
                    f"on equal chunks ({t1 - t0:.2f} s) + reference merge_chunks incl. output.txt "
-                   f"text write ({t2 - t1:.2f} s); host nproc={os.cpu_count()}; chunks sorted={ok}"),
+                   f"text write ({t2 - t1:.2f} s); chunks sorted={ok}; host {hi['cpu_model']}, "
+                   f"nproc={hi['nproc']}, usable={hi['affinity_cpus']}"),
+        "host": hi,
+        "scaled_to_metric": {"keys": target_keys, "est_seconds": round(est, 2),
+                             "est_keys_per_s": target_keys / est,
+                             "rule": "sort time x (N/n) x log2(N/4)/log2(n/4) + merge time x N/n"},
+        "c1_reference_tcp": reference_tcp_c1(),
     }
 
 
 def pmc_traffic(kernel, n, w):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
-    (profiles/r1_pmc_traffic.json: FETCH_SIZE x2 + WRITE_SIZE, see its calibration note), scaled
-    to this run's key count; None when the file is absent or was measured on another key width."""
-    path = os.path.join(REPO, "profiles", "r1_pmc_traffic.json")
-    try:
-        with open(path) as f:
-            rec = json.load(f)["kernels"][kernel]
-    except (OSError, KeyError, ValueError):
-        return None
-    if w != 4:
-        return None
-    return round(rec.get("traffic_bytes_per_pass", rec["traffic_bytes"]) * n / (1 << 30))
+    """HBM bytes per merge pass from the newest committed rocprofv3 PMC passes (FETCH_SIZE x2 +
+    WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md), scaled to this run's key count;
+    None when absent or measured on another key width."""
+    for name in ("r2_pmc_traffic.json", "r1_pmc_traffic.json"):
+        path = os.path.join(REPO, "profiles", name)
+        try:
+            with open(path) as f:
+                doc = json.load(f)
+            rec = doc["kernels"][kernel]
+        except (OSError, KeyError, ValueError):
+            continue
+        if w != doc.get("key_bytes", 4):
+            return None
+        return round(rec.get("traffic_bytes_per_pass", rec["traffic_bytes"]) * n / doc.get("keys", 1 << 30))
+    return None
 
 
 # ------------------------------------------------------------------------- GPU runs
 def make_input(ctx, n, first, dtype, dist):
+    import torch
+
     tdt = torch.int32 if dtype == "i32" else torch.int64
     t = torch.empty(max(n, 1), dtype=tdt, device="cuda")[:n]
     if dist == "zipf":
@@ -164,6 +338,10 @@ def make_input(ctx, n, first, dtype, dist):
 
 
 def run_single(args):
+    import torch
+
+    import dsort
+
     ctx = dsort.Context(0)
     n = args.keys
     w = 4 if args.dtype == "i32" else 8
@@ -180,7 +358,7 @@ def run_single(args):
     if not ok:
         raise SystemExit("bench: sorted output failed verification")
     torch.cuda.synchronize()
-    kms, klaunch, bms, tot = 0.0, 0, 0.0, 0.0
+    kms, klaunch, bms, tot, npass = 0.0, 0, 0.0, 0.0, 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         ctx.sort_dev(t_in, out)
@@ -189,24 +367,26 @@ def run_single(args):
         klaunch += st["merge_kernel_launches"]
         bms += st["block_sort_ms"]
         tot += st["total_ms"]
+        npass += st["merge_passes"]
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    elapsed = t1 - t0
     stats = ctx.stats()
     ctx.close()
-    return elapsed, {"kernel_ms": kms, "launches": klaunch, "block_ms": bms, "device_ms": tot,
-                     "passes": stats["merge_passes"], "tile": stats["tile_keys"], "w": w, "n_gpu": n}
+    return t1 - t0, {"kernel_ms": kms, "launches": klaunch, "block_ms": bms, "device_ms": tot,
+                     "passes": stats["merge_passes"], "npass": npass, "tile": stats["tile_keys"], "w": w}
 
 
-def run_multi(args):
-    """One rank per GPU (torch.distributed.run): gloo for control, RCCL (inside libdsort) for
-    the key exchange.  Strong scaling: the 2^30 keys are split into equal contiguous chunks."""
+def run_multi(args, rank, world):
+    """One rank per GPU: gloo for control, RCCL (inside libdsort) for the key exchange.  Strong
+    scaling: the --keys total is split into equal contiguous chunks (server.c:185-216)."""
+    import torch
     import torch.distributed as dist
-    rank = int(os.environ["RANK"])
-    world = int(os.environ["WORLD_SIZE"])
+
+    import dsort
+
     local = int(os.environ.get("LOCAL_RANK", rank))
     torch.cuda.set_device(local)
-    dist.init_process_group("gloo")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
     ctx = dsort.Context(local)
     uid = [dsort.Context.unique_id() if rank == 0 else None]
     dist.broadcast_object_list(uid, src=0)
@@ -241,17 +421,28 @@ def run_multi(args):
     torch.cuda.synchronize()
     dist.barrier()
     t0 = time.perf_counter()
-    ex, fm = 0.0, 0.0
+    acc = {"exchange_ms": 0.0, "alltoall_ms": 0.0, "final_merge_ms": 0.0, "merge_kernel_ms": 0.0,
+           "merge_kernel_launches": 0, "merge_passes": 0, "sent": 0}
     for _ in range(args.steps):
         ptr, nout = ctx.sample_sort_dev(t_in)
         st = ctx.stats()  # synchronizes this rank's stream
-        ex += st["exchange_ms"]
-        fm += st["final_merge_ms"]
+        for k in ("exchange_ms", "alltoall_ms", "final_merge_ms", "merge_kernel_ms"):
+            acc[k] += st[k]
+        acc["merge_kernel_launches"] += st["merge_kernel_launches"]
+        acc["merge_passes"] += st["merge_passes"]
+        acc["sent"] += st["keys_sent"]
     torch.cuda.synchronize()
     dist.barrier()
     t1 = time.perf_counter()
     el = torch.tensor([t1 - t0], dtype=torch.float64)
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    # per-rank figures of the roofline, gathered (rank 0 reports the slowest rank)
+    steps = max(args.steps, 1)
+    per_pass = acc["merge_kernel_ms"] / acc["merge_passes"] if acc["merge_passes"] else 0.0
+    mine = torch.tensor([per_pass, acc["alltoall_ms"] / steps, acc["exchange_ms"] / steps,
+                         acc["final_merge_ms"] / steps, acc["sent"] / steps, sz], dtype=torch.float64)
+    everyone = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(everyone, mine)
     A = torch.stack(allinfo)
     ok = bool((A[:, 0] == 0).all()) and int(A[:, 1].sum()) == n
     ok &= sum(f[0] for f in fps) & M == sum(f[2] for f in fps) & M
@@ -263,32 +454,104 @@ def run_multi(args):
     for r in range(world - 1):
         if A[r, 1] > 0 and A[r + 1, 1] > 0:
             ok &= bool(A[r, 3] <= A[r + 1, 2])
-    # the local sort's merge-pass kernel on this rank's chunk (HIP events per launch), outside the
-    # timed region: the roofline line of the multi-GPU run
-    t_loc = torch.empty_like(t_in)
-    ctx.sort_dev(t_in, t_loc)
-    lst = ctx.stats()
-    del t_loc
     ctx.comm_destroy()
     ctx.close()
-    return rank, world, float(el.item()), ok, {"exchange_ms": ex, "final_merge_ms": fm, "w": w,
-                                                "n_gpu": sz, "local_kernel_ms": lst["merge_kernel_ms"],
-                                                "local_launches": lst["merge_kernel_launches"],
-                                                "local_passes": lst["merge_passes"]}
+    dist.barrier()
+    dist.destroy_process_group()
+    return float(el.item()), ok, torch.stack(everyone).numpy(), w
+
+
+def result_header(args, world):
+    metric = "sorted keys/sec (int32, 2^30 keys)" if args.dtype == "i32" else "sorted keys/sec (int64)"
+    return {"metric": metric, "unit": "keys/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "int32" if args.dtype == "i32" else "int64",
+            "data": f"synthetic {args.dist} keys, splitmix64(seed={SEED:#x} + global index)"}
+
+
+def report_single(args, elapsed, k):
+    result = result_header(args, 1)
+    n = args.keys
+    step_ms = 1000.0 * elapsed / args.steps
+    result.update({"value": n * args.steps / elapsed, "ms_per_step": step_ms})
+    # one merge pass = one read + one write of every key; a pass of the bucketed sort is one
+    # launch per kernel fan-in among its buckets, so time is summed per pass
+    npass = k["npass"]
+    avg_pass_ms = k["kernel_ms"] / max(npass, 1)
+    bytes_per_pass = 2 * k["w"] * n
+    achieved = bytes_per_pass / (avg_pass_ms * 1e-3) / 1e9 if k["launches"] and npass else 0.0
+    cfg = "C2-style" if args.dtype == "i32" else "C4-style"
+    result["config"] = {"workload": f"{cfg} single-GPU sort of {n} {args.dist} {result['dtype']} keys "
+                                    f"(BASELINE metric size); tile {k['tile']} keys, {k['passes']} merge passes",
+                        "keys": n, "parallelism": "1 GPU"}
+    result["roofline"] = {
+        "bound": "hbm", "kernel": "mergew_kernel (k-way merge-path pass)", "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": pmc_traffic("mergew_kernel", n, k["w"]), "avg_pass_ms": round(avg_pass_ms, 4),
+        "algorithmic_bytes_per_pass": bytes_per_pass,
+        "launches_per_pass": round(k["launches"] / max(npass, 1), 2),
+        "partition_and_tile_sort_ms": round(k["block_ms"] / args.steps, 3),
+        "whole_sort_single_pass_bound_frac": round(2 * k["w"] * n / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+    }
+    if not args.no_cpu_baseline and args.dtype == "i32":
+        result["cpu_baseline"] = cpu_baseline(args.cpu_sample_keys, n)
+    print(json.dumps(result), flush=True)
+
+
+def report_multi(args, world, elapsed, per_rank, w):
+    result = result_header(args, world)
+    n = args.keys
+    step_ms = 1000.0 * elapsed / args.steps
+    result.update({"value": n * args.steps / elapsed, "ms_per_step": step_ms})
+    result["config"] = {"workload": f"sample sort of {n} {args.dist} {result['dtype']} keys over {world} GPUs "
+                                    "(equal contiguous chunks, splitters, RCCL all-to-all over xGMI, merge)",
+                        "keys": n, "keys_per_gpu": n // world, "parallelism": f"samplesort x{world}"}
+    slow = int(np.argmax(per_rank[:, 0]))
+    pass_ms = float(per_rank[slow, 0])
+    n_gpu = float(per_rank[slow, 5])
+    bpl = 2 * w * n_gpu  # one read + one write of the rank's chunk per merge pass
+    ach = bpl / (pass_ms * 1e-3) / 1e9 if pass_ms > 0 else None
+    roof = {"bound": "hbm", "kernel": "mergew_kernel (local-sort merge pass, slowest rank)",
+            "achieved": round(ach, 1) if ach else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None,
+            "traffic": pmc_traffic("mergew_kernel", int(n_gpu), w), "avg_pass_ms": round(pass_ms, 4),
+            "algorithmic_bytes_per_pass": int(bpl),
+            "whole_sort_single_pass_bound_frac": round(
+                2 * w * n / (step_ms * 1e-3) / 1e9 / (HBM_PEAK_GBS * world), 4)}
+    if world > 1:
+        # the all-to-all: every GPU ships w * N_g * (P-1)/P bytes to its P-1 peers, one xGMI link
+        # each; the slowest rank's transfer time against (P-1) links x 153 GB/s
+        sent = per_rank[:, 4] * w
+        a2a = per_rank[:, 1]
+        r = int(np.argmax(a2a))
+        xg = sent[r] / (a2a[r] * 1e-3) / 1e9 if a2a[r] > 0 else None
+        peak = (world - 1) * XGMI_LINK_GBS
+        roof["xgmi"] = {"achieved": round(xg, 1) if xg else None, "peak": peak, "unit": "GB/s",
+                        "frac": round(xg / peak, 4) if xg else None,
+                        "algorithmic_bytes_per_gpu": int(w * (n // world) * (world - 1) / world),
+                        "measured_bytes_slowest_rank": int(sent[r]),
+                        "alltoall_ms": round(float(a2a[r]), 4),
+                        "exchange_stage_ms": round(float(per_rank[:, 2].max()), 4),
+                        "final_merge_ms": round(float(per_rank[:, 3].max()), 4)}
+    result["roofline"] = roof
+    print(json.dumps(result), flush=True)
 
 
 def run_fault(args):
-    """BASELINE config C5 through ftsort.Master (server.c's role): a fault-free run, then a run in
-    which worker `--kill-rank` dies after merge pass `--kill-after-pass` of its local sort; the
-    survivors detect it, rebuild the communicator and sort the dead chunk from its replica."""
+    """BASELINE config C5 through the C master (dsort_master --mode samplesort, server.c's role,
+    driven by ftsort.fault_run): a fault-free run, then a run in which worker `--kill-rank` dies in
+    its local sort (after merge pass --kill-after-pass) or inside the key exchange; the master
+    sees it (socket EOF / exit / heartbeat), reassigns its chunk from the pinned replica by the
+    reference's rule, and the survivors abort the communicator, rebuild it and finish."""
     import ftsort
 
-    ndev = torch.cuda.device_count()
-    share = args.gpus > ndev  # one GPU box: the workers share it and exchange through gloo
-    devices = [0] * args.gpus if share else list(range(args.gpus))
-    transport = "host" if share or args.gpus == 1 else "rccl"
+    ndev = _device_count()
+    share = args.gpus > ndev  # one GPU box: the workers share it and exchange through the master
+    devices = "share" if share else list(range(args.gpus))
+    transport = "relay" if share else "rccl"
     r = ftsort.fault_run(args.gpus, args.keys, args.kill_rank, args.kill_after_pass,
-                         "i32" if args.dtype == "i32" else "i64", args.dist, transport, devices, args.reassign)
+                         "i32" if args.dtype == "i32" else "i64", args.dist, transport, devices, args.reassign,
+                         stage=args.kill_stage)
     if not r["ok"]:
         raise SystemExit(f"bench: fault run failed verification: {json.dumps(r)}")
     free, fault = r["fault_free"], r["fault"]
@@ -296,15 +559,22 @@ def run_fault(args):
            "value": round(r["recovery_ms"], 3), "unit": "ms", "n_gpus": args.gpus, "higher_is_better": False,
            "dtype": "int32" if args.dtype == "i32" else "int64", "data": f"synthetic {args.dist} keys",
            "config": {"workload": f"sample sort of {args.keys} keys over {args.gpus} workers, worker "
-                                  f"{args.kill_rank} killed after merge pass {args.kill_after_pass}",
+                                  f"{args.kill_rank} killed in the {args.kill_stage} stage",
                       "transport": transport, "reassign": args.reassign, "devices": devices},
            "fault_free_ms": round(free["t_end_ms"], 3), "fault_ms": round(fault["t_end_ms"], 3),
            "fault_free_keys_per_s": args.keys / (free["t_end_ms"] * 1e-3),
            "fault_keys_per_s": args.keys / (fault["t_end_ms"] * 1e-3),
            "fault_seen_by_master_ms": fault["t_fault_seen_ms"],
            "survivors_notified_ms": fault["t_survivors_notified_ms"],
-           "plan": fault["plan"], "slices": fault["slices"], "verified": True}
+           "rebuild_ms": fault["t_rebuild_ms"], "owners": fault["owners"], "slices": fault["slices"],
+           "verified": True}
     print(json.dumps(out), flush=True)
+
+
+def _device_count():
+    import torch
+
+    return torch.cuda.device_count()  # does not initialise the GPU on this image
 
 
 def run_codec(args):
@@ -312,6 +582,10 @@ def run_codec(args):
     keys to output.txt bytes (server.c:517-519) and parses them back (server.c:179/213's %d
     tokens), each timed over `--steps` calls with the data resident in HBM; verifies the round
     trip.  The CPU leg times the oracle's single-threaded codec on a 2^24-key sample."""
+    import torch
+
+    import dsort
+
     ctx = dsort.Context(0)
     n = args.keys
     keys = make_input(ctx, n, 0, "i32", "uniform")
@@ -375,78 +649,41 @@ def run_codec(args):
     ctx.close()
 
 
-def main():
-    args = parse()
-    if args.codec:
-        run_codec(args)
-        return
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
     if args.kill_rank is not None:
         if "WORLD_SIZE" in os.environ:
             raise SystemExit("--kill-rank runs its own master and workers: launch it without torchrun")
         run_fault(args)
-        return
+        return 0
+    if args.codec:
+        run_codec(args)
+        return 0
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args.gpus, argv, check_devices=not args.launcher_selftest)
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if args.gpus != world and world != 1:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    metric = "sorted keys/sec (int32, 2^30 keys)" if args.dtype == "i32" else "sorted keys/sec (int64)"
-    result = {"metric": metric, "unit": "keys/s", "n_gpus": args.gpus, "steps": args.steps,
-              "warmup": args.warmup, "higher_is_better": True, "scaling": "strong",
-              "vs_baseline": None, "dtype": "int32" if args.dtype == "i32" else "int64",
-              "data": f"synthetic {args.dist} keys, splitmix64(seed={SEED:#x} + global index)"}
-    if world == 1 and args.gpus == 1:
+    rank = int(os.environ.get("RANK", "0"))
+    if args.launcher_selftest:
+        launcher_selftest()
+        return 0
+    if args.gpus != world:
+        raise SystemExit(f"bench: --gpus {args.gpus} but {world} rank process(es) (WORLD_SIZE); "
+                         "they must match (one rank per GPU)")
+    path = args.path if args.path != "auto" else ("single" if world == 1 else "samplesort")
+    if path == "single":
+        if world != 1:
+            raise SystemExit("bench: --path single runs on one GPU")
         elapsed, k = run_single(args)
-        n = args.keys
-        step_ms = 1000.0 * elapsed / args.steps
-        result.update({"value": n * args.steps / elapsed, "ms_per_step": step_ms})
-        # one merge pass = one read + one write of every key; a pass of the bucketed int32 sort
-        # is one launch per kernel fan-in among its buckets, so time is summed per pass
-        npass = k["passes"] * args.steps
-        avg_launch_ms = k["kernel_ms"] / max(npass, 1)
-        bytes_per_launch = 2 * k["w"] * n
-        achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if k["launches"] and npass else 0.0
-        cfg = "C2-style" if args.dtype == "i32" else "C4-style"
-        result["config"] = {"workload": f"{cfg} single-GPU sort of {n} {args.dist} {result['dtype']} keys "
-                                        f"(BASELINE metric size); tile {k['tile']} keys, {k['passes']} merge passes",
-                            "keys": n, "parallelism": "1 GPU"}
-        result["roofline"] = {
-            "bound": "hbm", "kernel": "mergew_kernel (k-way merge pass)" if args.dtype == "i32"
-            else "mergek_kernel (k-way merge pass, LDS merge path)", "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": pmc_traffic("mergew_kernel", n, k["w"]), "avg_pass_ms": round(avg_launch_ms, 4),
-            "algorithmic_bytes_per_pass": bytes_per_launch,
-            "launches_per_pass": round(k["launches"] / max(npass, 1), 2),
-            "partition_and_tile_sort_ms": round(k["block_ms"] / args.steps, 3),
-            "whole_sort_single_pass_bound_frac": round(2 * k["w"] * n / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-        }
-        if not args.no_cpu_baseline and args.dtype == "i32":
-            result["cpu_baseline"] = cpu_baseline(args.cpu_sample_keys)
-        print(json.dumps(result), flush=True)
-    else:
-        rank, world, elapsed, ok, k = run_multi(args)
-        if rank == 0:
-            if not ok:
-                raise SystemExit("bench: distributed output failed verification")
-            n = args.keys
-            step_ms = 1000.0 * elapsed / args.steps
-            result.update({"value": n * args.steps / elapsed, "ms_per_step": step_ms})
-            result["config"] = {"workload": f"sample sort of {n} {args.dist} {result['dtype']} keys over {world} GPUs "
-                                            "(equal chunks, RCCL all-to-all)", "keys": n,
-                                "parallelism": f"sample-sort x{world}"}
-            nl = k["local_passes"] if k["local_launches"] else 0  # launches of one pass are summed
-            avg = k["local_kernel_ms"] / nl if nl else 0.0
-            bpl = 2 * k["w"] * k["n_gpu"]  # one read + one write of the rank's chunk per launch
-            ach = bpl / (avg * 1e-3) / 1e9 if nl and avg > 0 else None
-            result["roofline"] = {"bound": "hbm", "kernel": "mergew_kernel (rank 0 local sort, per GPU)",
-                                  "achieved": round(ach, 1) if ach else None, "peak": HBM_PEAK_GBS,
-                                  "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None,
-                                  "traffic": pmc_traffic("mergew_kernel", k["n_gpu"], k["w"]),
-                                  "avg_pass_ms": round(avg, 4), "algorithmic_bytes_per_pass": bpl,
-                                  "rank0_exchange_ms": round(k["exchange_ms"] / args.steps, 3),
-                                  "rank0_final_merge_ms": round(k["final_merge_ms"] / args.steps, 3),
-                                  "whole_sort_single_pass_bound_frac": round(
-                                      2 * k["w"] * n / (step_ms * 1e-3) / 1e9 / (HBM_PEAK_GBS * world), 4)}
-            print(json.dumps(result), flush=True)
+        report_single(args, elapsed, k)
+        return 0
+    elapsed, ok, per_rank, w = run_multi(args, rank, world)
+    if rank == 0:
+        if not ok:
+            raise SystemExit("bench: distributed output failed verification")
+        report_multi(args, world, elapsed, per_rank, w)
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -4,12 +4,16 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <signal.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
+#include <time.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cmath>
+#include <mutex>
 #include <new>
 #include <string>
 #include <vector>
@@ -336,21 +340,84 @@ template <typename T> static ncclDataType_t nccl_type();
 template <> ncclDataType_t nccl_type<int32_t>() { return ncclInt32; }
 template <> ncclDataType_t nccl_type<int64_t>() { return ncclInt64; }
 
-#define DSORT_NCCL(ctx, call)                                                             \
+
+static double now_ms() {
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+}
+
+// The communicator mutex: held by a running exchange; dsort_comm_abort from another thread finds
+// it taken and only raises ctx->abort_req (see dsort.h).
+static std::mutex &comm_mutex(dsort_ctx *ctx) {
+    static std::mutex table[64];
+    return table[(reinterpret_cast<uintptr_t>(ctx) >> 6) & 63];
+}
+
+static void abort_comm_locked(dsort_ctx *ctx) {
+    if (ctx->comm) ncclCommAbort(ctx->comm);
+    ctx->comm = nullptr;
+    ctx->has_transport = false;
+    ctx->nranks = 1;
+    ctx->rank = 0;
+}
+
+// Every wait of an exchange: polls the stream, RCCL's asynchronous error (non-blocking
+// communicator), the abort flag and the deadline, and aborts the communicator on a failure,
+// instead of a hipStreamSynchronize that a dead peer would block forever.
+static int exch_wait(dsort_ctx *ctx, hipStream_t s, bool with_stream, double deadline, const char *what) {
+    for (;;) {
+        const hipError_t q = with_stream ? hipStreamQuery(s) : hipSuccess;
+        ncclResult_t ae = ncclSuccess;
+        if (ctx->comm) ncclCommGetAsyncError(ctx->comm, &ae);
+        if (q == hipSuccess && ae != ncclInProgress && (ae == ncclSuccess || !ctx->comm)) return DSORT_OK;
+        if (q != hipSuccess && q != hipErrorNotReady) return hip_err(ctx, q, what);
+        if (ae != ncclSuccess && ae != ncclInProgress) {
+            abort_comm_locked(ctx);
+            return set_err(ctx, DSORT_ECOMM, std::string(what) + ": RCCL error " + ncclGetErrorString(ae) +
+                                                 " (a peer failed); communicator aborted");
+        }
+        if (ctx->abort_req.load()) {
+            abort_comm_locked(ctx);
+            return set_err(ctx, DSORT_ECOMM, std::string(what) + ": aborted by dsort_comm_abort");
+        }
+        if (deadline > 0 && now_ms() > deadline) {
+            abort_comm_locked(ctx);
+            return set_err(ctx, DSORT_ETIMEOUT, std::string(what) + ": no progress before the deadline "
+                                                    "(DSORT_OPT_COMM_TIMEOUT_MS); communicator aborted");
+        }
+        usleep(20);
+    }
+}
+
+// An RCCL call on the non-blocking communicator: ncclInProgress is success-so-far.
+#define DSORT_NCCLNB(ctx, call)                                                           \
     do {                                                                                  \
         ncclResult_t r_ = (call);                                                         \
-        if (r_ != ncclSuccess)                                                            \
+        if (r_ != ncclSuccess && r_ != ncclInProgress) {                                  \
+            abort_comm_locked(ctx);                                                       \
             return dsort::set_err((ctx), DSORT_ECOMM,                                     \
                                   std::string(#call) + ": " + ncclGetErrorString(r_));    \
+        }                                                                                 \
     } while (0)
+
+static void exchange_fault_point(dsort_ctx *ctx, int stage) {
+    if (ctx->opt.kill_in_exchange == stage) raise(SIGKILL);
+}
 
 template <typename T>
 static int sample_sort(dsort_ctx *ctx, const T *d_in, size_t n_local, T **d_out, size_t *n_out,
                        void *stream, bool presorted) {
     if (!ctx || !d_out || !n_out || (n_local && !d_in)) return set_err(ctx, DSORT_EINVAL, "null argument");
+    std::unique_lock<std::mutex> lock(comm_mutex(ctx));
+    if (ctx->abort_req.load()) {
+        abort_comm_locked(ctx);
+        return set_err(ctx, DSORT_ECOMM, "communicator aborted (dsort_comm_abort)");
+    }
     if (!ctx->comm && !ctx->has_transport)
         return set_err(ctx, DSORT_ECOMM, "communicator not initialised (dsort_comm_init)");
     hipStream_t s = pick(ctx, stream);
+    const double deadline = ctx->opt.comm_timeout_ms > 0 ? now_ms() + (double)ctx->opt.comm_timeout_ms : 0.0;
     const int P = ctx->nranks, me = ctx->rank, S = kSamplesPerRank;
     const bool host_tx = ctx->has_transport;
     int rc;
@@ -407,13 +474,16 @@ static int sample_sort(dsort_ctx *ctx, const T *d_in, size_t n_local, T **d_out,
     DSORT_HIP(ctx, hipMemcpyAsync(dsm + off_cnt, &nl, 8, hipMemcpyHostToDevice, s));
     // 3. all-gather samples and sizes
     if (!host_tx) {
-        DSORT_NCCL(ctx, ncclGroupStart());
-        DSORT_NCCL(ctx, ncclAllGather(dsm + off_samp, dsm + off_all, (size_t)S, nccl_type<T>(), ctx->comm, s));
-        DSORT_NCCL(ctx, ncclAllGather(dsm + off_cnt, dsm + off_n, 1, ncclUint64, ctx->comm, s));
-        DSORT_NCCL(ctx, ncclGroupEnd());
+        DSORT_NCCLNB(ctx, ncclGroupStart());
+        DSORT_NCCLNB(ctx, ncclAllGather(dsm + off_samp, dsm + off_all, (size_t)S, nccl_type<T>(), ctx->comm, s));
+        DSORT_NCCLNB(ctx, ncclAllGather(dsm + off_cnt, dsm + off_n, 1, ncclUint64, ctx->comm, s));
+        DSORT_NCCLNB(ctx, ncclGroupEnd());
+        rc = exch_wait(ctx, s, false, deadline, "sample all-gather (enqueue)");
+        if (rc) return rc;
         DSORT_HIP(ctx, hipMemcpyAsync(hsm + off_all, dsm + off_all, (size_t)P * S * sizeof(T) + (size_t)P * 8,
                                       hipMemcpyDeviceToHost, s));
-        DSORT_HIP(ctx, hipStreamSynchronize(s));
+        rc = exch_wait(ctx, s, true, deadline, "sample all-gather");
+        if (rc) return rc;
     } else {
         // [S samples | n_local] per rank through the caller's all-gather
         const size_t rec = (size_t)S * sizeof(T) + 8;
@@ -421,7 +491,8 @@ static int sample_sort(dsort_ctx *ctx, const T *d_in, size_t n_local, T **d_out,
         if (rc) return rc;
         char *mine = static_cast<char *>(ctx->xfer), *all = mine + rec;
         DSORT_HIP(ctx, hipMemcpyAsync(mine, dsm + off_samp, (size_t)S * sizeof(T), hipMemcpyDeviceToHost, s));
-        DSORT_HIP(ctx, hipStreamSynchronize(s));
+        rc = exch_wait(ctx, s, true, deadline, "local sort");
+        if (rc) return rc;
         memcpy(mine + (size_t)S * sizeof(T), &nl, 8);
         if (ctx->transport.allgather(ctx->transport.user, mine, all, rec))
             return set_err(ctx, DSORT_ECOMM, "host transport allgather (samples) failed");
@@ -430,6 +501,7 @@ static int sample_sort(dsort_ctx *ctx, const T *d_in, size_t n_local, T **d_out,
             memcpy(hsm + off_n + (size_t)r * 8, all + (size_t)r * rec + (size_t)S * sizeof(T), 8);
         }
     }
+    exchange_fault_point(ctx, 1);
     // 4. splitters on the host (tiny: P*S composites)
     {
         const T *hs = reinterpret_cast<const T *>(hsm + off_all);
@@ -451,16 +523,20 @@ static int sample_sort(dsort_ctx *ctx, const T *d_in, size_t n_local, T **d_out,
                        reinterpret_cast<uint64_t *>(dsm + off_cut));
     DSORT_HIP(ctx, hipGetLastError());
     DSORT_HIP(ctx, hipMemcpyAsync(hsm + off_cut, dsm + off_cut, (size_t)(P + 1) * 8, hipMemcpyDeviceToHost, s));
-    DSORT_HIP(ctx, hipStreamSynchronize(s));
+    rc = exch_wait(ctx, s, true, deadline, "cut search");
+    if (rc) return rc;
     const uint64_t *hcut = reinterpret_cast<const uint64_t *>(hsm + off_cut);
     uint64_t *hcnt = reinterpret_cast<uint64_t *>(hsm + off_cnt);
     for (int r = 0; r < P; ++r) hcnt[r] = hcut[r + 1] - hcut[r];
     // 6. count matrix
     if (!host_tx) {
         DSORT_HIP(ctx, hipMemcpyAsync(dsm + off_cnt, hcnt, (size_t)P * 8, hipMemcpyHostToDevice, s));
-        DSORT_NCCL(ctx, ncclAllGather(dsm + off_cnt, dsm + off_mat, (size_t)P, ncclUint64, ctx->comm, s));
+        DSORT_NCCLNB(ctx, ncclAllGather(dsm + off_cnt, dsm + off_mat, (size_t)P, ncclUint64, ctx->comm, s));
+        rc = exch_wait(ctx, s, false, deadline, "count all-gather (enqueue)");
+        if (rc) return rc;
         DSORT_HIP(ctx, hipMemcpyAsync(hsm + off_mat, dsm + off_mat, (size_t)P * P * 8, hipMemcpyDeviceToHost, s));
-        DSORT_HIP(ctx, hipStreamSynchronize(s));
+        rc = exch_wait(ctx, s, true, deadline, "count all-gather");
+        if (rc) return rc;
     } else if (ctx->transport.allgather(ctx->transport.user, hcnt, hsm + off_mat, (size_t)P * 8)) {
         return set_err(ctx, DSORT_ECOMM, "host transport allgather (counts) failed");
     }
@@ -477,15 +553,28 @@ static int sample_sort(dsort_ctx *ctx, const T *d_in, size_t n_local, T **d_out,
     rc = ensure(ctx, &ctx->recv2, &ctx->recv2_bytes, (nrecv ? nrecv : 1) * sizeof(T), "merge output");
     if (rc) return rc;
     T *rb = static_cast<T *>(ctx->recv);
+    exchange_fault_point(ctx, 2);
+    uint64_t sent = 0;
+    for (int r = 0; r < P; ++r) sent += r == me ? 0 : hcnt[r];
+    if (ctx->ev_ok) {
+        DSORT_HIP(ctx, hipEventRecord(ctx->ev[5], s));
+        ctx->ev_mask |= 32u;
+    }
     // 7. key exchange: one send and one receive per peer link, grouped (RCCL all-to-all-v)
     if (!host_tx) {
-        DSORT_NCCL(ctx, ncclGroupStart());
+        DSORT_NCCLNB(ctx, ncclGroupStart());
         for (int r = 0; r < P; ++r) {
             if (r == me) continue;
-            if (hcnt[r]) DSORT_NCCL(ctx, ncclSend(d_keys + hcut[r], hcnt[r], nccl_type<T>(), r, ctx->comm, s));
-            if (rlen[r]) DSORT_NCCL(ctx, ncclRecv(rb + roff[r], rlen[r], nccl_type<T>(), r, ctx->comm, s));
+            if (hcnt[r]) DSORT_NCCLNB(ctx, ncclSend(d_keys + hcut[r], hcnt[r], nccl_type<T>(), r, ctx->comm, s));
+            if (rlen[r]) DSORT_NCCLNB(ctx, ncclRecv(rb + roff[r], rlen[r], nccl_type<T>(), r, ctx->comm, s));
         }
-        DSORT_NCCL(ctx, ncclGroupEnd());
+        DSORT_NCCLNB(ctx, ncclGroupEnd());
+        rc = exch_wait(ctx, s, false, deadline, "key all-to-all (enqueue)");
+        if (rc) return rc;
+        if (ctx->ev_ok) {
+            DSORT_HIP(ctx, hipEventRecord(ctx->ev[6], s));
+            ctx->ev_mask |= 64u;
+        }
         if (hcnt[me])
             DSORT_HIP(ctx, hipMemcpyAsync(rb + roff[me], d_keys + hcut[me], hcnt[me] * sizeof(T),
                                           hipMemcpyDeviceToDevice, s));
@@ -497,7 +586,8 @@ static int sample_sort(dsort_ctx *ctx, const T *d_in, size_t n_local, T **d_out,
         if (rc) return rc;
         if (n_local)
             DSORT_HIP(ctx, hipMemcpyAsync(ctx->xfer, d_keys, n_local * sizeof(T), hipMemcpyDeviceToHost, s));
-        DSORT_HIP(ctx, hipStreamSynchronize(s));
+        rc = exch_wait(ctx, s, true, deadline, "key staging");
+        if (rc) return rc;
         std::vector<size_t> sc(P), sd(P), rcn(P), rd(P);
         for (int r = 0; r < P; ++r) {
             sc[r] = hcnt[r] * sizeof(T);
@@ -509,23 +599,32 @@ static int sample_sort(dsort_ctx *ctx, const T *d_in, size_t n_local, T **d_out,
                                      rcn.data(), rd.data()))
             return set_err(ctx, DSORT_ECOMM, "host transport alltoallv (keys) failed");
         if (nrecv) DSORT_HIP(ctx, hipMemcpyAsync(rb, ctx->xfer2, nrecv * sizeof(T), hipMemcpyHostToDevice, s));
+        if (ctx->ev_ok) {
+            DSORT_HIP(ctx, hipEventRecord(ctx->ev[6], s));
+            ctx->ev_mask |= 64u;
+        }
     }
     if (ctx->ev_ok) {
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[3], s));
         ctx->ev_mask |= 8u;
     }
-    // 8. merge the P received runs (source-rank order keeps the merge deterministic)
+    // 8. merge the P received runs (source-rank order keeps the merge deterministic); the
+    // local sort's statistics and per-launch events stay
     T *outp = static_cast<T *>(ctx->recv2);
-    rc = merge_device<T>(ctx, rb, rlen.data(), P, outp, s);
+    rc = merge_device<T>(ctx, rb, rlen.data(), P, outp, s, true);
     if (rc) return rc;
+    if (!host_tx) {  // the receives must have landed before the caller reads the slice
+        rc = exch_wait(ctx, s, true, deadline, "key all-to-all");
+        if (rc) return rc;
+    }
     if (ctx->ev_ok) {
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[4], s));
         ctx->ev_mask |= 16u;
     }
     ctx->last_stream = s;
     st.keys_out = nrecv;
+    st.keys_sent = sent;
     ctx->stats = st;
-    ctx->stats.merge_passes = st.merge_passes;
     *d_out = outp;
     *n_out = nrecv;
     return DSORT_OK;
@@ -576,7 +675,7 @@ int dsort_finalize(dsort_ctx *ctx) {
     hipSetDevice(ctx->device);
     if (ctx->stream) hipStreamSynchronize(ctx->stream);
     if (ctx->comm) {
-        ncclCommDestroy(ctx->comm);
+        ncclCommAbort(ctx->comm);  // peers may be gone: never wait for them here
         ctx->comm = nullptr;
     }
     void *bufs[] = {ctx->scratch, ctx->scratch2, ctx->splits, ctx->groups, ctx->io, ctx->io2, ctx->red,
@@ -602,6 +701,63 @@ int dsort_finalize(dsort_ctx *ctx) {
 }
 
 const char *dsort_last_error(const dsort_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int dsort_set_option(dsort_ctx *ctx, int option, int64_t v) {
+    if (!ctx) return DSORT_EINVAL;
+    dsort_opts &o = ctx->opt;
+    switch (option) {
+        case DSORT_OPT_BUCKETS:
+            if (v < -1 || v == 1 || v > 1024) return set_err(ctx, DSORT_EINVAL, "DSORT_OPT_BUCKETS: -1, 0 or 2..1024");
+            o.buckets = v;
+            return DSORT_OK;
+        case DSORT_OPT_BUCKET_KEYS:
+            if (v < 1) return set_err(ctx, DSORT_EINVAL, "DSORT_OPT_BUCKET_KEYS: >= 1");
+            o.bucket_keys = v;
+            return DSORT_OK;
+        case DSORT_OPT_BUCKET_OVERSAMPLE:
+            if (v < 1 || v > 4096) return set_err(ctx, DSORT_EINVAL, "DSORT_OPT_BUCKET_OVERSAMPLE: 1..4096");
+            o.bucket_os = v;
+            return DSORT_OK;
+        case DSORT_OPT_BUCKET_SKEW:
+            if (v != 0 && v != 1) return set_err(ctx, DSORT_EINVAL, "DSORT_OPT_BUCKET_SKEW: 0 or 1");
+            o.bucket_skew = v;
+            return DSORT_OK;
+        case DSORT_OPT_MAX_FANIN_LOG2:
+            if (v != -1 && (v < 1 || v > kMaxLogF)) return set_err(ctx, DSORT_EINVAL, "DSORT_OPT_MAX_FANIN_LOG2: -1 or 1..6");
+            o.max_logf = v;
+            return DSORT_OK;
+        case DSORT_OPT_KILL_AFTER_PASS:
+            if (v < -1) return set_err(ctx, DSORT_EINVAL, "DSORT_OPT_KILL_AFTER_PASS: -1 or a pass index");
+            o.kill_after_pass = v;
+            return DSORT_OK;
+        case DSORT_OPT_KILL_IN_EXCHANGE:
+            if (v != -1 && v != 1 && v != 2) return set_err(ctx, DSORT_EINVAL, "DSORT_OPT_KILL_IN_EXCHANGE: -1, 1 or 2");
+            o.kill_in_exchange = v;
+            return DSORT_OK;
+        case DSORT_OPT_COMM_TIMEOUT_MS:
+            if (v < 0) return set_err(ctx, DSORT_EINVAL, "DSORT_OPT_COMM_TIMEOUT_MS: >= 0");
+            o.comm_timeout_ms = v;
+            return DSORT_OK;
+        default:
+            return set_err(ctx, DSORT_EINVAL, "unknown option " + std::to_string(option));
+    }
+}
+
+int dsort_get_option(const dsort_ctx *ctx, int option, int64_t *v) {
+    if (!ctx || !v) return DSORT_EINVAL;
+    const dsort_opts &o = ctx->opt;
+    switch (option) {
+        case DSORT_OPT_BUCKETS: *v = o.buckets; return DSORT_OK;
+        case DSORT_OPT_BUCKET_KEYS: *v = o.bucket_keys; return DSORT_OK;
+        case DSORT_OPT_BUCKET_OVERSAMPLE: *v = o.bucket_os; return DSORT_OK;
+        case DSORT_OPT_BUCKET_SKEW: *v = o.bucket_skew; return DSORT_OK;
+        case DSORT_OPT_MAX_FANIN_LOG2: *v = o.max_logf; return DSORT_OK;
+        case DSORT_OPT_KILL_AFTER_PASS: *v = o.kill_after_pass; return DSORT_OK;
+        case DSORT_OPT_KILL_IN_EXCHANGE: *v = o.kill_in_exchange; return DSORT_OK;
+        case DSORT_OPT_COMM_TIMEOUT_MS: *v = o.comm_timeout_ms; return DSORT_OK;
+        default: return DSORT_EINVAL;
+    }
+}
 
 int dsort_get_stats(const dsort_ctx *cctx, dsort_stats *out) {
     if (!cctx || !out) return DSORT_EINVAL;
@@ -629,6 +785,7 @@ int dsort_get_stats(const dsort_ctx *cctx, dsort_stats *out) {
         out->exchange_ms = el(2, 3);
         out->final_merge_ms = el(3, 4);
         out->total_ms = el(0, 4);
+        out->alltoall_ms = el(5, 6);
     } else {
         out->total_ms = el(0, 2);
     }
@@ -692,14 +849,36 @@ int dsort_comm_init(dsort_ctx *ctx, int nranks, int rank, const char id[DSORT_UN
     if (!ctx || !id || nranks < 1 || rank < 0 || rank >= nranks) return set_err(ctx, DSORT_EINVAL, "bad argument");
     if (ctx->comm || ctx->has_transport) return set_err(ctx, DSORT_EINVAL, "communicator already initialised");
     DSORT_HIP(ctx, hipSetDevice(ctx->device));
+    std::unique_lock<std::mutex> lock(comm_mutex(ctx));
+    ctx->abort_req.store(0);  // a flag left by the previous communicator's abort
     ncclUniqueId u;
     memcpy(&u, id, sizeof(u));
     ncclComm_t c = nullptr;
-    const ncclResult_t r = ncclCommInitRank(&c, nranks, u, rank);
-    if (r != ncclSuccess)
-        return set_err(ctx, DSORT_ECOMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r) +
+    // non-blocking communicator: no RCCL call may block on a dead peer (exch_wait polls instead)
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    ncclResult_t r = ncclCommInitRankConfig(&c, nranks, u, rank, &cfg);
+    const double deadline = ctx->opt.comm_timeout_ms > 0 ? now_ms() + (double)ctx->opt.comm_timeout_ms : 0.0;
+    while (r == ncclInProgress && c) {
+        ncclCommGetAsyncError(c, &r);
+        if (r != ncclInProgress) break;
+        if (deadline > 0 && now_ms() > deadline) {
+            ncclCommAbort(c);
+            return set_err(ctx, DSORT_ETIMEOUT, "ncclCommInitRankConfig: peers did not join before the deadline");
+        }
+        if (ctx->abort_req.load()) {
+            ncclCommAbort(c);
+            ctx->abort_req.store(0);
+            return set_err(ctx, DSORT_ECOMM, "ncclCommInitRankConfig: aborted by dsort_comm_abort");
+        }
+        usleep(50);
+    }
+    if (r != ncclSuccess) {
+        if (c) ncclCommAbort(c);
+        return set_err(ctx, DSORT_ECOMM, std::string("ncclCommInitRankConfig: ") + ncclGetErrorString(r) +
                                              " (RCCL needs one GPU per rank; ranks sharing a GPU use "
                                              "dsort_comm_init_transport)");
+    }
     ctx->comm = c;
     ctx->nranks = nranks;
     ctx->rank = rank;
@@ -709,7 +888,9 @@ int dsort_comm_init(dsort_ctx *ctx, int nranks, int rank, const char id[DSORT_UN
 int dsort_comm_init_transport(dsort_ctx *ctx, int nranks, int rank, const dsort_transport *t) {
     if (!ctx || !t || !t->allgather || !t->alltoallv || nranks < 1 || rank < 0 || rank >= nranks)
         return set_err(ctx, DSORT_EINVAL, "bad argument");
+    std::unique_lock<std::mutex> lock(comm_mutex(ctx));
     if (ctx->comm || ctx->has_transport) return set_err(ctx, DSORT_EINVAL, "communicator already initialised");
+    ctx->abort_req.store(0);  // a flag left by the previous communicator's abort
     ctx->transport = *t;
     ctx->has_transport = true;
     ctx->nranks = nranks;
@@ -719,20 +900,30 @@ int dsort_comm_init_transport(dsort_ctx *ctx, int nranks, int rank, const dsort_
 
 int dsort_comm_abort(dsort_ctx *ctx) {
     if (!ctx) return DSORT_EINVAL;
-    ctx->has_transport = false;
-    if (ctx->comm) ncclCommAbort(ctx->comm);
-    ctx->comm = nullptr;
-    ctx->nranks = 1;
-    ctx->rank = 0;
+    std::unique_lock<std::mutex> lock(comm_mutex(ctx), std::try_to_lock);
+    if (!lock.owns_lock()) {  // an exchange is running on another thread: it aborts itself
+        ctx->abort_req.store(1);
+        return DSORT_OK;
+    }
+    abort_comm_locked(ctx);
+    ctx->abort_req.store(0);
     return DSORT_OK;
 }
 
 int dsort_comm_destroy(dsort_ctx *ctx) {
     if (!ctx) return DSORT_EINVAL;
+    std::unique_lock<std::mutex> lock(comm_mutex(ctx));
     ctx->has_transport = false;
     if (ctx->comm) {
         hipStreamSynchronize(ctx->stream);
-        ncclCommDestroy(ctx->comm);
+        // non-blocking communicator: finalize, wait for it, then destroy
+        ncclResult_t r = ncclCommFinalize(ctx->comm);
+        while (r == ncclInProgress) {
+            ncclCommGetAsyncError(ctx->comm, &r);
+            if (r == ncclInProgress) usleep(50);
+        }
+        if (r == ncclSuccess) ncclCommDestroy(ctx->comm);
+        else ncclCommAbort(ctx->comm);
     }
     ctx->comm = nullptr;
     ctx->nranks = 1;
@@ -836,6 +1027,25 @@ int dsort_copy_h2d(dsort_ctx *ctx, void *d, const void *h, size_t bytes) {
 int dsort_copy_d2h(dsort_ctx *ctx, void *h, const void *d, size_t bytes) {
     if (!ctx) return DSORT_EINVAL;
     if (bytes) DSORT_HIP(ctx, hipMemcpy(h, d, bytes, hipMemcpyDeviceToHost));
+    return DSORT_OK;
+}
+
+int dsort_copy_d2d(dsort_ctx *ctx, void *d, const void *src, size_t bytes) {
+    if (!ctx) return DSORT_EINVAL;
+    if (bytes) {
+        DSORT_HIP(ctx, hipMemcpyAsync(d, src, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+        DSORT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    return DSORT_OK;
+}
+int dsort_host_register(dsort_ctx *ctx, void *host, size_t bytes) {
+    if (!ctx || (!host && bytes)) return DSORT_EINVAL;
+    if (bytes) DSORT_HIP(ctx, hipHostRegister(host, bytes, hipHostRegisterDefault));
+    return DSORT_OK;
+}
+int dsort_host_unregister(dsort_ctx *ctx, void *host) {
+    if (!ctx) return DSORT_EINVAL;
+    if (host) DSORT_HIP(ctx, hipHostUnregister(host));
     return DSORT_OK;
 }
 

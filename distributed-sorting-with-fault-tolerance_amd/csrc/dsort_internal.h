@@ -6,6 +6,7 @@
 #include <stdint.h>
 #include <stddef.h>
 
+#include <atomic>
 #include <string>
 
 #include "dsort.h"
@@ -67,8 +68,24 @@ struct PassDesc {
 
 }  // namespace dsort
 
+// Per-context options (dsort_set_option; defaults = the tuned values).
+struct dsort_opts {
+    int64_t buckets = -1;           // DSORT_OPT_BUCKETS: -1 auto, 0 off, B forced
+    int64_t bucket_keys = 1 << 20;  // DSORT_OPT_BUCKET_KEYS (int32)
+    int64_t bucket_os = 256;        // DSORT_OPT_BUCKET_OVERSAMPLE (int32)
+    int64_t bucket_skew = 1;        // DSORT_OPT_BUCKET_SKEW (int32)
+    int64_t max_logf = -1;          // DSORT_OPT_MAX_FANIN_LOG2: -1 = per key type default
+    int64_t kill_after_pass = -1;   // DSORT_OPT_KILL_AFTER_PASS
+    int64_t kill_in_exchange = -1;  // DSORT_OPT_KILL_IN_EXCHANGE
+    int64_t comm_timeout_ms = 0;    // DSORT_OPT_COMM_TIMEOUT_MS
+};
+
 // The context.  One per host thread, bound to one device.
 struct dsort_ctx {
+    dsort_opts opt;
+    int nested = 0;  // > 0 inside a sort the library runs for itself (the splitter-sample sort):
+                     // such a sort never buckets and never fires the fault injection
+    std::atomic<int> abort_req{0};  // dsort_comm_abort from another thread during an exchange
     int device = 0;
     hipStream_t stream = nullptr;
     std::string err;
@@ -119,7 +136,8 @@ struct dsort_ctx {
     void *small_host = nullptr;  // pinned
     size_t small_host_bytes = 0;
     // stage timing
-    hipEvent_t ev[8] = {};
+    hipEvent_t ev[8] = {};  // 0 start, 1 tile sort done, 2 local sort done, 3 exchange done,
+                            // 4 final merge done, 5/6 around the key all-to-all
     unsigned ev_mask = 0;             // events recorded by the last call (bit i = ev[i])
     hipStream_t last_stream = nullptr;  // stream of the last asynchronous call
     static constexpr int kMaxKev = 128;  // per-launch events of the merge kernel (2 per pass)
@@ -143,18 +161,20 @@ template <typename T>
 int sort_device(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipStream_t s, bool timed);
 template <typename T>
 int merge_device(dsort_ctx *ctx, const T *d_in, const size_t *lens, int k, T *d_out,
-                 hipStream_t s);
+                 hipStream_t s, bool keep_stats = false);
 // int32 path on wave-register bitonic networks (dsort_wave.hip); sort_device/merge_device route
-// 32-bit keys here unless DSORT_KERNELS=legacy selects the LDS merge-path kernels.
+// 32-bit keys here.  wave_merge_i32 with keep_stats leaves the statistics and per-launch events of
+// the preceding local sort alone (the sample sort's final merge).
 int wave_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys, size_t n, hipStream_t s,
                   bool timed);
 int wave_merge_i32(dsort_ctx *ctx, const int32_t *d_in, const size_t *lens, int k, int32_t *d_out,
-                   hipStream_t s);
-bool use_legacy_kernels();
-// Fault injection for the fault-tolerance tests and bench (BASELINE config C5): when
-// DSORT_INJECT_KILL_AFTER_PASS=k is set, the process SIGKILLs itself right after merge pass k of a
-// local sort has finished on the GPU -- a worker dying mid-sort.  No effect otherwise.
-void fault_point(hipStream_t s, int pass_done);
+                   hipStream_t s, bool keep_stats = false);
+// Fault injection for the fault-tolerance tests and bench (BASELINE config C5): with
+// DSORT_OPT_KILL_AFTER_PASS = k the process SIGKILLs itself right after merge pass k of a local
+// (non-nested) sort has finished on the GPU -- a worker dying mid-sort.  No effect otherwise.
+void fault_point(dsort_ctx *ctx, hipStream_t s, int pass_done);
+// Largest log2 fan-in of one merge pass: the option, else the key type's default.
+int max_logf(const dsort_ctx *ctx, int type_default, int type_cap);
 
 }  // namespace dsort
 

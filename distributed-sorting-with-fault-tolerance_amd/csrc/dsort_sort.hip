@@ -400,23 +400,18 @@ static int ceil_log2(uint64_t x) {
     return p;
 }
 
-// Largest F (log2) a pass may use; DSORT_MAX_LOGF overrides it for experiments.
-static int max_logf() {
-    static int v = -1;
-    if (v < 0) {
-        const char *e = getenv("DSORT_MAX_LOGF");
-        int x = e ? atoi(e) : 5;
-        v = x < 1 ? 1 : (x > kMaxLogF ? kMaxLogF : x);
-    }
-    return v;
+int max_logf(const dsort_ctx *ctx, int type_default, int type_cap) {
+    const int64_t o = ctx->opt.max_logf;
+    const int x = o < 0 ? type_default : (int)o;
+    return x < 1 ? 1 : (x > type_cap ? type_cap : x);
 }
 
 // log2(F) of each pass: as few passes as the cap allows, the bits spread evenly over them.
-static std::vector<int> plan_passes(uint64_t runs) {
+static std::vector<int> plan_passes(const dsort_ctx *ctx, uint64_t runs) {
     std::vector<int> out;
     const int bits = ceil_log2(runs);
     if (bits == 0) return out;
-    const int cap = max_logf();
+    const int cap = max_logf(ctx, 5, kMaxLogF);
     const int P = (bits + cap - 1) / cap;
     for (int p = 0; p < P; ++p) out.push_back(bits / P + (p < bits % P ? 1 : 0));
     return out;
@@ -453,31 +448,22 @@ static int launch_pass(dsort_ctx *ctx, const T *src, T *dst, const PassDesc &pd,
     return DSORT_OK;
 }
 
-void fault_point(hipStream_t s, int pass_done) {
-    const char *e = getenv("DSORT_INJECT_KILL_AFTER_PASS");  // read per call: armed per sort
-    if (e && atoi(e) == pass_done) {
+void fault_point(dsort_ctx *ctx, hipStream_t s, int pass_done) {
+    if (ctx->nested == 0 && ctx->opt.kill_after_pass >= 0 && ctx->opt.kill_after_pass == pass_done) {
         (void)hipStreamSynchronize(s);
         raise(SIGKILL);
     }
-}
-
-bool use_legacy_kernels() {
-    static int v = -1;
-    if (v < 0) {
-        const char *e = getenv("DSORT_KERNELS");
-        v = (e && std::string(e) == "legacy") ? 1 : 0;
-    }
-    return v == 1;
 }
 
 // ---- bucketed int64 sort (dsort_bucket.h) --------------------------------------------------
 // As the int32 one (dsort_wave.hip): B ~ n / 2^21 buckets by (key, index) splitters, one
 // partition pass, then the tile sort (4096-key tiles) and the k-way passes inside every bucket
 // (groups of <= 2^max_logf runs): 2 merge passes at 2^30 keys instead of 4.  The 32*B samples
-// are sorted on the host (16-byte (key, index) pairs).  DSORT_BUCKETS as for int32.
-static int bucket_count_i64(uint64_t n) {
-    const char *e = getenv("DSORT_BUCKETS");
-    const int forced = e ? atoi(e) : -1;
+// are sorted on the host (16-byte (key, index) pairs).  DSORT_OPT_BUCKETS as for int32; a nested
+// sort never buckets.
+static int bucket_count_i64(const dsort_ctx *ctx, uint64_t n) {
+    if (ctx->nested) return 0;
+    const int64_t forced = ctx->opt.buckets;
     if (forced == 0) return 0;
     uint64_t B = forced > 0 ? (uint64_t)forced : (n >> 21);
     if (forced < 0 && n < (1ull << 25)) return 0;
@@ -570,7 +556,7 @@ static int bucket_sort_i64(dsort_ctx *ctx, const int64_t *d_in, int64_t *d_keys,
         for (uint64_t o = h; o < len; o += TILE) runs[b].push_back(len - o < (uint64_t)TILE ? len - o : TILE);
         maxruns = runs[b].size() > maxruns ? runs[b].size() : maxruns;
     }
-    const std::vector<int> pbits = plan_passes(maxruns);
+    const std::vector<int> pbits = plan_passes(ctx, maxruns);
     const int passes = (int)pbits.size();
     ctx->stats.merge_passes = passes;
     T *bufs[2] = {d_keys, scratch};
@@ -589,7 +575,6 @@ static int bucket_sort_i64(dsort_ctx *ctx, const int64_t *d_in, int64_t *d_keys,
     // 4. group tables of every pass (one staging buffer, one copy), then the passes.  Per-bucket
     // fan-in as in the int32 driver: the passes after the first keep the global fan-in, the first
     // resolves only the levels the bucket still needs; one launch per kernel fan-in of a pass.
-    const bool per_bucket = !(getenv("DSORT_BUCKET_FANIN") && std::string(getenv("DSORT_BUCKET_FANIN")) == "global");
     struct PassPlan { int logf; uint64_t ngroups, ntiles; size_t group_off, tile_off; int pass; };
     std::vector<PassPlan> plan;  // one entry per launch
     std::vector<GroupK> groups;
@@ -603,12 +588,9 @@ static int bucket_sort_i64(dsort_ctx *ctx, const int64_t *d_in, int64_t *d_keys,
         std::vector<int> pk;
         uint64_t base = 0;
         for (int b = 0; b < B; ++b) {
-            int fb = pbits[p];
-            if (per_bucket) {
-                const int need = blev[b] - tail[p + 1];
-                fb = need < 0 ? 0 : (need < pbits[p] ? need : pbits[p]);
-                blev[b] -= fb;
-            }
+            const int need = blev[b] - tail[p + 1];
+            const int fb = need < 0 ? 0 : (need < pbits[p] ? need : pbits[p]);
+            blev[b] -= fb;
             const size_t MAXF = (size_t)1 << fb;
             std::vector<uint64_t> next;
             const size_t nr = runs[b].size();
@@ -684,7 +666,7 @@ static int bucket_sort_i64(dsort_ctx *ctx, const int64_t *d_in, int64_t *d_keys,
             if (rc) return rc;
             if (q + 1 == plan.size() || plan[q + 1].pass != plan[q].pass) {  // pass complete
                 cur ^= 1;
-                fault_point(s, plan[q].pass);
+                fault_point(ctx, s, plan[q].pass);
             }
         }
     }
@@ -698,10 +680,9 @@ static int bucket_sort_i64(dsort_ctx *ctx, const int64_t *d_in, int64_t *d_keys,
 template <typename T>
 int sort_device(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipStream_t s, bool timed) {
     if constexpr (std::is_same<T, int32_t>::value) {
-        if (!use_legacy_kernels()) return wave_sort_i32(ctx, d_in, d_keys, n, s, timed);
+        return wave_sort_i32(ctx, d_in, d_keys, n, s, timed);
     } else {
-        if (const int B = bucket_count_i64(n)) return bucket_sort_i64(ctx, d_in, d_keys, n, s, timed, B);
-    }
+    if (const int B = bucket_count_i64(ctx, n)) return bucket_sort_i64(ctx, d_in, d_keys, n, s, timed, B);
     constexpr int THREADS = Geom<T>::THREADS, K = Geom<T>::K, TILE = Geom<T>::TILE;
     ctx->stats = dsort_stats{};
     ctx->stats.keys_in = n;
@@ -716,7 +697,7 @@ int sort_device(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipStream_t 
         return DSORT_OK;
     }
     const uint64_t tiles = ceil_div(n, TILE);
-    const std::vector<int> plan = plan_passes(tiles);
+    const std::vector<int> plan = plan_passes(ctx, tiles);
     const int passes = (int)plan.size();
     ctx->stats.merge_passes = passes;
     T *scratch = nullptr;
@@ -753,13 +734,14 @@ int sort_device(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipStream_t 
         if (rc) return rc;
         R <<= plan[p];
         cur ^= 1;
-        fault_point(s, p);
+        fault_point(ctx, s, p);
     }
     if (timed && ctx->ev_ok) {
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[2], s));
         ctx->ev_mask |= 4u;
     }
     return DSORT_OK;
+    }
 }
 
 // k-way merge of back-to-back runs of arbitrary lengths (the master merge, server.c:481-515,
@@ -767,19 +749,23 @@ int sort_device(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipStream_t 
 // levels of kMaxF-run groups.  Lower runs win ties at every level.
 template <typename T>
 int merge_device(dsort_ctx *ctx, const T *d_in, const size_t *lens, int k, T *d_out,
-                 hipStream_t s) {
+                 hipStream_t s, bool keep_stats) {
     if constexpr (std::is_same<T, int32_t>::value) {
-        if (!use_legacy_kernels()) return wave_merge_i32(ctx, d_in, lens, k, d_out, s);
-    }
+        return wave_merge_i32(ctx, d_in, lens, k, d_out, s, keep_stats);
+    } else {
     constexpr int THREADS = Geom<T>::THREADS, K = Geom<T>::K, TILE = Geom<T>::TILE;
-    ctx->stats = dsort_stats{};
+    if (!keep_stats) {
+        ctx->stats = dsort_stats{};
+        ctx->kev_used = 0;
+    }
     ctx->last_stream = s;
-    ctx->kev_used = 0;
     uint64_t n = 0;
     std::vector<uint64_t> rl(lens, lens + k);
     for (int j = 0; j < k; ++j) n += lens[j];
-    ctx->stats.keys_in = ctx->stats.keys_out = n;
-    ctx->stats.tile_keys = TILE;
+    if (!keep_stats) {
+        ctx->stats.keys_in = ctx->stats.keys_out = n;
+        ctx->stats.tile_keys = TILE;
+    }
     if (n == 0) return DSORT_OK;
     if (k == 1) {
         DSORT_HIP(ctx, hipMemcpyAsync(d_out, d_in, n * sizeof(T), hipMemcpyDeviceToDevice, s));
@@ -788,7 +774,7 @@ int merge_device(dsort_ctx *ctx, const T *d_in, const size_t *lens, int k, T *d_
     // levels: each merges groups of up to kMaxF consecutive runs
     int levels = 0;
     for (uint64_t r = (uint64_t)k; r > 1; r = ceil_div(r, kMaxF)) ++levels;
-    ctx->stats.merge_passes = levels;
+    if (!keep_stats) ctx->stats.merge_passes = levels;
     int rc;
     if (levels > 1) {
         rc = ensure(ctx, &ctx->scratch2, &ctx->scratch2_bytes, n * sizeof(T), "merge scratch");
@@ -849,6 +835,7 @@ int merge_device(dsort_ctx *ctx, const T *d_in, const size_t *lens, int k, T *d_
         which ^= 1;
     }
     return DSORT_OK;
+    }
 }
 
 template int sort_device<int32_t>(dsort_ctx *, const int32_t *, int32_t *, size_t, hipStream_t,
@@ -856,8 +843,8 @@ template int sort_device<int32_t>(dsort_ctx *, const int32_t *, int32_t *, size_
 template int sort_device<int64_t>(dsort_ctx *, const int64_t *, int64_t *, size_t, hipStream_t,
                                   bool);
 template int merge_device<int32_t>(dsort_ctx *, const int32_t *, const size_t *, int, int32_t *,
-                                   hipStream_t);
+                                   hipStream_t, bool);
 template int merge_device<int64_t>(dsort_ctx *, const int64_t *, const size_t *, int, int64_t *,
-                                   hipStream_t);
+                                   hipStream_t, bool);
 
 }  // namespace dsort

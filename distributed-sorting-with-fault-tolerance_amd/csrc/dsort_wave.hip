@@ -683,20 +683,11 @@ static int ceil_log2(uint64_t x) {
     while ((1ull << p) < x) ++p;
     return p;
 }
-static int max_logf() {
-    static int v = -1;
-    if (v < 0) {
-        const char *e = getenv("DSORT_MAX_LOGF");
-        int x = e ? atoi(e) : 4;
-        v = x < 1 ? 1 : (x > kWaveMaxLogF ? kWaveMaxLogF : x);
-    }
-    return v;
-}
-static std::vector<int> plan_passes(uint64_t runs) {
+static std::vector<int> plan_passes(const dsort_ctx *ctx, uint64_t runs) {
     std::vector<int> out;
     const int bits = ceil_log2(runs);
     if (bits == 0) return out;
-    const int cap = max_logf();
+    const int cap = max_logf(ctx, 4, kWaveMaxLogF);
     const int P = (bits + cap - 1) / cap;
     for (int p = 0; p < P; ++p) out.push_back(bits / P + (p < bits % P ? 1 : 0));
     return out;
@@ -733,17 +724,16 @@ static int launch_pass_w(dsort_ctx *ctx, const int *src, int *dst, const PassDes
 
 // ---- bucketed sort (dsort_bucket.h) ------------------------------------------------------
 // Buckets of about 2^20 keys (64 tiles): at most 1024, and none below 2^25 keys
-// (DSORT_BUCKETS=0 turns the partition off, DSORT_BUCKETS=<B> forces B buckets,
-// DSORT_BUCKET_KEYS=<k> sets the nominal bucket size).  At 2^30 keys the largest of the 1024
-// buckets stays below 128 tiles (7 merge levels: F = 16, then F = 8), and the buckets of <= 64
-// runs take F = 8 twice (per-bucket fan-in, below).  768 buckets of 1.4 M keys: 15.49-15.53 ms;
-// 1024: 15.32-15.37 ms (profiles/r1_bucket_fanin_ab.txt).
-static int bucket_count(uint64_t n) {
-    const char *e = getenv("DSORT_BUCKETS");  // read per call: tests force small bucket counts
-    const int forced = e ? atoi(e) : -1;
+// (DSORT_OPT_BUCKETS = 0 turns the partition off, B forces B buckets, DSORT_OPT_BUCKET_KEYS sets
+// the nominal bucket size).  At 2^30 keys the largest of the 1024 buckets stays below 128 tiles
+// (7 merge levels: F = 16, then F = 8), and the buckets of <= 64 runs take F = 8 twice
+// (per-bucket fan-in, below).  768 buckets of 1.4 M keys: 15.49-15.53 ms; 1024: 15.32-15.37 ms
+// (profiles/r1_bucket_fanin_ab.txt).  A nested sort (the splitter samples) never buckets.
+static int bucket_count(const dsort_ctx *ctx, uint64_t n) {
+    if (ctx->nested) return 0;
+    const int64_t forced = ctx->opt.buckets;
     if (forced == 0) return 0;
-    const char *k = getenv("DSORT_BUCKET_KEYS");
-    const uint64_t tk = k && atoll(k) > 0 ? (uint64_t)atoll(k) : (1ull << 20);
+    const uint64_t tk = ctx->opt.bucket_keys > 0 ? (uint64_t)ctx->opt.bucket_keys : (1ull << 20);
     uint64_t B = forced > 0 ? (uint64_t)forced : ceil_div(n, tk);
     if (forced < 0 && n < (1ull << 25)) return 0;
     if (n >= (1ull << 32)) return 0;  // 32-bit bucket positions in the scatter
@@ -752,31 +742,25 @@ static int bucket_count(uint64_t n) {
 }
 
 // Samples per bucket for the int32 splitters (sorted on the GPU): the relative spread of the
-// bucket sizes is about 1/sqrt(os).  DSORT_BUCKET_OS overrides.
-static int bucket_os() {
-    const char *e = getenv("DSORT_BUCKET_OS");
-    const int v = e ? atoi(e) : 256;
-    return v < 1 ? 1 : (v > 4096 ? 4096 : v);
+// bucket sizes is about 1/sqrt(os) (DSORT_OPT_BUCKET_OVERSAMPLE).
+static int bucket_os(const dsort_ctx *ctx) {
+    const int64_t v = ctx->opt.bucket_os;
+    return v < 1 ? 1 : (v > 4096 ? 4096 : (int)v);
 }
 
 // Skewed bucket sizes.  When the mean bucket holds about 64 tiles (2^30 keys in 1024 buckets),
 // about half the buckets land above 64 runs and merge F = 16 then F = 8, the rest F = 8 twice.
 // Instead the first k buckets get 56 tiles' worth of samples (below 64 runs despite the sampling
 // spread) and the others share the rest, about 104 tiles each (below 128): most keys then take
-// the cheaper F = 8 first pass.  Returns k and the samples per small / large bucket;
-// DSORT_BUCKET_SKEW=0 turns it off.
+// the cheaper F = 8 first pass (profiles/r1_bucket_skew_sweep.txt: 52:100 .. 60:112 all within
+// 0.06 ms of 56:104).  Returns k and the samples per small / large bucket; DSORT_OPT_BUCKET_SKEW
+// = 0 turns it off.
 struct Skew { int k, kos, los; };
-static Skew bucket_skew(uint64_t n, int B, int os) {
-    const char *e = getenv("DSORT_BUCKET_SKEW");
-    if (e && atoi(e) == 0) return Skew{0, 0, 0};
+static Skew bucket_skew(const dsort_ctx *ctx, uint64_t n, int B, int os) {
+    if (!ctx->opt.bucket_skew) return Skew{0, 0, 0};
     const double R = (double)n / ((double)B * TILE);  // mean tiles per bucket
     if (B < 16 || R <= 56.0 || R > 72.0) return Skew{0, 0, 0};
-    double small = 56.0, large = 104.0;  // DSORT_BUCKET_SKEW=<small>:<large> overrides (experiments)
-    if (e && strchr(e, ':')) {
-        small = atof(e);
-        large = atof(strchr(e, ':') + 1);
-        if (!(small > 0 && large > small)) return Skew{0, 0, 0};
-    }
+    const double small = 56.0, large = 104.0;
     const int k = (int)((double)B * (large - R) / (large - small));
     if (k <= 0 || k >= B) return Skew{0, 0, 0};
     const int kos = (int)((double)os * small / R);
@@ -801,7 +785,7 @@ static int bucket_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys,
     const int subs = bucket_wg_subs<int32_t>(n);
     const uint64_t G = ceil_div(n, (uint64_t)subs * BK_T * Geo<int32_t>::KPT);
     const uint64_t nchunk = ceil_div(G, BK_CHUNK);
-    const int os = bucket_os();
+    const int os = bucket_os(ctx);
     const uint32_t S = (uint32_t)B * (uint32_t)os;
     const uint64_t tmax = ceil_div(n, TILE) + 2 * (uint64_t)B;  // + a head and a tail per bucket
     // device arena: samples, splitters, counts, chunk sums, offsets, bucket starts, tile table
@@ -838,7 +822,9 @@ static int bucket_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys,
     // 1. splitters from a regular sample, sorted in (key, index) order by the int64 sort
     hipLaunchKernelGGL(bucket_sample_kernel<int32_t>, dim3(ceil_div(S, 256)), dim3(256), 0, s, d_in, (uint64_t)n, smp, S);
     DSORT_HIP(ctx, hipGetLastError());
+    ++ctx->nested;  // the sample sort never buckets and never fires the fault injection
     rc = sort_device<int64_t>(ctx, smp, smp, S, s, false);
+    --ctx->nested;
     if (rc) return rc;
     // (the int64 sort reset the statistics and events; the int32 sort's start from here)
     ctx->stats = dsort_stats{};
@@ -851,7 +837,7 @@ static int bucket_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys,
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[0], s));
         ctx->ev_mask |= 1u;
     }
-    const Skew sk = bucket_skew(n, B, os);
+    const Skew sk = bucket_skew(ctx, n, B, os);
     hipLaunchKernelGGL(bucket_splitter_kernel<int32_t>, dim3(1), dim3(BK_MAXB), 0, s, smp, B, BP, os, spl,
                        sk.k, sk.kos, sk.los);
     // 2. histograms, their scan, the scatter
@@ -891,7 +877,7 @@ static int bucket_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys,
         for (uint64_t o = h; o < bsz[b]; o += TILE) runs[b].push_back(bsz[b] - o < (uint64_t)TILE ? bsz[b] - o : TILE);
         maxruns = runs[b].size() > maxruns ? runs[b].size() : maxruns;
     }
-    const std::vector<int> pbits = plan_passes(maxruns);
+    const std::vector<int> pbits = plan_passes(ctx, maxruns);
     const int passes = (int)pbits.size();
     ctx->stats.merge_passes = passes;
     int32_t *bufs[2] = {d_keys, scratch};
@@ -908,8 +894,7 @@ static int bucket_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys,
     // fan-in per pass: the passes after the first keep the global plan's fan-in and the first
     // takes only the levels the bucket still needs (a bucket of <= 64 runs merges F = 8 twice
     // instead of F = 16 then F = 8).  A pass is then one launch per kernel fan-in among its
-    // groups (DSORT_BUCKET_FANIN=global keeps the global fan-in for every bucket).
-    const bool per_bucket = !(getenv("DSORT_BUCKET_FANIN") && std::string(getenv("DSORT_BUCKET_FANIN")) == "global");
+    // groups.
     std::vector<BucketPass> plan;  // one entry per launch
     std::vector<int> plan_pass;    // the pass of every launch
     std::vector<GroupK> groups;
@@ -923,12 +908,9 @@ static int bucket_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys,
         std::vector<int> pk;          // kernel log2 fan-in of every group
         uint64_t base = 0;
         for (int b = 0; b < B; ++b) {
-            int fb = pbits[p];
-            if (per_bucket) {
-                const int need = blev[b] - tail[p + 1];  // levels this pass must resolve
-                fb = need < 0 ? 0 : (need < pbits[p] ? need : pbits[p]);
-                blev[b] -= fb;
-            }
+            const int need = blev[b] - tail[p + 1];  // levels this pass must resolve
+            const int fb = need < 0 ? 0 : (need < pbits[p] ? need : pbits[p]);
+            blev[b] -= fb;
             const size_t MAXF = (size_t)1 << fb;
             std::vector<uint64_t> next;
             const size_t nr = runs[b].size();
@@ -1008,7 +990,7 @@ static int bucket_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys,
             if (rc) return rc;
             if (q + 1 == plan.size() || plan_pass[q + 1] != plan_pass[q]) {  // pass complete
                 cur ^= 1;
-                fault_point(s, plan_pass[q]);
+                fault_point(ctx, s, plan_pass[q]);
             }
         }
     }
@@ -1042,9 +1024,9 @@ int wave_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys, size_t n
             DSORT_HIP(ctx, hipMemcpyAsync(d_keys, d_in, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
         return DSORT_OK;
     }
-    if (const int B = bucket_count(n)) return bucket_sort_i32(ctx, d_in, d_keys, n, s, timed, B);
+    if (const int B = bucket_count(ctx, n)) return bucket_sort_i32(ctx, d_in, d_keys, n, s, timed, B);
     const uint64_t tiles = ceil_div(n, TILE);
-    const std::vector<int> plan = plan_passes(tiles);
+    const std::vector<int> plan = plan_passes(ctx, tiles);
     const int passes = (int)plan.size();
     ctx->stats.merge_passes = passes;
     int32_t *scratch = nullptr;
@@ -1077,7 +1059,7 @@ int wave_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys, size_t n
         if (rc) return rc;
         Rr <<= plan[p];
         cur ^= 1;
-        fault_point(s, p);
+        fault_point(ctx, s, p);
     }
     if (timed && ctx->ev_ok) {
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[2], s));
@@ -1087,17 +1069,21 @@ int wave_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys, size_t n
 }
 
 int wave_merge_i32(dsort_ctx *ctx, const int32_t *d_in, const size_t *lens, int k, int32_t *d_out,
-                   hipStream_t s) {
+                   hipStream_t s, bool keep_stats) {
     using namespace wv;
     constexpr int MAXF = 1 << kWaveMaxLogF;
-    ctx->stats = dsort_stats{};
+    if (!keep_stats) {
+        ctx->stats = dsort_stats{};
+        ctx->kev_used = 0;
+    }
     ctx->last_stream = s;
-    ctx->kev_used = 0;
     uint64_t n = 0;
     std::vector<uint64_t> rl(lens, lens + k);
     for (int j = 0; j < k; ++j) n += lens[j];
-    ctx->stats.keys_in = ctx->stats.keys_out = n;
-    ctx->stats.tile_keys = TILE;
+    if (!keep_stats) {
+        ctx->stats.keys_in = ctx->stats.keys_out = n;
+        ctx->stats.tile_keys = TILE;
+    }
     if (n == 0) return DSORT_OK;
     if (k == 1) {
         DSORT_HIP(ctx, hipMemcpyAsync(d_out, d_in, n * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
@@ -1105,7 +1091,7 @@ int wave_merge_i32(dsort_ctx *ctx, const int32_t *d_in, const size_t *lens, int 
     }
     int levels = 0;
     for (uint64_t r = (uint64_t)k; r > 1; r = ceil_div(r, MAXF)) ++levels;
-    ctx->stats.merge_passes = levels;
+    if (!keep_stats) ctx->stats.merge_passes = levels;
     int rc;
     if (levels > 1) {
         rc = ensure(ctx, &ctx->scratch2, &ctx->scratch2_bytes, n * sizeof(int32_t), "merge scratch");

@@ -6,6 +6,7 @@ present, the calls raise.  torch is imported BEFORE the library so that libdsort
 runtime torch already loaded (same soname libamdhip64.so.7): device memory from torch tensors and
 the library's kernels then live in one runtime.
 """
+import contextlib
 import ctypes
 import os
 
@@ -26,7 +27,7 @@ ERRORS = {-1: "EINVAL", -2: "ENOMEM", -3: "EHIP", -4: "ECOMM", -5: "ENODEV", -6:
 # every symbol include/dsort.h declares (checked by tests/test_abi.py)
 EXPORTS = [
     "dsort_init", "dsort_finalize", "dsort_last_error", "dsort_version", "dsort_get_stats",
-    "dsort_synchronize", "dsort_sort_i32", "dsort_sort_i64", "dsort_sort_dev_i32",
+    "dsort_synchronize", "dsort_set_option", "dsort_get_option", "dsort_sort_i32", "dsort_sort_i64", "dsort_sort_dev_i32",
     "dsort_sort_dev_i64", "dsort_sort_dev_copy_i32", "dsort_sort_dev_copy_i64",
     "dsort_merge_i32", "dsort_merge_i64", "dsort_merge_dev_i32", "dsort_merge_dev_i64",
     "dsort_comm_unique_id", "dsort_comm_init", "dsort_comm_init_transport", "dsort_comm_abort",
@@ -37,9 +38,15 @@ EXPORTS = [
     "dsort_plan_sample_positions", "dsort_gen_uniform_i32", "dsort_gen_uniform_i64",
     "dsort_gen_zipf_i64", "dsort_fingerprint_i32", "dsort_fingerprint_i64",
     "dsort_count_descents_i32", "dsort_count_descents_i64", "dsort_dev_alloc", "dsort_dev_free",
-    "dsort_copy_h2d", "dsort_copy_d2h", "dsort_write_text_i32", "dsort_format_text_dev_i32",
+    "dsort_copy_h2d", "dsort_copy_d2h", "dsort_copy_d2d", "dsort_host_register",
+    "dsort_host_unregister", "dsort_write_text_i32", "dsort_format_text_dev_i32",
     "dsort_parse_text_dev_i32", "dsort_parse_text_i32", "dsort_format_text_i32",
 ]
+
+
+# dsort_set_option / dsort_get_option (include/dsort.h)
+OPTIONS = {"buckets": 1, "bucket_keys": 2, "bucket_oversample": 3, "bucket_skew": 4,
+           "max_fanin_log2": 5, "kill_after_pass": 6, "kill_in_exchange": 7, "comm_timeout_ms": 8}
 
 
 class DsortError(RuntimeError):
@@ -52,7 +59,8 @@ class Stats(ctypes.Structure):
                 ("total_ms", ctypes.c_double), ("merge_kernel_ms", ctypes.c_double),
                 ("merge_kernel_launches", ctypes.c_int), ("merge_passes", ctypes.c_int),
                 ("tile_keys", ctypes.c_int), ("keys_in", ctypes.c_size_t),
-                ("keys_out", ctypes.c_size_t)]
+                ("keys_out", ctypes.c_size_t), ("alltoall_ms", ctypes.c_double),
+                ("keys_sent", ctypes.c_size_t)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -144,6 +152,8 @@ def load():
         "dsort_version": (ctypes.c_char_p, []),
         "dsort_get_stats": (ctypes.c_int, [P, ctypes.POINTER(Stats)]),
         "dsort_synchronize": (ctypes.c_int, [P]),
+        "dsort_set_option": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int64]),
+        "dsort_get_option": (ctypes.c_int, [P, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]),
         "dsort_sort_i32": (ctypes.c_int, [P, P, SZ]),
         "dsort_sort_i64": (ctypes.c_int, [P, P, SZ]),
         "dsort_sort_dev_i32": (ctypes.c_int, [P, P, SZ, P]),
@@ -179,6 +189,9 @@ def load():
         "dsort_dev_free": (ctypes.c_int, [P, P]),
         "dsort_copy_h2d": (ctypes.c_int, [P, P, P, SZ]),
         "dsort_copy_d2h": (ctypes.c_int, [P, P, P, SZ]),
+        "dsort_copy_d2d": (ctypes.c_int, [P, P, P, SZ]),
+        "dsort_host_register": (ctypes.c_int, [P, P, SZ]),
+        "dsort_host_unregister": (ctypes.c_int, [P, P]),
         "dsort_write_text_i32": (ctypes.c_int, [ctypes.c_char_p, P, SZ]),
         "dsort_format_text_dev_i32": (ctypes.c_int, [P, P, SZ, P, SZ, ctypes.POINTER(SZ), P]),
         "dsort_parse_text_dev_i32": (ctypes.c_int, [P, P, SZ, P, SZ, ctypes.POINTER(SZ), P]),
@@ -286,6 +299,27 @@ class Context:
 
     def check(self, rc):
         return _check(self.h, rc)
+
+    # ---------------- options (dsort_set_option) -----------------------------------------
+    def set_option(self, name, value):
+        self.check(self.lib.dsort_set_option(self.h, OPTIONS[name], int(value)))
+
+    def get_option(self, name):
+        v = ctypes.c_int64()
+        self.check(self.lib.dsort_get_option(self.h, OPTIONS[name], ctypes.byref(v)))
+        return v.value
+
+    @contextlib.contextmanager
+    def options(self, **kw):
+        """Sets options for the body of a with-statement and restores the previous values."""
+        old = {k: self.get_option(k) for k in kw}
+        try:
+            for k, v in kw.items():
+                self.set_option(k, v)
+            yield self
+        finally:
+            for k, v in old.items():
+                self.set_option(k, v)
 
     # ---------------- host-buffer entry points (reference drop-ins) ----------------------
     def sort(self, keys):

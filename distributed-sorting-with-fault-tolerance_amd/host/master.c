@@ -3,6 +3,7 @@
  *   dsort_master [--workers N] [--proto v0|v1] [--device D] [--timeout SEC]
  *                [--retry-delay-ms MS] [--reassign first|least-loaded] [--codec gpu|cpu]
  *                [--output PATH] server.conf
+ *   dsort_master --mode samplesort --gpus N ...   the multi-GPU sample sort (ss_master.c)
  *
  * Same session model as server.c: accept exactly N worker connections (server.c:148-157), then
  * read file names from stdin until "exit" (server.c:160-168).  Per file:
@@ -182,7 +183,7 @@ static char *read_file(const char *path, size_t *len) {
 
 /* %d tokens separated by whitespace; returns the count or -1 on a non-integer token (where
  * server.c:179 would spin forever). */
-static long parse_keys(const char *t, size_t len, int32_t **out) {
+long master_parse_keys(const char *t, size_t len, int32_t **out) {
     size_t cap = len / 2 + 1, n = 0;
     int32_t *k = (int32_t *)malloc(cap * sizeof(int32_t));
     if (!k) return -1;
@@ -230,7 +231,12 @@ static void usage(void) {
     exit(2);
 }
 
+int samplesort_master(int argc, char **argv, const char *argv0); /* ss_master.c */
+
 int main(int argc, char **argv) {
+    for (int i = 1; i + 1 < argc; ++i)
+        if (!strcmp(argv[i], "--mode") && !strcmp(argv[i + 1], "samplesort"))
+            return samplesort_master(argc - 1, argv + 1, argv[0]);
     static cluster cl;
     memset(&cl, 0, sizeof cl);
     cl.n = 4; /* MAX_WORKERS, server.c:11 */
@@ -330,7 +336,7 @@ int main(int argc, char **argv) {
                 keys = NULL;
             }
         } else {
-            nk = parse_keys(text, len, &keys);
+            nk = master_parse_keys(text, len, &keys);
         }
         free(text);
         if (nk < 0) {

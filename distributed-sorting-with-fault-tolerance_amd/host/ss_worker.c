@@ -1,0 +1,456 @@
+/* ss_worker.c -- dsort_worker --mode samplesort: one GPU worker of the multi-GPU sample sort
+ * (client.c's role, protocol in ss.h).
+ *
+ *   dsort_worker --mode samplesort --connect HOST:PORT [--device D] [--verbose]
+ *
+ * Per job: map the master's chunk replicas and pin them (dsort_host_register); stage this rank's
+ * chunk in HBM (generated on the GPU and copied into the replica, or copied from it); build the
+ * communicator of epoch 0; on GO sort the chunk (dsort_sort_dev_copy_*: where client.c:117 calls
+ * merge_sort) and run the exchange (dsort_sample_merge_dev_*), report DONE.  A PLAN from the
+ * master (a peer failed) aborts the communicator -- also from inside a running exchange, through
+ * dsort_comm_abort on the reader thread -- and starts the recovery epoch: the chunks this worker
+ * now owns that it has not sorted yet come from the pinned replica, are sorted and merged into
+ * its run, and the exchange runs again over the survivors. */
+#define _GNU_SOURCE
+#include <arpa/inet.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/socket.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "dsort.h"
+#include "ss.h"
+#include "wire.h"
+
+typedef struct wk {
+    int fd;
+    dsort_ctx *ctx;
+    pthread_mutex_t send_mu;
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+    int go, bye, closed, slice_req, stop;
+    int plan_pending;
+    ss_plan plan;
+    uint32_t epoch;      /* epoch of the communicator in use */
+    int world;           /* ranks of that epoch */
+    int32_t relay_seq;   /* next relay request of this epoch */
+    int resp_ready;
+    int32_t resp_tag;
+    char *resp;
+    size_t resp_len;
+    uint32_t hb_ms;
+} wk;
+
+static double now_ms(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec * 1e3 + ts.tv_nsec / 1e6;
+}
+
+/* Sends one frame whose payload is up to two pieces (no copy). */
+static int send_frame2(wk *w, uint16_t type, int32_t status, const void *a, size_t na, const void *b, size_t nb) {
+    pthread_mutex_lock(&w->send_mu);
+    wire_hdr h = {WIRE_MAGIC, WIRE_VERSION, type, 1, status, (uint64_t)(na + nb)};
+    int rc = wire_send_all(w->fd, &h, sizeof h);
+    if (!rc && na) rc = wire_send_all(w->fd, a, na);
+    if (!rc && nb) rc = wire_send_all(w->fd, b, nb);
+    pthread_mutex_unlock(&w->send_mu);
+    return rc;
+}
+static int send_frame(wk *w, uint16_t type, const void *p, size_t bytes) {
+    return send_frame2(w, type, 0, p, bytes, NULL, 0);
+}
+
+/* The only reader of the socket after start-up: demultiplexes the master's frames. */
+static void *reader_main(void *arg) {
+    wk *w = (wk *)arg;
+    for (;;) {
+        wire_hdr h;
+        char *buf = NULL;
+        int bad = wire_v1_recv_hdr(w->fd, &h);
+        if (!bad && h.count) {
+            buf = (char *)malloc(h.count);
+            bad = !buf || wire_recv_all(w->fd, buf, h.count);
+        }
+        pthread_mutex_lock(&w->mu);
+        if (bad) {
+            w->closed = 1;
+            dsort_comm_abort(w->ctx); /* the master is gone: abandon any exchange in flight */
+            pthread_cond_broadcast(&w->cv);
+            pthread_mutex_unlock(&w->mu);
+            free(buf);
+            return NULL;
+        }
+        switch (h.type) {
+            case SS_GO: w->go = 1; break;
+            case SS_BYE: w->bye = 1; break;
+            case SS_GET_SLICE: w->slice_req = 1; break;
+            case SS_PLAN:
+                if (h.count == sizeof(ss_plan)) {
+                    memcpy(&w->plan, buf, sizeof(ss_plan));
+                    w->plan_pending = 1;
+                    /* under w->mu: the main thread cannot have built the next epoch's
+                     * communicator yet.  Inside a running exchange this only raises the abort
+                     * flag; the exchange aborts the communicator itself (dsort.h). */
+                    dsort_comm_abort(w->ctx);
+                }
+                break;
+            case SS_RELAY_RESP:
+                free(w->resp);
+                w->resp = buf;
+                buf = NULL;
+                w->resp_len = h.count;
+                w->resp_tag = h.status;
+                w->resp_ready = 1;
+                break;
+            default:
+                break;
+        }
+        pthread_cond_broadcast(&w->cv);
+        pthread_mutex_unlock(&w->mu);
+        free(buf);
+    }
+}
+
+static void *heartbeat_main(void *arg) {
+    wk *w = (wk *)arg;
+    for (;;) {
+        pthread_mutex_lock(&w->mu);
+        struct timespec ts;
+        clock_gettime(CLOCK_REALTIME, &ts);
+        ts.tv_nsec += (long)w->hb_ms * 1000000L;
+        ts.tv_sec += ts.tv_nsec / 1000000000L;
+        ts.tv_nsec %= 1000000000L;
+        while (!w->stop && !w->closed)
+            if (pthread_cond_timedwait(&w->cv, &w->mu, &ts) == ETIMEDOUT) break;
+        const int done = w->stop || w->closed;
+        pthread_mutex_unlock(&w->mu);
+        if (done || send_frame(w, SS_HB, NULL, 0)) return NULL;
+    }
+}
+
+/* ---- relay transport: the sample sort's exchanges through the master -------------------- */
+static int superseded(wk *w) { return w->closed || (w->plan_pending && w->plan.epoch > w->epoch); }
+
+static int relay(wk *w, uint16_t type, const void *a, size_t na, const void *b, size_t nb, char **resp,
+                 size_t *resp_len) {
+    pthread_mutex_lock(&w->mu);
+    if (superseded(w)) {
+        pthread_mutex_unlock(&w->mu);
+        return -1;
+    }
+    const int32_t tag = (int32_t)((w->epoch << 20) | (uint32_t)w->relay_seq++);
+    w->resp_ready = 0;
+    pthread_mutex_unlock(&w->mu);
+    if (send_frame2(w, type, tag, a, na, b, nb)) return -1;
+    pthread_mutex_lock(&w->mu);
+    while (!(w->resp_ready && w->resp_tag == tag) && !superseded(w)) pthread_cond_wait(&w->cv, &w->mu);
+    const int ok = w->resp_ready && w->resp_tag == tag;
+    if (ok) {
+        *resp = w->resp;
+        *resp_len = w->resp_len;
+        w->resp = NULL;
+        w->resp_ready = 0;
+    }
+    pthread_mutex_unlock(&w->mu);
+    return ok ? 0 : -1;
+}
+
+static int relay_allgather(void *user, const void *send, void *recv, size_t bytes) {
+    wk *w = (wk *)user;
+    char *r = NULL;
+    size_t rl = 0;
+    if (relay(w, SS_RELAY_AG, send, bytes, NULL, 0, &r, &rl)) return 1;
+    const int bad = rl != bytes * (size_t)w->world;
+    if (!bad) memcpy(recv, r, rl);
+    free(r);
+    return bad;
+}
+
+/* request: P send counts (uint64), then the pieces in destination order; response: P receive
+ * counts, then the pieces in source order */
+static int relay_alltoallv(void *user, const void *send, const size_t *sc, const size_t *sd, void *recv,
+                           const size_t *rcnt, const size_t *rd) {
+    wk *w = (wk *)user;
+    const int P = w->world;
+    uint64_t tot = 0;
+    for (int d = 0; d < P; ++d) tot += sc[d];
+    char *req = (char *)malloc((size_t)P * 8 + tot);
+    if (!req) return 1;
+    uint64_t off = (uint64_t)P * 8;
+    for (int d = 0; d < P; ++d) {
+        const uint64_t c = sc[d];
+        memcpy(req + (size_t)d * 8, &c, 8);
+        if (c) memcpy(req + off, (const char *)send + sd[d], c);
+        off += c;
+    }
+    char *r = NULL;
+    size_t rl = 0;
+    const int rc = relay(w, SS_RELAY_A2A, req, off, NULL, 0, &r, &rl);
+    free(req);
+    if (rc) return 1;
+    int bad = rl < (size_t)P * 8;
+    uint64_t pos = (uint64_t)P * 8;
+    for (int s = 0; s < P && !bad; ++s) {
+        uint64_t c;
+        memcpy(&c, r + (size_t)s * 8, 8);
+        if (c != rcnt[s] || pos + c > rl) {
+            bad = 1;
+            break;
+        }
+        if (c) memcpy((char *)recv + rd[s], r + pos, c);
+        pos += c;
+    }
+    free(r);
+    return bad;
+}
+
+/* ---- the sort ------------------------------------------------------------------------- */
+static void chunk_range(uint64_t n, uint32_t world, uint32_t c, uint64_t *off, uint64_t *len) {
+    const uint64_t q = n / world, r = n % world; /* server.c:185-216 */
+    *len = q + (c < r ? 1 : 0);
+    *off = (uint64_t)c * q + (c < r ? c : r);
+}
+
+#define CHECK(call)                                                                               \
+    do {                                                                                          \
+        int rc_ = (call);                                                                         \
+        if (rc_) {                                                                                \
+            fprintf(stderr, "worker: %s failed (%d): %s\n", #call, rc_, dsort_last_error(ctx));   \
+            return 1;                                                                             \
+        }                                                                                         \
+    } while (0)
+
+static int comm_up(wk *w, const ss_job *job, uint32_t epoch, int world, int rank, const char *uid,
+                   dsort_transport *tx) {
+    dsort_ctx *ctx = w->ctx;
+    pthread_mutex_lock(&w->mu);
+    w->epoch = epoch;
+    w->world = world;
+    w->relay_seq = 0;
+    pthread_mutex_unlock(&w->mu);
+    if (job->transport == 0) return dsort_comm_init(ctx, world, rank, uid);
+    return dsort_comm_init_transport(ctx, world, rank, tx);
+}
+
+int samplesort_worker(const char *host, int port, int device, int verbose) {
+    (void)verbose;
+    dsort_ctx *ctx = NULL;
+    int rc = dsort_init(&ctx, device);
+    if (rc) {
+        fprintf(stderr, "worker: dsort_init(device %d) failed (%d): a gfx950 GPU is required\n", device, rc);
+        return 3;
+    }
+    int fd = socket(AF_INET, SOCK_STREAM, 0);
+    struct sockaddr_in addr;
+    memset(&addr, 0, sizeof addr);
+    addr.sin_family = AF_INET;
+    addr.sin_port = htons((uint16_t)port);
+    if (fd < 0 || inet_pton(AF_INET, host, &addr.sin_addr) <= 0 ||
+        connect(fd, (struct sockaddr *)&addr, sizeof addr) < 0) {
+        perror("worker: connect");
+        return 1;
+    }
+    wire_set_nodelay(fd);
+    static wk w;
+    memset(&w, 0, sizeof w);
+    w.fd = fd;
+    w.ctx = ctx;
+    pthread_mutex_init(&w.send_mu, NULL);
+    pthread_mutex_init(&w.mu, NULL);
+    pthread_cond_init(&w.cv, NULL);
+    ss_hello hello = {(int32_t)getpid(), device};
+    if (send_frame(&w, SS_HELLO, &hello, sizeof hello)) return 1;
+    wire_hdr h;
+    ss_job job;
+    if (wire_v1_recv_hdr(fd, &h) || h.type != SS_JOB || h.count != sizeof job || wire_recv_all(fd, &job, sizeof job)) {
+        fprintf(stderr, "worker: no job from the master\n");
+        return 1;
+    }
+    const double t_setup0 = now_ms();
+    w.hb_ms = job.heartbeat_ms ? job.heartbeat_ms : 50;
+    const size_t kb = job.key_bytes;
+    const int i64 = kb == 8;
+    /* the master's chunk replicas: shared memory, pinned here for DMA */
+    const size_t shm_bytes = (job.n_total * kb) ? job.n_total * kb : 1;
+    int sfd = shm_open(job.shm_name, O_RDWR, 0600);
+    char *rep = sfd < 0 ? MAP_FAILED : (char *)mmap(NULL, shm_bytes, PROT_READ | PROT_WRITE, MAP_SHARED, sfd, 0);
+    if (rep == MAP_FAILED) {
+        perror("worker: chunk replicas (shm)");
+        return 1;
+    }
+    close(sfd);
+    CHECK(dsort_host_register(ctx, rep, shm_bytes));
+    const uint64_t n0 = job.chunk_len;
+    void *d_chunk = NULL, *d_run = NULL;
+    CHECK(dsort_dev_alloc(ctx, &d_chunk, (n0 ? n0 : 1) * kb));
+    CHECK(dsort_dev_alloc(ctx, &d_run, (n0 ? n0 : 1) * kb));
+    char *my_rep = rep + job.chunk_off * kb;
+    if (job.source == 2) {
+        CHECK(dsort_copy_h2d(ctx, d_chunk, my_rep, n0 * kb));
+    } else if (n0) {
+        if (job.source == 1) CHECK(dsort_gen_zipf_i64(ctx, (int64_t *)d_chunk, n0, job.seed, job.chunk_off, NULL));
+        else if (i64) CHECK(dsort_gen_uniform_i64(ctx, (int64_t *)d_chunk, n0, job.seed, job.chunk_off, NULL));
+        else CHECK(dsort_gen_uniform_i32(ctx, (int32_t *)d_chunk, n0, job.seed, job.chunk_off, NULL));
+        CHECK(dsort_synchronize(ctx));
+        CHECK(dsort_copy_d2h(ctx, my_rep, d_chunk, n0 * kb)); /* the master's replica of this chunk */
+    }
+    ss_ready ready = {job.rank, 0, n0, 0, 0, 0.0};
+    if (n0) {
+        if (i64) CHECK(dsort_fingerprint_i64(ctx, (const int64_t *)d_chunk, n0, &ready.fp_sum, &ready.fp_xor));
+        else CHECK(dsort_fingerprint_i32(ctx, (const int32_t *)d_chunk, n0, &ready.fp_sum, &ready.fp_xor));
+    }
+    CHECK(dsort_set_option(ctx, DSORT_OPT_COMM_TIMEOUT_MS, job.comm_timeout_ms));
+    CHECK(dsort_set_option(ctx, DSORT_OPT_KILL_IN_EXCHANGE, job.kill_in_exchange));
+    dsort_transport tx = {&w, relay_allgather, relay_alltoallv};
+    pthread_t rd_th, hb_th;
+    pthread_create(&rd_th, NULL, reader_main, &w);
+    pthread_create(&hb_th, NULL, heartbeat_main, &w);
+    CHECK(comm_up(&w, &job, 0, (int)job.world, (int)job.rank, job.uid, &tx));
+    ready.t_setup_ms = now_ms() - t_setup0;
+    if (send_frame(&w, SS_READY, &ready, sizeof ready)) return 1;
+
+    pthread_mutex_lock(&w.mu);
+    while (!w.go && !w.bye && !w.closed && !w.plan_pending) pthread_cond_wait(&w.cv, &w.mu);
+    const int start = w.go;
+    pthread_mutex_unlock(&w.mu);
+    int exit_code = 0;
+    if (start) {
+        const double t_go = now_ms();
+        /* the local sort: the worker's merge_sort (client.c:117); the fault injection of config C5
+         * strikes inside it, after merge pass k */
+        CHECK(dsort_set_option(ctx, DSORT_OPT_KILL_AFTER_PASS, job.kill_after_pass));
+        if (i64) CHECK(dsort_sort_dev_copy_i64(ctx, (const int64_t *)d_chunk, (int64_t *)d_run, n0, NULL));
+        else CHECK(dsort_sort_dev_copy_i32(ctx, (const int32_t *)d_chunk, (int32_t *)d_run, n0, NULL));
+        CHECK(dsort_synchronize(ctx));
+        CHECK(dsort_set_option(ctx, DSORT_OPT_KILL_AFTER_PASS, -1));
+        const double t_sorted = now_ms() - t_go;
+        uint64_t run_len = n0;
+        uint32_t owned[SS_MAX_CHUNKS];
+        uint32_t nowned = 1;
+        owned[0] = job.rank;
+        double t_rebuild = 0.0;
+        for (;;) {
+            /* one epoch's exchange over the current communicator */
+            const double t_ex = now_ms();
+            void *out = NULL;
+            size_t nout = 0;
+            rc = i64 ? dsort_sample_merge_dev_i64(ctx, (const int64_t *)d_run, run_len, (int64_t **)&out, &nout, NULL)
+                     : dsort_sample_merge_dev_i32(ctx, (const int32_t *)d_run, run_len, (int32_t **)&out, &nout, NULL);
+            if (!rc) rc = dsort_synchronize(ctx);
+            ss_done done;
+            memset(&done, 0, sizeof done);
+            done.epoch = w.epoch;
+            done.rank = (uint32_t)-1;
+            done.status = rc;
+            done.run_keys = run_len;
+            done.t_local_sort_ms = t_sorted;
+            done.t_exchange_ms = now_ms() - t_ex;
+            done.t_rebuild_ms = t_rebuild;
+            if (!rc) {
+                if (nout) {
+                    if (i64) {
+                        CHECK(dsort_count_descents_i64(ctx, (const int64_t *)out, nout, &done.descents));
+                        CHECK(dsort_fingerprint_i64(ctx, (const int64_t *)out, nout, &done.fp_sum, &done.fp_xor));
+                        int64_t v;
+                        CHECK(dsort_copy_d2h(ctx, &v, out, 8));
+                        done.first = v;
+                        CHECK(dsort_copy_d2h(ctx, &v, (char *)out + (nout - 1) * 8, 8));
+                        done.last = v;
+                    } else {
+                        CHECK(dsort_count_descents_i32(ctx, (const int32_t *)out, nout, &done.descents));
+                        CHECK(dsort_fingerprint_i32(ctx, (const int32_t *)out, nout, &done.fp_sum, &done.fp_xor));
+                        int32_t v;
+                        CHECK(dsort_copy_d2h(ctx, &v, out, 4));
+                        done.first = v;
+                        CHECK(dsort_copy_d2h(ctx, &v, (char *)out + (nout - 1) * 4, 4));
+                        done.last = v;
+                    }
+                }
+                done.n_out = nout;
+            }
+            if (send_frame(&w, SS_DONE, &done, sizeof done)) {
+                exit_code = 1;
+                break;
+            }
+            /* wait for the end of the job, a slice request or a recovery plan */
+            ss_plan plan;
+            int have_plan = 0;
+            for (;;) {
+                pthread_mutex_lock(&w.mu);
+                while (!w.bye && !w.closed && !w.slice_req && !(w.plan_pending && w.plan.epoch > w.epoch))
+                    pthread_cond_wait(&w.cv, &w.mu);
+                const int bye = w.bye || w.closed, slice = w.slice_req;
+                if (w.plan_pending && w.plan.epoch > w.epoch) {
+                    plan = w.plan;
+                    have_plan = 1;
+                }
+                w.slice_req = 0;
+                pthread_mutex_unlock(&w.mu);
+                if (slice && !rc) {
+                    char *hbuf = (char *)malloc(nout * kb + 1);
+                    if (!hbuf || dsort_copy_d2h(ctx, hbuf, out, nout * kb)) return 1;
+                    send_frame(&w, SS_SLICE, hbuf, nout * kb);
+                    free(hbuf);
+                    continue;
+                }
+                if (bye || have_plan) break;
+            }
+            if (!have_plan) break;
+            /* recovery epoch: drop the communicator, rebuild the run from the chunks now owned */
+            dsort_comm_abort(ctx);
+            const double t_rb = now_ms();
+            for (uint32_t i = 0; i < plan.nchunks; ++i) {
+                const uint32_t c = plan.chunks[i];
+                int have = 0;
+                for (uint32_t j = 0; j < nowned; ++j) have |= owned[j] == c;
+                if (have) continue;
+                uint64_t off, len;
+                chunk_range(job.n_total, job.world, c, &off, &len);
+                void *d_x = NULL, *d_both = NULL, *d_m = NULL;
+                CHECK(dsort_dev_alloc(ctx, &d_x, (len ? len : 1) * kb));
+                CHECK(dsort_dev_alloc(ctx, &d_both, (run_len + len + 1) * kb));
+                CHECK(dsort_dev_alloc(ctx, &d_m, (run_len + len + 1) * kb));
+                CHECK(dsort_copy_h2d(ctx, d_x, rep + off * kb, len * kb)); /* the master's pinned replica */
+                CHECK(dsort_copy_d2d(ctx, d_both, d_run, run_len * kb));
+                if (i64) CHECK(dsort_sort_dev_copy_i64(ctx, (const int64_t *)d_x, (int64_t *)((char *)d_both + run_len * kb), len, NULL));
+                else CHECK(dsort_sort_dev_copy_i32(ctx, (const int32_t *)d_x, (int32_t *)((char *)d_both + run_len * kb), len, NULL));
+                const size_t lens[2] = {run_len, len};
+                if (i64) CHECK(dsort_merge_dev_i64(ctx, (const int64_t *)d_both, lens, 2, (int64_t *)d_m, NULL));
+                else CHECK(dsort_merge_dev_i32(ctx, (const int32_t *)d_both, lens, 2, (int32_t *)d_m, NULL));
+                CHECK(dsort_synchronize(ctx));
+                dsort_dev_free(ctx, d_x);
+                dsort_dev_free(ctx, d_both);
+                dsort_dev_free(ctx, d_run);
+                d_run = d_m;
+                run_len += len;
+                owned[nowned++] = c;
+            }
+            t_rebuild = now_ms() - t_rb;
+            rc = comm_up(&w, &job, plan.epoch, (int)plan.world, (int)plan.rank, plan.uid, &tx);
+            if (rc) fprintf(stderr, "worker: communicator of epoch %u failed (%d): %s\n", plan.epoch, rc, dsort_last_error(ctx));
+        }
+    }
+    pthread_mutex_lock(&w.mu);
+    w.stop = 1;
+    pthread_cond_broadcast(&w.cv);
+    pthread_mutex_unlock(&w.mu);
+    pthread_join(hb_th, NULL);
+    dsort_comm_destroy(ctx);
+    shutdown(fd, SHUT_RDWR);
+    pthread_join(rd_th, NULL);
+    close(fd);
+    dsort_dev_free(ctx, d_chunk);
+    dsort_dev_free(ctx, d_run);
+    dsort_host_unregister(ctx, rep);
+    munmap(rep, shm_bytes);
+    dsort_finalize(ctx);
+    return exit_code;
+}

@@ -1,6 +1,7 @@
 /* worker.c -- the GPU worker node (role of the reference's client.c).
  *
  *   dsort_worker [--proto v0|v1] [--device D] [--fault MODE:K] [--verbose] client.conf
+ *   dsort_worker --mode samplesort --connect HOST:PORT --device D   (ss_worker.c)
  *
  * Connects to the master (client.c:68-88), then serves chunks until the master closes the
  * connection (client.c:94-134).  Where the reference calls merge_sort(chunk, 0, n-1)
@@ -55,7 +56,25 @@ static void maybe_fault(enum fault_mode mode, long at, long chunk_no) {
     }
 }
 
+int samplesort_worker(const char *host, int port, int device, int verbose); /* ss_worker.c */
+
 int main(int argc, char **argv) {
+    int samplesort = 0;
+    const char *connect_to = NULL;
+    for (int i = 1; i + 1 < argc; ++i) {
+        if (!strcmp(argv[i], "--mode") && !strcmp(argv[i + 1], "samplesort")) samplesort = 1;
+        if (!strcmp(argv[i], "--connect")) connect_to = argv[i + 1];
+    }
+    if (samplesort) {
+        int dev = 0;
+        for (int i = 1; i + 1 < argc; ++i)
+            if (!strcmp(argv[i], "--device")) dev = atoi(argv[i + 1]);
+        const char *colon = connect_to ? strrchr(connect_to, ':') : NULL;
+        if (!colon) usage();
+        char host[64];
+        snprintf(host, sizeof host, "%.*s", (int)(colon - connect_to), connect_to);
+        return samplesort_worker(host, atoi(colon + 1), dev, 0);
+    }
     int proto = 0, device = 0, verbose = 0;
     enum fault_mode fmode = FAULT_NONE;
     long fat = 0;

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define DSORT_ABI_VERSION 1
+#define DSORT_ABI_VERSION 2
 
 #define DSORT_OK 0
 #define DSORT_EINVAL (-1)   /* bad argument */
@@ -63,6 +63,8 @@ typedef struct dsort_stats {
     int tile_keys;          /* keys per block-sort tile                                   */
     size_t keys_in;         /* keys handed to the call                                    */
     size_t keys_out;        /* keys produced (multi-GPU: this rank's key range)           */
+    double alltoall_ms;     /* multi-GPU: the key all-to-all alone (grouped send/recv)    */
+    size_t keys_sent;       /* multi-GPU: keys this rank shipped to other ranks           */
 } dsort_stats;
 
 /* ---------------------------------------------------------------- lifecycle ---------- */
@@ -74,6 +76,27 @@ const char *dsort_version(void);
 int dsort_get_stats(const dsort_ctx *ctx, dsort_stats *out);
 /* Blocks until all work queued by this context has finished. */
 int dsort_synchronize(dsort_ctx *ctx);
+
+/* Per-context options (tuning and fault injection).  Defaults are the tuned values; nothing in
+ * the library reads the environment.  dsort_set_option returns DSORT_EINVAL for an unknown
+ * option or a value out of range. */
+#define DSORT_OPT_BUCKETS 1           /* partition pass: -1 automatic (default), 0 off, B >= 2 forces B
+                                         buckets at any size (<= 1024)                               */
+#define DSORT_OPT_BUCKET_KEYS 2       /* int32: nominal keys per bucket (default 2^20)                 */
+#define DSORT_OPT_BUCKET_OVERSAMPLE 3 /* int32: splitter samples per bucket, 1..4096 (default 256)     */
+#define DSORT_OPT_BUCKET_SKEW 4       /* int32: 1 = skewed bucket sizes where they save a merge level
+                                         (default), 0 = equal buckets                                  */
+#define DSORT_OPT_MAX_FANIN_LOG2 5    /* cap on log2(F) of one merge pass; -1 = per key type default   */
+#define DSORT_OPT_KILL_AFTER_PASS 6   /* fault injection (config C5): SIGKILL the calling process right
+                                         after merge pass k of a local sort; -1 = off (default)        */
+#define DSORT_OPT_KILL_IN_EXCHANGE 7  /* fault injection: SIGKILL inside the sample-sort exchange, at
+                                         stage 1 (samples all-gathered) or 2 (counts exchanged, keys
+                                         about to move); -1 = off (default)                            */
+#define DSORT_OPT_COMM_TIMEOUT_MS 8   /* deadline of every wait inside one sample-sort exchange on
+                                         RCCL (ms); on expiry the communicator is aborted and the call
+                                         returns DSORT_ETIMEOUT.  0 = no deadline (default)            */
+int dsort_set_option(dsort_ctx *ctx, int option, int64_t value);
+int dsort_get_option(const dsort_ctx *ctx, int option, int64_t *value);
 
 /* ---------------------------------------------------------------- worker sort -------- */
 /* Drop-in for `merge_sort(chunk, 0, n-1)` (client.c:117 -> client.c:166-173): sorts the
@@ -111,8 +134,12 @@ int dsort_merge_dev_i64(dsort_ctx *ctx, const int64_t *d_in, const size_t lens[]
 
 /* ---------------------------------------------------------------- multi-GPU ---------- */
 /* One process per GPU.  Rank 0 creates the 128-byte RCCL unique id and ships it to the other
- * ranks by any side channel (the bench uses torch.distributed's store; the C master uses its
- * TCP control socket); every rank then calls dsort_comm_init. */
+ * ranks by any side channel (the bench uses torch.distributed's store; the C master of
+ * `dsort_master --mode samplesort` creates it and sends it in every worker's JOB frame over its
+ * TCP control socket, host/master.c); every rank then calls dsort_comm_init.  The communicator
+ * is non-blocking: every wait of the exchange polls the stream, RCCL's asynchronous error and the
+ * abort flag (dsort_comm_abort from another thread), so a dead peer surfaces as DSORT_ECOMM or,
+ * with DSORT_OPT_COMM_TIMEOUT_MS, DSORT_ETIMEOUT instead of a hang. */
 #define DSORT_UNIQUE_ID_BYTES 128
 int dsort_comm_unique_id(char id[DSORT_UNIQUE_ID_BYTES]);
 int dsort_comm_init(dsort_ctx *ctx, int nranks, int rank, const char id[DSORT_UNIQUE_ID_BYTES]);
@@ -130,7 +157,9 @@ typedef struct dsort_transport {
                      void *recv, const size_t *rcounts, const size_t *rdispls);
 } dsort_transport;
 int dsort_comm_init_transport(dsort_ctx *ctx, int nranks, int rank, const dsort_transport *t);
-/* Abort in-flight collectives (fault path: a peer died) and drop the communicator. */
+/* Abort in-flight collectives (fault path: a peer died) and drop the communicator.  Safe to
+ * call from another thread while this context is inside a sample sort: the call only raises the
+ * abort flag, and the sample sort aborts the communicator itself and returns DSORT_ECOMM. */
 int dsort_comm_abort(dsort_ctx *ctx);
 int dsort_comm_destroy(dsort_ctx *ctx);
 
@@ -201,6 +230,11 @@ int dsort_dev_alloc(dsort_ctx *ctx, void **d_ptr, size_t bytes);
 int dsort_dev_free(dsort_ctx *ctx, void *d_ptr);
 int dsort_copy_h2d(dsort_ctx *ctx, void *d_dst, const void *h_src, size_t bytes);
 int dsort_copy_d2h(dsort_ctx *ctx, void *h_dst, const void *d_src, size_t bytes);
+int dsort_copy_d2d(dsort_ctx *ctx, void *d_dst, const void *d_src, size_t bytes);
+/* Pins a host range for DMA (hipHostRegister) and releases it: the master's chunk replicas,
+ * mapped from shared memory by every worker of the C sample sort (host/ss.h). */
+int dsort_host_register(dsort_ctx *ctx, void *host, size_t bytes);
+int dsort_host_unregister(dsort_ctx *ctx, void *host);
 
 /* Text output of the reference (server.c:517-519): one "%d\n" per key into `path`.
  * Host-only helper; returns DSORT_EINVAL if the file cannot be written. */

@@ -68,11 +68,11 @@ def listening(port):
 
 class Session:
     def __init__(self, workdir, workers=4, master="ours", worker_kinds=None, worker_args=None,
-                 master_args=(), lib_dir=None, proto="v0"):
+                 master_args=(), lib_dir=None, proto="v0", bin_dir=BIN, env=None):
         self.dir = str(workdir)
         self.port = free_port()
         self.n = workers
-        self.env = dict(os.environ)
+        self.env = dict(os.environ if env is None else env)
         if lib_dir:
             self.env["LD_LIBRARY_PATH"] = lib_dir + ":" + self.env.get("LD_LIBRARY_PATH", "")
         with open(os.path.join(self.dir, "server.conf"), "w") as f:
@@ -81,7 +81,7 @@ class Session:
             f.write(f"SERVER_IP=127.0.0.1\nSERVER_PORT={self.port}\n")
         self.mlog = open(os.path.join(self.dir, "master.log"), "w")
         if master == "ours":
-            cmd = [os.path.join(BIN, "dsort_master"), "--workers", str(workers), "--proto", proto,
+            cmd = [os.path.join(bin_dir, "dsort_master"), "--workers", str(workers), "--proto", proto,
                    *master_args, "server.conf"]
         else:
             cmd = [os.path.join(REF_BUILD, "server"), "server.conf"]
@@ -98,7 +98,7 @@ class Session:
         for i, kind in enumerate(kinds):
             log = open(os.path.join(self.dir, f"worker{i + 1}.log"), "w")
             if kind == "ours":
-                wc = [os.path.join(BIN, "dsort_worker"), "--proto", proto, *wargs[i], "client.conf"]
+                wc = [os.path.join(bin_dir, "dsort_worker"), "--proto", proto, *wargs[i], "client.conf"]
             else:
                 wc = [os.path.join(REF_BUILD, "client"), "client.conf"]
             p = subprocess.Popen(wc, cwd=self.dir, stdout=log, stderr=subprocess.STDOUT, env=self.env)

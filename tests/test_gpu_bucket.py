@@ -1,8 +1,8 @@
 """The bucketed int32 sort (dsort_bucket.h: sample-splitter partition pass, then the tile sort and
-the k-way merge passes inside every bucket) against numpy on the MI355X.  DSORT_BUCKETS forces a
-bucket count at any size (the library reads it per call), so small inputs exercise the same
-kernels as the 2^30-key bench: empty buckets, single-run buckets, 0..3-key head tiles, heavy
-duplicates split across buckets by the (key, index) composite."""
+the k-way merge passes inside every bucket) against numpy on the MI355X.  The option
+DSORT_OPT_BUCKETS forces a bucket count at any size, so small inputs exercise the same kernels as
+the 2^30-key bench: empty buckets, single-run buckets, 0..3-key head tiles, heavy duplicates split
+across buckets by the (key, index) composite."""
 import numpy as np
 import pytest
 
@@ -48,63 +48,96 @@ def _sort(ctx, a, inplace):
 @pytest.mark.parametrize("B,n", [(2, 100_003), (3, 17), (7, 3 * TILE + 5), (33, 1_000_003),
                                  (64, 4 * TILE), (1024, 500_000)])
 @pytest.mark.parametrize("inplace", [False, True])
-def test_bucketed_sort_vs_numpy(gpu_ctx, monkeypatch, kind, B, n, inplace):
-    monkeypatch.setenv("DSORT_BUCKETS", str(B))
+def test_bucketed_sort_vs_numpy(gpu_ctx, kind, B, n, inplace):
     a = _keys(np.random.default_rng(B * 131 + n), kind, n)
-    assert np.array_equal(_sort(gpu_ctx, a, inplace), np.sort(a))
+    with gpu_ctx.options(buckets=B):
+        assert np.array_equal(_sort(gpu_ctx, a, inplace), np.sort(a))
 
 
 @pytest.mark.parametrize("tiles,passes", [(200, 2), (300, 3)])
-def test_bucketed_sort_multi_pass_buckets(gpu_ctx, monkeypatch, tiles, passes):
+def test_bucketed_sort_multi_pass_buckets(gpu_ctx, tiles, passes):
     """Few buckets of many tiles: more than 16 (256) runs per bucket -> 2 (3) merge passes."""
-    monkeypatch.setenv("DSORT_BUCKETS", "2")
     a = _keys(np.random.default_rng(tiles), "uniform", 2 * tiles * TILE + 777)
-    assert np.array_equal(_sort(gpu_ctx, a, False), np.sort(a))
-    assert gpu_ctx.stats()["merge_passes"] == passes
+    with gpu_ctx.options(buckets=2):
+        assert np.array_equal(_sort(gpu_ctx, a, False), np.sort(a))
+        assert gpu_ctx.stats()["merge_passes"] == passes
 
 
 @pytest.mark.parametrize("dtype", ["i32", "i64"])
-@pytest.mark.parametrize("fanin", ["per-bucket", "global"])
 @pytest.mark.parametrize("B", [3, 9])
-def test_bucketed_sort_mixed_fanin(gpu_ctx, monkeypatch, dtype, fanin, B):
+def test_bucketed_sort_mixed_fanin(gpu_ctx, dtype, B):
     """Buckets whose mean size sits at a power-of-two run count (64 int32 tiles, 256 int64
     tiles), so the sampling spread puts some buckets above it and some below: a pass mixes
-    per-bucket fan-ins (one launch per kernel fan-in).  DSORT_BUCKET_FANIN=global plans every
-    bucket with the largest bucket's fan-in.  Both must sort exactly (keys: a dense duplicate-heavy
-    cluster plus the full int range)."""
+    per-bucket fan-ins (one launch per kernel fan-in).  It must sort exactly (keys: a dense
+    duplicate-heavy cluster plus the full int range)."""
     import torch
-    monkeypatch.setenv("DSORT_BUCKETS", str(B))
-    if fanin == "global":
-        monkeypatch.setenv("DSORT_BUCKET_FANIN", "global")
-    else:
-        monkeypatch.delenv("DSORT_BUCKET_FANIN", raising=False)
-    rng = np.random.default_rng(B * 7 + len(fanin))
+    rng = np.random.default_rng(B * 7 + 3)
     n = B * 64 * TILE + 333
     dense = rng.integers(-1000, 1000, n // 2)
     tail = rng.integers(INT_MIN, INT_MAX, n - n // 2, endpoint=True)
     a = rng.permutation(np.concatenate([dense, tail])).astype(np.int32 if dtype == "i32" else np.int64)
     t = torch.from_numpy(a).cuda()
     out = torch.empty_like(t)
-    gpu_ctx.sort_dev(t, out)
-    torch.cuda.synchronize()
+    with gpu_ctx.options(buckets=B):
+        gpu_ctx.sort_dev(t, out)
+        torch.cuda.synchronize()
+        assert gpu_ctx.stats()["merge_passes"] >= 1
     assert np.array_equal(out.cpu().numpy(), np.sort(a))
-    assert gpu_ctx.stats()["merge_passes"] >= 1
 
 
-def test_bucketed_default_at_2p26_matches_regular_path(gpu_ctx, monkeypatch):
-    """Default bucket count at 2^26 (64 buckets) and DSORT_BUCKETS=0 (regular passes): same
-    output, no descents, same multiset."""
+def test_forced_buckets_small_input_matches_unforced(gpu_ctx):
+    """with a forced bucket count the splitter samples used to be sorted by the
+    bucketed int64 sort in place over its own arena.  The nested sample sort now never buckets:
+    a forced-B sort equals the default path and numpy."""
+    import torch
+    rng = np.random.default_rng(11)
+    for kind in ("uniform", "few", "equal"):
+        a = _keys(rng, kind, 1 << 21)
+        t = torch.from_numpy(a).cuda()
+        o1, o2 = torch.empty_like(t), torch.empty_like(t)
+        with gpu_ctx.options(buckets=1024):
+            gpu_ctx.sort_dev(t, o1)
+        gpu_ctx.sort_dev(t, o2)
+        torch.cuda.synchronize()
+        assert torch.equal(o1, o2)
+        assert np.array_equal(o1.cpu().numpy(), np.sort(a))
+
+
+@pytest.mark.parametrize("skew", [0, 1])
+@pytest.mark.parametrize("kind", ["uniform", "few", "zipfish"])
+@pytest.mark.parametrize("R", [57, 64, 71])
+def test_skewed_buckets_on_and_off(gpu_ctx, skew, kind, R):
+    """ADVICE r1 (low): skewed bucket sizes engage for B >= 16 buckets of 56 < R <= 72 mean tiles;
+    on and off, at the edges of that window, for uniform, few-distinct and duplicate-heavy int32."""
+    import torch
+    B = 16
+    n = B * R * TILE + 101
+    rng = np.random.default_rng(R * 10 + skew)
+    if kind == "zipfish":
+        a = (rng.zipf(1.3, n) % 100_003).astype(np.int32) * 7919 - 40_000_000
+    else:
+        a = _keys(rng, kind, n)
+    t = torch.from_numpy(a).cuda()
+    out = torch.empty_like(t)
+    with gpu_ctx.options(buckets=B, bucket_skew=skew):
+        gpu_ctx.sort_dev(t, out)
+        torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), np.sort(a))
+
+
+def test_bucketed_default_at_2p26_matches_regular_path(gpu_ctx):
+    """Default bucket count at 2^26 (64 buckets) and buckets=0 (regular passes): same output, no
+    descents, same multiset."""
     import torch
     n = 1 << 26
     t = torch.empty(n, dtype=torch.int32, device="cuda")
     gpu_ctx.gen_uniform(t, 0x5EED2026)
     fp = gpu_ctx.fingerprint(t)
     o1, o2 = torch.empty_like(t), torch.empty_like(t)
-    monkeypatch.delenv("DSORT_BUCKETS", raising=False)
     gpu_ctx.sort_dev(t, o1)
     assert gpu_ctx.stats()["merge_passes"] == 2  # 64 buckets of ~2^20 keys: ~64 runs each
-    monkeypatch.setenv("DSORT_BUCKETS", "0")
-    gpu_ctx.sort_dev(t, o2)
+    with gpu_ctx.options(buckets=0):
+        gpu_ctx.sort_dev(t, o2)
     torch.cuda.synchronize()
     assert gpu_ctx.descents(o1) == 0 and gpu_ctx.fingerprint(o1) == fp
     assert torch.equal(o1, o2)
@@ -130,13 +163,13 @@ def _keys64(rng, kind, n):
 @pytest.mark.parametrize("kind", ["uniform", "equal", "few", "extremes", "small"])
 @pytest.mark.parametrize("B,n", [(2, 50_001), (5, 4096 * 3 + 1), (64, 1_000_003), (1024, 300_000)])
 @pytest.mark.parametrize("inplace", [False, True])
-def test_bucketed_sort_i64_vs_numpy(gpu_ctx, monkeypatch, kind, B, n, inplace):
-    monkeypatch.setenv("DSORT_BUCKETS", str(B))
+def test_bucketed_sort_i64_vs_numpy(gpu_ctx, kind, B, n, inplace):
     a = _keys64(np.random.default_rng(B * 7 + n), kind, n)
-    assert np.array_equal(_sort(gpu_ctx, a, inplace), np.sort(a))
+    with gpu_ctx.options(buckets=B):
+        assert np.array_equal(_sort(gpu_ctx, a, inplace), np.sort(a))
 
 
-def test_bucketed_zipf_i64_2p26(gpu_ctx, monkeypatch):
+def test_bucketed_zipf_i64_2p26(gpu_ctx):
     """Default bucket count on the BASELINE config-4 distribution (heavy duplicates): sorted,
     same multiset, identical to the regular passes."""
     import torch
@@ -145,10 +178,9 @@ def test_bucketed_zipf_i64_2p26(gpu_ctx, monkeypatch):
     gpu_ctx.gen_zipf_i64(t, 0x5EED2026)
     fp = gpu_ctx.fingerprint(t)
     o1, o2 = torch.empty_like(t), torch.empty_like(t)
-    monkeypatch.delenv("DSORT_BUCKETS", raising=False)
     gpu_ctx.sort_dev(t, o1)
-    monkeypatch.setenv("DSORT_BUCKETS", "0")
-    gpu_ctx.sort_dev(t, o2)
+    with gpu_ctx.options(buckets=0):
+        gpu_ctx.sort_dev(t, o2)
     torch.cuda.synchronize()
     assert gpu_ctx.descents(o1) == 0 and gpu_ctx.fingerprint(o1) == fp
     assert torch.equal(o1, o2)
@@ -157,20 +189,20 @@ def test_bucketed_zipf_i64_2p26(gpu_ctx, monkeypatch):
 @pytest.mark.parametrize("dtype", ["i32", "i64"])
 @pytest.mark.parametrize("shift_in,shift_out", [(1, 3), (3, 0), (0, 5), (2, 2)])
 @pytest.mark.parametrize("B,n", [(5, 300_001), (700, 2_000_003)])
-def test_bucketed_sort_unaligned_views(gpu_ctx, monkeypatch, dtype, shift_in, shift_out, B, n):
+def test_bucketed_sort_unaligned_views(gpu_ctx, dtype, shift_in, shift_out, B, n):
     """Input and output tensors that start at element offsets (not 16-byte aligned): the 16-byte
     loads of the tile sort and the line-aligned bucket scatter must not assume aligned caller
     buffers."""
     import torch
-    monkeypatch.setenv("DSORT_BUCKETS", str(B))
     rng = np.random.default_rng(B + shift_in * 7 + shift_out)
     a = _keys(rng, "uniform", n) if dtype == "i32" else _keys64(rng, "uniform", n)
     tdt = torch.int32 if dtype == "i32" else torch.int64
     src = torch.empty(n + 8, dtype=tdt, device="cuda")
     dst = torch.full((n + 8,), 77, dtype=tdt, device="cuda")
     src[shift_in:shift_in + n] = torch.from_numpy(a).cuda()
-    gpu_ctx.sort_dev(src[shift_in:shift_in + n], dst[shift_out:shift_out + n])
-    torch.cuda.synchronize()
+    with gpu_ctx.options(buckets=B):
+        gpu_ctx.sort_dev(src[shift_in:shift_in + n], dst[shift_out:shift_out + n])
+        torch.cuda.synchronize()
     d = dst.cpu().numpy()
     assert np.array_equal(d[shift_out:shift_out + n], np.sort(a))
     assert (d[:shift_out] == 77).all() and (d[shift_out + n:] == 77).all()  # nothing written outside
@@ -179,17 +211,17 @@ def test_bucketed_sort_unaligned_views(gpu_ctx, monkeypatch, dtype, shift_in, sh
 
 @pytest.mark.parametrize("dtype", ["i32", "i64"])
 @pytest.mark.parametrize("shift", [1, 2, 3])
-def test_bucketed_sort_unaligned_view_in_place(gpu_ctx, monkeypatch, dtype, shift):
+def test_bucketed_sort_unaligned_view_in_place(gpu_ctx, dtype, shift):
     import torch
-    monkeypatch.setenv("DSORT_BUCKETS", "37")
     n = 1_500_007
     rng = np.random.default_rng(shift)
     a = _keys(rng, "few", n) if dtype == "i32" else _keys64(rng, "few", n)
     tdt = torch.int32 if dtype == "i32" else torch.int64
     buf = torch.full((n + 8,), 5, dtype=tdt, device="cuda")
     buf[shift:shift + n] = torch.from_numpy(a).cuda()
-    gpu_ctx.sort_dev(buf[shift:shift + n])
-    torch.cuda.synchronize()
+    with gpu_ctx.options(buckets=37):
+        gpu_ctx.sort_dev(buf[shift:shift + n])
+        torch.cuda.synchronize()
     d = buf.cpu().numpy()
     assert np.array_equal(d[shift:shift + n], np.sort(a))
     assert (d[:shift] == 5).all() and (d[shift + n:] == 5).all()

@@ -27,6 +27,26 @@ def test_c1_kat_gpu_workers(tmp_path):
     print(s.master_log().splitlines()[-2])
 
 
+@pytest.mark.parametrize("proto", ["v0", "v1"])
+def test_c1_three_gpu_workers(tmp_path, proto):
+    """BASELINE config C1 as written: 1 server + 3 client processes (the reference hard-codes 4,
+    server.c:11; the build takes --workers).  Chunks of 3334/3333/3333 keys; output.txt bytes
+    identical to the reference's."""
+    exp = ref_files(tmp_path)
+    s = Session(tmp_path, workers=3, proto=proto)
+    assert s.sort_files(["input.txt"], timeout=100) == 0, s.master_log()
+    assert s.output() == exp
+    assert "workers=3 alive=3" in s.master_log()
+
+
+def test_c1_three_gpu_workers_one_fails(tmp_path):
+    exp = ref_files(tmp_path)
+    s = Session(tmp_path, workers=3, worker_args=[[], ["--fault", "exit-before-reply:1"], []])
+    assert s.sort_files(["input.txt"], timeout=100) == 0, s.master_log()
+    assert s.output() == exp
+    assert "Reassigning chunk 2 to worker node 1" in s.master_log()
+
+
 @pytest.mark.skipif(not HAVE_REF, reason="reference not built")
 def test_c1_gpu_master_reference_clients(tmp_path):
     exp = ref_files(tmp_path)

@@ -167,14 +167,20 @@ def test_gpu_fingerprint_matches_oracle(gpu_ctx, oracle):
     assert gpu_ctx.descents(t) == int((a[1:] < a[:-1]).sum())
 
 
-@pytest.mark.parametrize("n,dt", [(1 << 28, "i32"), ((1 << 26) + 12345, "i64")])
-def test_full_size_properties(gpu_ctx, n, dt):
+@pytest.mark.parametrize("n,dt,dist", [(1 << 28, "i32", "uniform"), ((1 << 26) + 12345, "i64", "uniform"),
+                                       (1 << 30, "i32", "uniform"), (1 << 30, "i64", "zipf")])
+def test_full_size_properties(gpu_ctx, n, dt, dist):
     """At BASELINE sizes the oracle is too slow: check size-independent properties on the GPU --
-    the output is ascending and is the same multiset as the input (fingerprint)."""
+    the output is ascending and is the same multiset as the input (fingerprint).  2^28 int32 is
+    config C2; 2^30 int32 is the metric's size with the default 1024-bucket skewed layout; 2^30
+    Zipf int64 is config C4 on one GPU."""
     import torch
     tdt = torch.int32 if dt == "i32" else torch.int64
     t = torch.empty(n, dtype=tdt, device="cuda")
-    gpu_ctx.gen_uniform(t, 0x5EED2026, 0)
+    if dist == "zipf":
+        gpu_ctx.gen_zipf_i64(t, 0x5EED2026, 0)
+    else:
+        gpu_ctx.gen_uniform(t, 0x5EED2026, 0)
     fp_in = gpu_ctx.fingerprint(t)
     out = torch.empty_like(t)
     gpu_ctx.sort_dev(t, out)

@@ -47,6 +47,17 @@ def test_kat_ours_v0(tmp_path, libdir):
     assert "Sorting completed for file input.txt" in s.master_log()
 
 
+@pytest.mark.parametrize("proto", ["v0", "v1"])
+def test_kat_three_workers(tmp_path, libdir, proto):
+    """BASELINE config C1 as written (1 server + 3 clients): the build's worker count is a flag;
+    the reference (MAX_WORKERS = 4, server.c:11) would block in accept."""
+    exp = ref_files(tmp_path)
+    s = Session(tmp_path, workers=3, lib_dir=libdir, proto=proto)
+    assert s.sort_files(["input.txt"]) == 0, s.master_log()
+    assert s.output() == exp
+    assert "workers=3 alive=3" in s.master_log()
+
+
 @pytest.mark.skipif(not HAVE_REF, reason="reference not built")
 def test_interop_our_master_reference_clients(tmp_path, libdir):
     exp = ref_files(tmp_path)
