@@ -173,15 +173,36 @@ def reference_tcp_c1(reps=5, timeout=60.0):
             f.write(f"SERVER_IP=127.0.0.1\nSERVER_PORT={port}\n")
         with open(src, "rb") as fi, open(os.path.join(d, "input.txt"), "wb") as fo:
             fo.write(fi.read())
-        srv = subprocess.Popen([server, "server.conf"], cwd=d, stdin=subprocess.PIPE, stdout=subprocess.PIPE,
-                               stderr=subprocess.STDOUT, bufsize=0)
+        # the server's stdout on a pseudo-terminal: printf is then line-buffered, as on the
+        # reference's console, so every line is seen when it is printed.  Boxes without pty
+        # devices fall back to watching output.txt: merge_chunks() writes it whole and closes it
+        # (server.c:484-523) just before the "Sorting completed" line.
+        import pty
+
+        try:
+            mfd, sfd = pty.openpty()
+        except OSError:
+            return _reference_tcp_c1_filepoll(d, server, client, reps, timeout)
+        srv = subprocess.Popen([server, "server.conf"], cwd=d, stdin=subprocess.PIPE, stdout=sfd,
+                               stderr=sfd, bufsize=0)
+        os.close(sfd)
         clients = []
         try:
             lines = []
 
             def reader():
-                for raw in iter(srv.stdout.readline, b""):
-                    lines.append((time.perf_counter(), raw))
+                buf = b""
+                while True:
+                    try:
+                        chunk = os.read(mfd, 1 << 16)
+                    except OSError:
+                        break
+                    if not chunk:
+                        break
+                    buf += chunk
+                    *full, buf = buf.split(b"\n")
+                    now = time.perf_counter()
+                    lines.extend((now, ln) for ln in full)
 
             th = threading.Thread(target=reader, daemon=True)
             th.start()
@@ -216,10 +237,52 @@ def reference_tcp_c1(reps=5, timeout=60.0):
                 if p.poll() is None:
                     p.kill()
                 p.wait()
+            os.close(mfd)
+    return _c1_result(times, ok, "pty")
+
+
+def _reference_tcp_c1_filepoll(d, server, client, reps, timeout):
+    """reference_tcp_c1 without a pty: the server's stdout is discarded; each file's end is the
+    moment output.txt (removed before the file name is sent) reaches the reference output's full
+    size.  The first file also waits for the 4 clients to connect, so only the median is fair."""
+    want = open(os.path.join(REPO, "tests", "golden", "ref_output.txt"), "rb").read()
+    outp = os.path.join(d, "output.txt")
+    srv = subprocess.Popen([server, "server.conf"], cwd=d, stdin=subprocess.PIPE, stdout=subprocess.DEVNULL,
+                           stderr=subprocess.DEVNULL, bufsize=0)
+    clients = []
+    try:
+        time.sleep(0.3)
+        for _ in range(4):
+            clients.append(subprocess.Popen([client, "client.conf"], cwd=d, stdout=subprocess.DEVNULL,
+                                            stderr=subprocess.DEVNULL))
+        t0 = time.time()
+        times = []
+        for _ in range(reps):
+            if os.path.exists(outp):
+                os.remove(outp)
+            ts = time.perf_counter()
+            srv.stdin.write(b"input.txt\n")
+            while not (os.path.exists(outp) and os.path.getsize(outp) >= len(want)):
+                if time.time() - t0 > timeout or srv.poll() is not None:
+                    return None
+                time.sleep(0.0002)
+            times.append(time.perf_counter() - ts)
+        time.sleep(0.05)
+        ok = open(outp, "rb").read() == want
+        srv.stdin.write(b"exit\n")
+    finally:
+        for p in clients + [srv]:
+            if p.poll() is None:
+                p.kill()
+            p.wait()
+    return _c1_result(times, ok, "output-file poll (no pty)")
+
+
+def _c1_result(times, ok, mode):
     med = sorted(times)[len(times) // 2]
-    return {"keys": 10000, "files": reps, "first_file_ms": round(1e3 * times[0], 3),
+    return {"keys": 10000, "files": len(times), "first_file_ms": round(1e3 * times[0], 3),
             "median_file_ms": round(1e3 * med, 3), "keys_per_s_median": 10000 / med,
-            "output_matches_reference_output_txt": ok}
+            "output_matches_reference_output_txt": ok, "timing": mode}
 
 
 def cpu_baseline(sample_keys, target_keys):
@@ -386,6 +449,9 @@ def run_multi(args, rank, world):
 
     local = int(os.environ.get("LOCAL_RANK", rank))
     torch.cuda.set_device(local)
+    if world == 1:  # --path samplesort on one GPU without a launcher: a one-rank rendezvous
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(free_port()))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     ctx = dsort.Context(local)
     uid = [dsort.Context.unique_id() if rank == 0 else None]

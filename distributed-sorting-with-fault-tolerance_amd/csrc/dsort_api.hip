@@ -43,7 +43,7 @@ int ensure(dsort_ctx *ctx, void **buf, size_t *have, size_t need, const char *wh
         // the old arena may still be used by queued work on any stream of this device
         hipError_t e = hipDeviceSynchronize();
         if (e != hipSuccess) return hip_err(ctx, e, "hipDeviceSynchronize (arena grow)");
-        hipFree(*buf);
+        (void)hipFree(*buf);
         *buf = nullptr;
         *have = 0;
     }
@@ -458,7 +458,7 @@ static int sample_sort(dsort_ctx *ctx, const T *d_in, size_t n_local, T **d_out,
     rc = ensure(ctx, &ctx->small, &ctx->small_bytes, total_small, "sample-sort small buffers");
     if (rc) return rc;
     if (ctx->small_host_bytes < total_small) {
-        if (ctx->small_host) hipHostFree(ctx->small_host);
+        if (ctx->small_host) (void)hipHostFree(ctx->small_host);
         ctx->small_host = nullptr;
         ctx->small_host_bytes = 0;
         DSORT_HIP(ctx, hipHostMalloc(&ctx->small_host, total_small, hipHostMallocDefault));
@@ -672,8 +672,8 @@ int dsort_init(dsort_ctx **out, int device) {
 
 int dsort_finalize(dsort_ctx *ctx) {
     if (!ctx) return DSORT_EINVAL;
-    hipSetDevice(ctx->device);
-    if (ctx->stream) hipStreamSynchronize(ctx->stream);
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->comm) {
         ncclCommAbort(ctx->comm);  // peers may be gone: never wait for them here
         ctx->comm = nullptr;
@@ -682,9 +682,9 @@ int dsort_finalize(dsort_ctx *ctx) {
                     ctx->local, ctx->recv, ctx->recv2, ctx->small, ctx->text_status,
                     ctx->bucket};
     for (void *b : bufs)
-        if (b) hipFree(b);
-    if (ctx->red_host) hipHostFree(ctx->red_host);
-    if (ctx->small_host) hipHostFree(ctx->small_host);
+        if (b) (void)hipFree(b);
+    if (ctx->red_host) (void)hipHostFree(ctx->red_host);
+    if (ctx->small_host) (void)hipHostFree(ctx->small_host);
     if (ctx->xfer) (void)hipHostFree(ctx->xfer);
     if (ctx->xfer2) (void)hipHostFree(ctx->xfer2);
     if (ctx->groups_host) (void)hipHostFree(ctx->groups_host);
@@ -695,7 +695,7 @@ int dsort_finalize(dsort_ctx *ctx) {
         if (e) (void)hipEventDestroy(e);
     for (auto &e : ctx->kev)
         if (e) (void)hipEventDestroy(e);
-    if (ctx->stream) hipStreamDestroy(ctx->stream);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return DSORT_OK;
 }
@@ -723,7 +723,7 @@ int dsort_set_option(dsort_ctx *ctx, int option, int64_t v) {
             o.bucket_skew = v;
             return DSORT_OK;
         case DSORT_OPT_MAX_FANIN_LOG2:
-            if (v != -1 && (v < 1 || v > kMaxLogF)) return set_err(ctx, DSORT_EINVAL, "DSORT_OPT_MAX_FANIN_LOG2: -1 or 1..6");
+            if (v != -1 && (v < 1 || v > kMaxLogF)) return set_err(ctx, DSORT_EINVAL, "DSORT_OPT_MAX_FANIN_LOG2: -1 or 1..5");
             o.max_logf = v;
             return DSORT_OK;
         case DSORT_OPT_KILL_AFTER_PASS:
@@ -915,7 +915,7 @@ int dsort_comm_destroy(dsort_ctx *ctx) {
     std::unique_lock<std::mutex> lock(comm_mutex(ctx));
     ctx->has_transport = false;
     if (ctx->comm) {
-        hipStreamSynchronize(ctx->stream);
+        (void)hipStreamSynchronize(ctx->stream);
         // non-blocking communicator: finalize, wait for it, then destroy
         ncclResult_t r = ncclCommFinalize(ctx->comm);
         while (r == ncclInProgress) {

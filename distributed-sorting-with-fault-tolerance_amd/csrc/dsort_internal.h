@@ -16,36 +16,13 @@ struct ncclComm;
 namespace dsort {
 
 // ----------------------------------------------------------------------------------------
-// Geometry of the two hot kernels.  One workgroup owns one tile of TILE keys in LDS.
-//   i32: 512 threads x 16 keys = 8192 keys = 32 KiB LDS per workgroup (4 workgroups / CU)
-//   i64: 512 threads x  8 keys = 4096 keys = 32 KiB LDS per workgroup
-// ----------------------------------------------------------------------------------------
-template <typename T> struct Geom;
-template <> struct Geom<int32_t> {
-    static constexpr int THREADS = 512;
-    static constexpr int K = 16;
-    static constexpr int TILE = THREADS * K;
-};
-#ifndef DSORT_T64
-#define DSORT_T64 512
-#endif
-#ifndef DSORT_K64
-#define DSORT_K64 8
-#endif
-template <> struct Geom<int64_t> {
-    static constexpr int THREADS = DSORT_T64;
-    static constexpr int K = DSORT_K64;
-    static constexpr int TILE = THREADS * K;
-};
-
-// ----------------------------------------------------------------------------------------
 // k-way merge passes.  A pass merges GROUPS of up to F sorted runs (F a power of two <= kMaxF)
 // that lie back to back; every group's output is cut into TILE-key output tiles, one workgroup
 // per tile.  Regular passes (the sort): runs of length R, groups of F runs, so every group is
 // a multiple of TILE long and tile j covers output [j*TILE, (j+1)*TILE).  Irregular passes (the
 // master merge, the multi-GPU receive merge): a table of groups with arbitrary run lengths.
 // ----------------------------------------------------------------------------------------
-constexpr int kMaxLogF = 6;
+constexpr int kMaxLogF = 5;
 constexpr int kMaxF = 1 << kMaxLogF;
 
 struct GroupK {
@@ -162,12 +139,16 @@ int sort_device(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipStream_t 
 template <typename T>
 int merge_device(dsort_ctx *ctx, const T *d_in, const size_t *lens, int k, T *d_out,
                  hipStream_t s, bool keep_stats = false);
-// int32 path on wave-register bitonic networks (dsort_wave.hip); sort_device/merge_device route
-// 32-bit keys here.  wave_merge_i32 with keep_stats leaves the statistics and per-launch events of
+// The wave-register bitonic kernels (dsort_wave.hip); sort_device/merge_device route both key
+// widths here.  wave_merge_* with keep_stats leaves the statistics and per-launch events of
 // the preceding local sort alone (the sample sort's final merge).
 int wave_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys, size_t n, hipStream_t s,
                   bool timed);
 int wave_merge_i32(dsort_ctx *ctx, const int32_t *d_in, const size_t *lens, int k, int32_t *d_out,
+                   hipStream_t s, bool keep_stats = false);
+int wave_sort_i64(dsort_ctx *ctx, const int64_t *d_in, int64_t *d_keys, size_t n, hipStream_t s,
+                  bool timed);
+int wave_merge_i64(dsort_ctx *ctx, const int64_t *d_in, const size_t *lens, int k, int64_t *d_out,
                    hipStream_t s, bool keep_stats = false);
 // Fault injection for the fault-tolerance tests and bench (BASELINE config C5): with
 // DSORT_OPT_KILL_AFTER_PASS = k the process SIGKILLs itself right after merge pass k of a local

@@ -1,39 +1,44 @@
-// dsort_wave.hip -- the int32 sort and merge on wave-wide register bitonic networks (gfx950).
+// dsort_wave.hip -- the sort and the k-way merge on wave-wide register bitonic networks (gfx950),
+// for 32-bit and 64-bit keys.
 //
 // Replaces merge_sort()/merge() (reference client.c:140-173) and the merge loop of
-// merge_chunks() (server.c:481-515) for 32-bit keys.  Same result as the legacy LDS merge-path
-// kernels of dsort_sort.hip (the input multiset in ascending signed order), different machine
-// mapping:
+// merge_chunks() (server.c:481-515).  Result: the input multiset in ascending signed order.
+// Machine mapping:
 //
 //   * A wave holds 1024 keys, 16 per lane.  Every merge step of the sort is a bitonic network
 //     executed in registers: compare-exchanges between registers of one lane, cross-lane ones
-//     through DPP (quad_perm, row_ror, row_shl/shr, row_mirror) and v_med3_i32 with a per-lane
-//     +-inf constant (one instruction gives the min to the lower lane and the max to the upper),
-//     and the two row-crossing bits by v_permlane16/32_swap transpositions.  No per-lane
-//     merge-path search and no data-dependent LDS addressing: LDS is only read and written with
-//     consecutive lanes on consecutive words.
-//   * block_sort_w_kernel: one workgroup (16 waves) sorts a TILE of 16384 keys: each wave sorts
-//     its 1024 keys in registers (Batcher network per lane, then bitonic merges of 32..1024),
-//     then four LDS levels merge runs of 1024 -> 16384.
+//     through DPP (quad_perm, row_ror, row_shl/shr, row_mirror) -- for int32 with v_med3_i32 and a
+//     per-lane +-inf constant (one instruction gives the min to the lower lane and the max to the
+//     upper), for int64 a 64-bit compare and a select by lane side -- and the two row-crossing
+//     bits by v_permlane16/32_swap transpositions.  No per-lane merge-path search and no
+//     data-dependent LDS addressing: LDS is only read and written with consecutive lanes on
+//     consecutive words.
+//   * block_sort_w_kernel: one workgroup (WAVES waves) sorts a TILE of WAVES * 1024 keys: each
+//     wave sorts its 1024 keys in registers (Batcher network per lane, then bitonic merges of
+//     32..1024), then log2(WAVES) LDS levels merge runs of 1024 -> TILE.
 //   * mergew_kernel: one workgroup merges one output tile of a k-way pass: the F input windows
 //     (cut by partk_kernel, dsort_part.h) are staged back to back in LDS and merged in log2(F)
 //     pairwise levels.
 //   * An LDS level cuts every pair of runs into windows of 1024 outputs.  The B run of a pair is
 //     kept descending in LDS (every level writes the groups that become B runs reversed), so
 //     after one 64-ary merge-path search for the window start (64 probes per step, ballot) the
-//     window is min(A[a0 + e], B[b0 + 1023 - e]) -- two ascending LDS reads and a v_min per key,
+//     window is min(A[a0 + e], B[b0 + 1023 - e]) -- two ascending LDS reads and a min per key,
 //     a bitonic sequence -- sorted by the 10-stage half-cleaner network.  Windows are held in
 //     registers across a barrier, so the level merges in place in one LDS buffer.
+//   Key types: int32 tiles of 16 waves (16384 keys, 64 KiB LDS, two workgroups per CU); int64
+//   tiles of 8 waves (8192 keys, 64 KiB).
 //
-// Algorithmic HBM traffic: 8 bytes per key for the tile sort and for every pass.
+// Algorithmic HBM traffic: 2 * sizeof(key) bytes per key for the tile sort and for every pass.
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
 
+#include <algorithm>
 #include <climits>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "dsort_bucket.h"
@@ -45,15 +50,29 @@ namespace wv {
 
 constexpr int R = 16;              // keys per lane
 constexpr int WK = 64 * R;         // keys per wave: one bitonic window
-constexpr int WAVES = 16;          // waves per workgroup
-constexpr int THREADS = 64 * WAVES;
-constexpr int TILE = WK * WAVES;   // keys per workgroup tile (64 KiB of LDS)
-constexpr int KMAX = INT32_MAX;
-constexpr int KMIN = INT32_MIN;
-constexpr int kWaveMaxLogF = 5;    // fan-in cap of one merge pass (<= 2 windows per wave)
+constexpr int kWaveMaxLogF = 5;    // fan-in cap of one merge pass
 constexpr int kWaveMaxF = 1 << kWaveMaxLogF;
-constexpr int SLACK = TILE / 32;   // cut tolerance of partk
-constexpr int TNOM = TILE - 2 * SLACK;
+
+#ifndef DSORT_MWAVES
+#define DSORT_MWAVES 16
+#endif
+// Per key type: waves of the tile sort and of the merge tile, and the occupancy they are
+// compiled for (waves per SIMD: two workgroups per CU).
+template <typename T> struct WG;
+template <> struct WG<int32_t> {
+    static constexpr int WAVES = 16, MWAVES = DSORT_MWAVES, OCC = 8, MAXLOGF = 5;
+};
+template <> struct WG<int64_t> {
+    // F = 32 would need 32 run heads of 64-bit keys per lane next to the window: it spills, so
+    // int64 passes stop at F = 16.
+    static constexpr int WAVES = 8, MWAVES = 8, OCC = 4, MAXLOGF = 4;
+};
+template <typename T> constexpr int TILE_OF = WK * WG<T>::WAVES;
+template <typename T> constexpr int MTILE_OF = WK * WG<T>::MWAVES;
+template <typename T> constexpr int MSLACK_OF = MTILE_OF<T> / 32;      // cut tolerance of partk
+template <typename T> constexpr int MTNOM_OF = MTILE_OF<T> - 2 * MSLACK_OF<T>;
+template <typename T> constexpr int KPC = 16 / (int)sizeof(T);         // keys per 16-byte chunk
+template <typename T> constexpr int LKPC = sizeof(T) == 4 ? 2 : 1;
 
 // DPP controls (gfx9 encoding)
 constexpr int QP_1032 = 0xB1;      // lane ^ 1
@@ -76,8 +95,6 @@ __device__ unsigned long long g_stamps[kStampTiles * 32];
         if ((threadIdx.x & 63) == 0 && (threadIdx.x >> 6) % 15 == 0 && blockIdx.x < kStampTiles) \
             g_stamps[blockIdx.x * 32 + (threadIdx.x >> 6 ? 16 : 0) + (k)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
-// wave 0's s_memrealtime (100 MHz, comparable across CUs) at tile start, staging start and end,
-// tile end, in free slots 13, 14, 15, 29
 #define RSTAMP(slot)                                                                          \
     do {                                                                                      \
         if (threadIdx.x == 0 && blockIdx.x < kStampTiles)                                     \
@@ -92,22 +109,58 @@ __device__ unsigned long long g_stamps[kStampTiles * 32];
     } while (0)
 #endif
 
+// ------------------------------------------------------------------------------------------
+// Key-type primitives.  `side` values are per-lane +-inf of the key type: -inf on lanes that
+// keep the min of a cross-lane compare-exchange, +inf on lanes that keep the max.
+// ------------------------------------------------------------------------------------------
 // median of three: with c = -inf it is min(a, b), with c = +inf max(a, b)
 __device__ __forceinline__ int med3(int a, int b, int c) {
     int r;
     asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
 }
+__device__ __forceinline__ int sel_side(int x, int p, int c) { return med3(x, p, c); }
+// int64 has no med3: the partner p is taken when it is below x on a min lane, above on a max
+// lane (either when equal)
+__device__ __forceinline__ int64_t sel_side(int64_t x, int64_t p, int64_t c) {
+    return ((c < 0) == (p < x)) ? p : x;
+}
 
 template <int CTRL>
 __device__ __forceinline__ int dpp(int x) {
     return __builtin_amdgcn_mov_dpp(x, CTRL, 0xF, 0xF, false);
 }
+__device__ __forceinline__ void split64(int64_t v, int &lo, int &hi) {
+    lo = (int)v;
+    hi = (int)(v >> 32);
+}
+__device__ __forceinline__ int64_t join64(int lo, int hi) {
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+template <int CTRL>
+__device__ __forceinline__ int64_t dpp(int64_t x) {
+    int lo, hi;
+    split64(x, lo, hi);
+    return join64(dpp<CTRL>(lo), dpp<CTRL>(hi));
+}
 
+// partner of lane ^ 4 within a row: banks 0,2 read the lane 4 above (row_shl:4), banks 1,3 the
+// lane 4 below (row_shr:4)
+__device__ __forceinline__ int xor4_partner(int x) {
+    int y;
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_mov_b32_dpp %0, %1 row_shl:4 row_mask:0xf bank_mask:0x5\n\t"
+        "v_mov_b32_dpp %0, %1 row_shr:4 row_mask:0xf bank_mask:0xa"
+        : "=&v"(y)
+        : "v"(x));
+    return y;
+}
 
 // compare-exchange with lane ^ 4: lanes in banks 0,2 (bit 2 clear) keep the min, banks 1,3 the
-// max; the DPP source of each half is the other half (row_shl:4 / row_shr:4)
-__device__ __forceinline__ int cex_xor4(int x) {
+// max; for int32 the DPP source of each half is the other half (row_shl:4 / row_shr:4) and the
+// min/max is fused into the DPP instruction
+__device__ __forceinline__ int cex_xor4(int x, int) {
     int y;
     asm volatile(
         "s_nop 1\n\t"
@@ -117,16 +170,23 @@ __device__ __forceinline__ int cex_xor4(int x) {
         : "v"(x));
     return y;
 }
+__device__ __forceinline__ int64_t cex_xor4(int64_t x, int64_t c2) {
+    int lo, hi;
+    split64(x, lo, hi);
+    return sel_side(x, join64(xor4_partner(lo), xor4_partner(hi)), c2);
+}
 
-__device__ __forceinline__ void cex(int &a, int &b) {
-    const int lo = a < b ? a : b;
-    const int hi = a < b ? b : a;
+template <typename T>
+__device__ __forceinline__ void cex(T &a, T &b) {
+    const T lo = a < b ? a : b;
+    const T hi = a < b ? b : a;
     a = lo;
     b = hi;
 }
 
 // +inf on lanes whose bit b is set (they keep the max of a compare-exchange), -inf elsewhere
-__device__ __forceinline__ int lane_side(int b) { return ((lane_id() >> b) & 1) ? KMAX : KMIN; }
+template <typename T>
+__device__ __forceinline__ T lane_side(int b) { return ((lane_id() >> b) & 1) ? key_max<T>() : key_min<T>(); }
 
 __device__ __forceinline__ void swap32(int &a, int &b) {
     const auto r = __builtin_amdgcn_permlane32_swap((unsigned)a, (unsigned)b, false, false);
@@ -137,6 +197,24 @@ __device__ __forceinline__ void swap16(int &a, int &b) {
     const auto r = __builtin_amdgcn_permlane16_swap((unsigned)a, (unsigned)b, false, false);
     a = (int)r[0];
     b = (int)r[1];
+}
+__device__ __forceinline__ void swap32(int64_t &a, int64_t &b) {
+    int al, ah, bl, bh;
+    split64(a, al, ah);
+    split64(b, bl, bh);
+    swap32(al, bl);
+    swap32(ah, bh);
+    a = join64(al, ah);
+    b = join64(bl, bh);
+}
+__device__ __forceinline__ void swap16(int64_t &a, int64_t &b) {
+    int al, ah, bl, bh;
+    split64(a, al, ah);
+    split64(b, bl, bh);
+    swap16(al, bl);
+    swap16(ah, bh);
+    a = join64(al, ah);
+    b = join64(bl, bh);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -152,7 +230,8 @@ __device__ __forceinline__ int out_lo(int t) {
     return ((t >> 4) & 1) << 7 | ((t >> 5) & 1) << 6 | (t & 15);
 }
 
-__device__ __forceinline__ void merge_net(int (&x)[R], int c0, int c1, int c2, int c3) {
+template <typename T>
+__device__ __forceinline__ void merge_net(T (&x)[R], T c0, T c1, T c2, T c3) {
 #pragma unroll
     for (int b = 3; b >= 0; --b) {  // element bits 9..6 = register bits 3..0
 #pragma unroll
@@ -171,19 +250,20 @@ __device__ __forceinline__ void merge_net(int (&x)[R], int c0, int c1, int c2, i
         cex(x[k], x[k + 2]);
     }
 #pragma unroll
-    for (int i = 0; i < R; ++i) x[i] = med3(x[i], dpp<ROW_ROR8>(x[i]), c3);
+    for (int i = 0; i < R; ++i) x[i] = sel_side(x[i], dpp<ROW_ROR8>(x[i]), c3);
 #pragma unroll
-    for (int i = 0; i < R; ++i) x[i] = cex_xor4(x[i]);
+    for (int i = 0; i < R; ++i) x[i] = cex_xor4(x[i], c2);
 #pragma unroll
-    for (int i = 0; i < R; ++i) x[i] = med3(x[i], dpp<QP_2301>(x[i]), c1);
+    for (int i = 0; i < R; ++i) x[i] = sel_side(x[i], dpp<QP_2301>(x[i]), c1);
 #pragma unroll
-    for (int i = 0; i < R; ++i) x[i] = med3(x[i], dpp<QP_1032>(x[i]), c0);
+    for (int i = 0; i < R; ++i) x[i] = sel_side(x[i], dpp<QP_1032>(x[i]), c0);
 }
 
 // ------------------------------------------------------------------------------------------
 // Sort of one wave's 1024 keys in registers, lane-major: x[i] at lane t is element 16 t + i.
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ void sort16(int (&v)[R]) {  // Batcher odd-even merge sort, 63 cex
+template <typename T>
+__device__ __forceinline__ void sort16(T (&v)[R]) {  // Batcher odd-even merge sort, 63 cex
 #pragma unroll
     for (int p = 1; p < R; p <<= 1) {
 #pragma unroll
@@ -201,24 +281,24 @@ __device__ __forceinline__ void sort16(int (&v)[R]) {  // Batcher odd-even merge
 }
 
 // Half-cleaner on element bit b of a lane-major wave (b <= 8).
-template <int B>
-__device__ __forceinline__ void hc_lane_major(int (&x)[R], const int (&c)[6]) {
+template <int B, typename T>
+__device__ __forceinline__ void hc_lane_major(T (&x)[R], const T (&c)[6]) {
     if constexpr (B <= 3) {
 #pragma unroll
         for (int i = 0; i < R; ++i)
             if (!(i & (1 << B))) cex(x[i], x[i | (1 << B)]);
     } else if constexpr (B == 4) {
 #pragma unroll
-        for (int i = 0; i < R; ++i) x[i] = med3(x[i], dpp<QP_1032>(x[i]), c[0]);
+        for (int i = 0; i < R; ++i) x[i] = sel_side(x[i], dpp<QP_1032>(x[i]), c[0]);
     } else if constexpr (B == 5) {
 #pragma unroll
-        for (int i = 0; i < R; ++i) x[i] = med3(x[i], dpp<QP_2301>(x[i]), c[1]);
+        for (int i = 0; i < R; ++i) x[i] = sel_side(x[i], dpp<QP_2301>(x[i]), c[1]);
     } else if constexpr (B == 6) {
 #pragma unroll
-        for (int i = 0; i < R; ++i) x[i] = cex_xor4(x[i]);
+        for (int i = 0; i < R; ++i) x[i] = cex_xor4(x[i], c[2]);
     } else if constexpr (B == 7) {
 #pragma unroll
-        for (int i = 0; i < R; ++i) x[i] = med3(x[i], dpp<ROW_ROR8>(x[i]), c[3]);
+        for (int i = 0; i < R; ++i) x[i] = sel_side(x[i], dpp<ROW_ROR8>(x[i]), c[3]);
     } else {  // B == 8: lane bit 4, through a permlane16 transposition with register bit 0
         static_assert(B == 8, "half-cleaner bit out of range");
 #pragma unroll
@@ -231,8 +311,8 @@ __device__ __forceinline__ void hc_lane_major(int (&x)[R], const int (&c)[6]) {
 }
 
 // Partner of the mirror stage of a merge of 2^M keys: lane t ^ (2^(M-4) - 1).
-template <int M>
-__device__ __forceinline__ int mirror_partner(int v) {
+template <int M, typename T>
+__device__ __forceinline__ T mirror_partner(T v) {
     if constexpr (M == 5) return dpp<QP_1032>(v);
     else if constexpr (M == 6) return dpp<QP_3210>(v);
     else if constexpr (M == 7) return dpp<ROW_HMIRROR>(v);
@@ -241,25 +321,26 @@ __device__ __forceinline__ int mirror_partner(int v) {
     else return __shfl_xor(v, 63);
 }
 
-template <int B, int M>
-__device__ __forceinline__ void hc_down(int (&x)[R], const int (&c)[6]) {
+template <int B, int M, typename T>
+__device__ __forceinline__ void hc_down(T (&x)[R], const T (&c)[6]) {
     hc_lane_major<B>(x, c);
     if constexpr (B > 0) hc_down<B - 1, M>(x, c);
 }
 
 // Merge of sorted (ascending) blocks of 2^(M-1) keys into blocks of 2^M: the first stage
 // compares element e with its mirror e ^ (2^M - 1), then half-cleaners on bits M-2 .. 0.
-template <int M>
-__device__ __forceinline__ void merge_lane_major(int (&x)[R], const int (&c)[6]) {
-    int y[R];
+template <int M, typename T>
+__device__ __forceinline__ void merge_lane_major(T (&x)[R], const T (&c)[6]) {
+    T y[R];
 #pragma unroll
-    for (int i = 0; i < R; ++i) y[i] = med3(x[i], mirror_partner<M>(x[R - 1 - i]), c[M - 5]);
+    for (int i = 0; i < R; ++i) y[i] = sel_side(x[i], mirror_partner<M>(x[R - 1 - i]), c[M - 5]);
 #pragma unroll
     for (int i = 0; i < R; ++i) x[i] = y[i];
     hc_down<M - 2, M>(x, c);
 }
 
-__device__ __forceinline__ void sort_wave(int (&x)[R], const int (&c)[6]) {
+template <typename T>
+__device__ __forceinline__ void sort_wave(T (&x)[R], const T (&c)[6]) {
     sort16(x);
     merge_lane_major<5>(x, c);
     merge_lane_major<6>(x, c);
@@ -279,10 +360,11 @@ __device__ __forceinline__ void sort_wave(int (&x)[R], const int (&c)[6]) {
 // that order they form a bitonic sequence.  Both operands are ascending LDS ranges
 // (s[pa + a0 + e] and s[pbe - b0 - 1023 + e]); when at least 1024 outputs remain from d0 a read
 // past either run lands on the other run's larger keys of the same pair and never wins the min
-// (DESIGN.md §3.3), so a full window needs one split search, 32 reads and 16 v_min.
+// (DESIGN.md §3.1), so a full window needs one split search, 32 reads and 16 min.
 
 // Number of A keys among the first d outputs of merge(A, B) (one 64-ary search, wave-uniform).
-__device__ __forceinline__ int coop_split_desc(const int *s, int pa, int na, int pbe, int nb, int d) {
+template <typename T>
+__device__ __forceinline__ int coop_split_desc(const T *s, int pa, int na, int pbe, int nb, int d) {
     int lo = d > nb ? d - nb : 0, hi = d < na ? d : na;
     const int lane = lane_id();
 #pragma unroll 1
@@ -304,13 +386,14 @@ __device__ __forceinline__ int coop_split_desc(const int *s, int pa, int na, int
 }
 
 // Full window: x[i] at lane t = min(s[ia0 + e], s[ib0 + e]), e = 64 i + t.
-__device__ __forceinline__ void load_min(const int *s, int ia0, int ib0, int (&x)[R]) {
+template <typename T>
+__device__ __forceinline__ void load_min(const T *s, int ia0, int ib0, T (&x)[R]) {
     const int t = lane_id();
-    const int *sa = s + ia0 + t;
-    const int *sb = s + ib0 + t;
+    const T *sa = s + ia0 + t;
+    const T *sb = s + ib0 + t;
 #pragma unroll
     for (int hlf = 0; hlf < 2; ++hlf) {
-        int vb[R / 2];
+        T vb[R / 2];
 #pragma unroll
         for (int k = 0; k < R / 2; ++k) {
             const int i = hlf * (R / 2) + k;
@@ -327,16 +410,17 @@ __device__ __forceinline__ void load_min(const int *s, int ia0, int ib0, int (&x
 
 // Pair of fewer than 1024 keys (one window, d0 = 0): A[e] for e < na, B[1023 - e] for
 // e >= 1024 - nb, +inf elsewhere.
-__device__ __forceinline__ void load_min_short(const int *s, int pa, int na, int pbe, int nb,
-                                               int (&x)[R]) {
+template <typename T>
+__device__ __forceinline__ void load_min_short(const T *s, int pa, int na, int pbe, int nb,
+                                               T (&x)[R]) {
     const int t = lane_id();
 #pragma unroll
     for (int i = 0; i < R; ++i) {
         const int e = 64 * i + t;
         int ib = pbe - 1023 + e;
         ib = ib < 0 ? 0 : ib;
-        const int va = e < na ? s[pa + e] : KMAX;
-        const int vb = e >= WK - nb ? s[ib] : KMAX;
+        const T va = e < na ? s[pa + e] : key_max<T>();
+        const T vb = e >= WK - nb ? s[ib] : key_max<T>();
         x[i] = va < vb ? va : vb;
     }
 }
@@ -347,8 +431,9 @@ struct WinD {
     int pa, na, nb, d0, skip, cnt, desc;
 };
 
-__device__ __forceinline__ void merge_window_desc(const int *s, const WinD &w, int (&x)[R], int c0,
-                                                  int c1, int c2, int c3) {
+template <typename T>
+__device__ __forceinline__ void merge_window_desc(const T *s, const WinD &w, T (&x)[R], T c0,
+                                                  T c1, T c2, T c3) {
     const int pbe = w.pa + w.na + w.nb - 1;
     if (w.na + w.nb >= WK) {
         const int a0 = coop_split_desc(s, w.pa, w.na, pbe, w.nb, w.d0);
@@ -361,12 +446,12 @@ __device__ __forceinline__ void merge_window_desc(const int *s, const WinD &w, i
 
 // Stores the kept outputs of a window: pair output position d lands at dst[ob + d] (ascending
 // group) or dst[ob + len - 1 - d] (descending group; LDS only: the last level is ascending).
-template <bool DESC, typename P>
-__device__ __forceinline__ void store_window_desc(P *dst, const WinD &w, int ob, int lo,
-                                                  const int (&x)[R]) {
+template <bool DESC, typename T>
+__device__ __forceinline__ void store_window_desc(T *dst, const WinD &w, int ob, int lo,
+                                                  const T (&x)[R]) {
     const bool part = w.skip != 0 || w.cnt != WK;
     if (!DESC || !w.desc) {
-        P *p = dst + ob + w.d0 + lo;
+        T *p = dst + ob + w.d0 + lo;
         if (!part) {
 #pragma unroll
             for (int i = 0; i < R; ++i) p[out_hi(i)] = x[i];
@@ -376,7 +461,7 @@ __device__ __forceinline__ void store_window_desc(P *dst, const WinD &w, int ob,
                 if ((unsigned)(out_hi(i) + lo - w.skip) < (unsigned)w.cnt) p[out_hi(i)] = x[i];
         }
     } else {
-        P *p = dst + ob + (w.na + w.nb - 1 - w.d0) - lo;
+        T *p = dst + ob + (w.na + w.nb - 1 - w.d0) - lo;
         if (!part) {
 #pragma unroll
             for (int i = 0; i < R; ++i) p[-out_hi(i)] = x[i];
@@ -388,16 +473,31 @@ __device__ __forceinline__ void store_window_desc(P *dst, const WinD &w, int ob,
     }
 }
 
+// 16-byte vector of keys
+template <typename T> struct V16;
+template <> struct V16<int32_t> {
+    using type = int4;
+    __device__ static void get(const int4 &v, int32_t *o) { o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w; }
+    __device__ static int4 make(const int32_t *o) { return make_int4(o[0], o[1], o[2], o[3]); }
+};
+template <> struct V16<int64_t> {
+    using type = longlong2;
+    __device__ static void get(const longlong2 &v, int64_t *o) { o[0] = v.x; o[1] = v.y; }
+    __device__ static longlong2 make(const int64_t *o) { return make_longlong2(o[0], o[1]); }
+};
+
 // ------------------------------------------------------------------------------------------
 // 1. Tile sort.
 // ------------------------------------------------------------------------------------------
 // tiles: NULL = tile j is keys [j * TILE, (j + 1) * TILE) of n; else tile j = tiles[j] (the
 // bucketed sort's tiles, which never cross a bucket), j < *ntiles.
-__global__ void __launch_bounds__(THREADS, 8) block_sort_w_kernel(const int *in, int *out,
-                                                                    uint64_t n, const uint4 *tiles,
-                                                                    const uint32_t *ntiles) {
+template <typename T>
+__global__ void __launch_bounds__(64 * WG<T>::WAVES, WG<T>::OCC) block_sort_w_kernel(
+    const T *in, T *out, uint64_t n, const uint4 *tiles, const uint32_t *ntiles) {
+    constexpr int TILE = TILE_OF<T>, N = KPC<T>;
+    using V = typename V16<T>::type;
     // `in` may alias `out`: every workgroup reads its tile before it writes it
-    __shared__ __attribute__((aligned(16))) int s[TILE + WK];  // + slack read by load_window
+    __shared__ __attribute__((aligned(16))) T s[TILE + WK];  // + slack read by load_window
     const int t = lane_id();
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
     uint64_t base;
@@ -412,27 +512,23 @@ __global__ void __launch_bounds__(THREADS, 8) block_sort_w_kernel(const int *in,
         const uint64_t rem = n - base;
         valid = rem < (uint64_t)TILE ? (int)rem : TILE;
     }
-    const int c[6] = {lane_side(0), lane_side(1), lane_side(2), lane_side(3), lane_side(4),
-                      lane_side(5)};
+    const T c[6] = {lane_side<T>(0), lane_side<T>(1), lane_side<T>(2), lane_side<T>(3), lane_side<T>(4),
+                    lane_side<T>(5)};
 
-    int x[R];
-    if (valid == TILE && (reinterpret_cast<uintptr_t>(in) & 15) == 0) {
-        const int4 *src = reinterpret_cast<const int4 *>(in + base) + w * (WK / 4);
+    // The wave's 1024 keys in any order (the order inside a wave is irrelevant before a sort):
+    // register N q + j of lane t holds key N (64 q + t) + j of the wave's range.
+    T x[R];
+    if (valid == TILE && (reinterpret_cast<uintptr_t>(in + base) & 15) == 0) {
+        const V *src = reinterpret_cast<const V *>(in + base) + w * (WK / N);
 #pragma unroll
-        for (int q = 0; q < R / 4; ++q) {
-            const int4 v = src[q * 64 + t];
-            x[4 * q] = v.x;
-            x[4 * q + 1] = v.y;
-            x[4 * q + 2] = v.z;
-            x[4 * q + 3] = v.w;
-        }
+        for (int q = 0; q < R / N; ++q) V16<T>::get(src[q * 64 + t], x + N * q);
     } else {
 #pragma unroll
-        for (int q = 0; q < R / 4; ++q) {
+        for (int q = 0; q < R / N; ++q) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int e = w * WK + 4 * (q * 64 + t) + j;
-                x[4 * q + j] = e < valid ? in[base + e] : KMAX;
+            for (int j = 0; j < N; ++j) {
+                const int e = w * WK + N * (q * 64 + t) + j;
+                x[N * q + j] = e < valid ? in[base + e] : key_max<T>();
             }
         }
     }
@@ -441,14 +537,18 @@ __global__ void __launch_bounds__(THREADS, 8) block_sort_w_kernel(const int *in,
     // stored descending
     {
         if (w & 1) {
-            int4 *dst = reinterpret_cast<int4 *>(s + w * WK + WK - R * (t + 1));
+            V *dst = reinterpret_cast<V *>(s + w * WK + WK - R * (t + 1));
 #pragma unroll
-            for (int q = 0; q < R / 4; ++q)
-                dst[3 - q] = make_int4(x[4 * q + 3], x[4 * q + 2], x[4 * q + 1], x[4 * q]);
+            for (int q = 0; q < R / N; ++q) {
+                T rv[N];
+#pragma unroll
+                for (int j = 0; j < N; ++j) rv[j] = x[R - 1 - (N * q + j)];
+                dst[q] = V16<T>::make(rv);
+            }
         } else {
-            int4 *dst = reinterpret_cast<int4 *>(s + w * WK + t * R);
+            V *dst = reinterpret_cast<V *>(s + w * WK + t * R);
 #pragma unroll
-            for (int q = 0; q < R / 4; ++q) dst[q] = make_int4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
+            for (int q = 0; q < R / N; ++q) dst[q] = V16<T>::make(x + N * q);
         }
     }
     __syncthreads();
@@ -476,18 +576,20 @@ __global__ void __launch_bounds__(THREADS, 8) block_sort_w_kernel(const int *in,
 // ------------------------------------------------------------------------------------------
 // 2. Merge of one output tile of a k-way pass (cuts from partk_kernel).
 // ------------------------------------------------------------------------------------------
-template <int LOGF, bool REG>
-__global__ void __launch_bounds__(THREADS, 8) mergew_kernel(const int *__restrict__ in,
-                                                            int *__restrict__ out, PassDesc pd,
-                                                            int tnom,
-                                                            const uint32_t *__restrict__ splits) {
+template <typename T, int LOGF, bool REG>
+__global__ void __launch_bounds__(64 * WG<T>::MWAVES, WG<T>::OCC) mergew_kernel(
+    const T *__restrict__ in, T *__restrict__ out, PassDesc pd, int tnom, const uint32_t *__restrict__ splits) {
+    constexpr int WAVES = WG<T>::MWAVES, THREADS = 64 * WAVES, TILE = MTILE_OF<T>;
+    constexpr int N = KPC<T>, LN = LKPC<T>;
+    using V = typename V16<T>::type;
     constexpr int F = 1 << LOGF;
     constexpr int MAXWIN = (WAVES + F / 2 + WAVES - 1) / WAVES;
-    __shared__ __attribute__((aligned(16))) int s[TILE + WK];  // + slack read by load_window
+    static_assert(WAVES * MAXWIN <= 64, "window table: one lane per window");
+    __shared__ __attribute__((aligned(16))) T s[TILE + WK];  // + slack read by load_window
     __shared__ int soff[F + 1];          // tile position of segment i (soff[F] = keys of the tile)
-    // Staging works on 16-byte-aligned chunks of 4 keys of each segment (absolute alignment):
+    // Staging works on 16-byte-aligned chunks of N keys of each segment (absolute alignment):
     __shared__ int cpre[F + 1];          // chunks before segment i (cpre[F] = chunks of the tile)
-    __shared__ int4 sinfo[F];            // cpre[i], soff[i], keys, first chunk - first key (-3..0)
+    __shared__ int4 sinfo[F];            // cpre[i], soff[i], keys, first chunk - first key
     __shared__ int64_t sa0[F];           // global index of the segment's first aligned chunk
     __shared__ uint64_t s_out;
     __shared__ int4 wtab_a[LOGF][WAVES * MAXWIN];  // per level and window: pa, na, nb, d0
@@ -514,10 +616,10 @@ __global__ void __launch_bounds__(THREADS, 8) mergew_kernel(const int *__restric
             before += __shfl_xor(before, o);
         }
         // aligned chunks of segment i (absolute 16-B alignment of &in[g])
-        const int mis = (int)((reinterpret_cast<uintptr_t>(in) >> 2) & 3);
+        const int mis = (int)((reinterpret_cast<uintptr_t>(in) / sizeof(T)) & (N - 1));
         const int64_t gs = (int64_t)(rs + s0);
-        const int64_t a0 = ((gs + mis) & ~(int64_t)3) - mis;
-        const int nc = len ? (int)((gs + len + mis + 3) >> 2) - (int)((gs + mis) >> 2) : 0;
+        const int64_t a0 = ((gs + mis) & ~(int64_t)(N - 1)) - mis;
+        const int nc = len ? (int)((gs + len + mis + N - 1) >> LN) - (int)((gs + mis) >> LN) : 0;
         int cinc = nc;
         for (int o = 1; o < F; o <<= 1) {
             const int v = __shfl_up(cinc, o);
@@ -541,18 +643,17 @@ __global__ void __launch_bounds__(THREADS, 8) mergew_kernel(const int *__restric
     if (nchunks == 0) return;  // empty tile (workgroup-uniform)
     STAMP(2);
     RSTAMP(14);
-    // Staging: chunk q (4 keys, 16-B aligned in global memory) is loaded by thread q % THREADS
+    // Staging: chunk q (N keys, 16-B aligned in global memory) is loaded by thread q % THREADS
     // with one dwordx4 (consecutive lanes on consecutive chunks of a segment: 1 KiB per wave
     // instruction); the keys of a chunk that lie outside its segment are dropped.  An aligned
     // 16-B block holding a key of the array never crosses a page, so edge chunks are safe; lanes
     // past the last chunk load the last chunk again and drop it.
     {
-        constexpr int NK = (TILE / 4 + kWaveMaxF + THREADS - 1) / THREADS;  // chunks per thread
-        int4 v[NK];
+        constexpr int NK = (TILE / N + kWaveMaxF + THREADS - 1) / THREADS;  // chunks per thread
+        V v[NK];
         int ebase[NK], lo4[NK], hi4[NK], dirk[NK], qc[NK], sg[NK];
         // All chunk addresses are computed branch-free and side by side (the searches of the NK
-        // chunks interleave), so the NK loads leave together; lanes past the last chunk load the
-        // last chunk again.
+        // chunks interleave), so the NK loads leave together.
 #pragma unroll
         for (int k = 0; k < NK; ++k) {
             const int q = threadIdx.x + k * THREADS;
@@ -567,65 +668,63 @@ __global__ void __launch_bounds__(THREADS, 8) mergew_kernel(const int *__restric
 #pragma unroll
         for (int k = 0; k < NK; ++k) {
             const int4 si = sinfo[sg[k]];
-            const int c = 4 * (qc[k] - si.x);
+            const int c = N * (qc[k] - si.x);
             const int off = si.w + c;  // key offset of the chunk in its segment
             // odd segments (B runs of level 0) are staged descending
             const bool odd = sg[k] & 1;
             dirk[k] = odd ? -1 : 1;
             ebase[k] = odd ? si.y + si.z - 1 - off : si.y + off;
-            lo4[k] = -off;  // valid j: -off <= j < len - off
+            lo4[k] = -off;  // valid jj: -off <= jj < len - off
             hi4[k] = threadIdx.x + k * THREADS < nchunks ? si.z - off : 0;
-            v[k] = *reinterpret_cast<const int4 *>(in + sa0[sg[k]] + c);
+            v[k] = *reinterpret_cast<const V *>(in + sa0[sg[k]] + c);
         }
         // Window table of every level, built from the segment offsets alone (they do not depend on
         // the keys): level l merges pairs of 2^l-segment groups; pair p is cut into ceil(len / 1024)
-        // windows; window k of the level goes to wave k % 16 (k < 16 * MAXWIN).  Wave l builds the
-        // table of level l while its staging loads are in flight.
-        if (w < LOGF) {
-            {
-                const int l = w;
-                const int npairs = F >> (l + 1);
-                int ps = 0, pm = 0, pe = 0, nw = 0;
-                if (t < npairs) {
-                    ps = soff[t << (l + 1)];
-                    pm = soff[((2 * t + 1) << l)];
-                    pe = soff[(t + 1) << (l + 1)];
-                    nw = (pe - ps + WK - 1) / WK;
+        // windows; window k of the level goes to wave k % WAVES (k < WAVES * MAXWIN).  Wave l
+        // builds the table of level l while its staging loads are in flight.
+        for (int l = w; l < LOGF; l += WAVES) {
+            const int npairs = F >> (l + 1);
+            int ps = 0, pm = 0, pe = 0, nw = 0;
+            if (t < npairs) {
+                ps = soff[t << (l + 1)];
+                pm = soff[((2 * t + 1) << l)];
+                pe = soff[(t + 1) << (l + 1)];
+                nw = (pe - ps + WK - 1) / WK;
+            }
+            int incl = nw;
+            for (int o = 1; o < 16; o <<= 1) {
+                const int vv = __shfl_up(incl, o);
+                if (t >= o) incl += vv;
+            }
+            // lane k (< WAVES * MAXWIN) describes window k: its pair is the number of pairs whose
+            // windows all come before k
+            int p = 0;
+            for (int q = 0; q < npairs; ++q) p += __builtin_amdgcn_readlane(incl, q) <= t ? 1 : 0;
+            const int pp = p < npairs ? p : 0;
+            const int fps = __shfl(ps, pp), fpm = __shfl(pm, pp), fpe = __shfl(pe, pp);
+            const int first = __shfl(incl - nw, pp);
+            if (t < WAVES * MAXWIN) {
+                int4 a = make_int4(0, 0, 0, 0), b = make_int4(0, 0, 0, 0);  // cnt 0: no window
+                if (p < npairs) {
+                    const int len = fpe - fps;
+                    const int dn = (t - first) * WK;  // nominal start of the window
+                    const int rem = len - dn;
+                    // the last window of a pair of >= 1024 keys is shifted to end at the pair's end
+                    const int d0 = rem < WK && len >= WK ? len - WK : dn;
+                    a = make_int4(fps, fpm - fps, fpe - fpm, d0);
+                    // groups that become the B run of the next level are stored descending
+                    b = make_int4(dn - d0, rem < WK ? rem : WK, (l + 1 < LOGF) && (p & 1), 0);
                 }
-                int incl = nw;
-                for (int o = 1; o < 16; o <<= 1) {
-                    const int v = __shfl_up(incl, o);
-                    if (t >= o) incl += v;
-                }
-                // lane k (< WAVES * MAXWIN) describes window k: its pair is the number of pairs whose
-                // windows all come before k
-                int p = 0;
-                for (int q = 0; q < npairs; ++q) p += __builtin_amdgcn_readlane(incl, q) <= t ? 1 : 0;
-                const int pp = p < npairs ? p : 0;
-                const int fps = __shfl(ps, pp), fpm = __shfl(pm, pp), fpe = __shfl(pe, pp);
-                const int first = __shfl(incl - nw, pp);
-                if (t < WAVES * MAXWIN) {
-                    int4 a = make_int4(0, 0, 0, 0), b = make_int4(0, 0, 0, 0);  // cnt 0: no window
-                    if (p < npairs) {
-                        const int len = fpe - fps;
-                        const int dn = (t - first) * WK;  // nominal start of the window
-                        const int rem = len - dn;
-                        // the last window of a pair of >= 1024 keys is shifted to end at the pair's end
-                        const int d0 = rem < WK && len >= WK ? len - WK : dn;
-                        a = make_int4(fps, fpm - fps, fpe - fpm, d0);
-                        // groups that become the B run of the next level are stored descending
-                        b = make_int4(dn - d0, rem < WK ? rem : WK, (l + 1 < LOGF) && (p & 1), 0);
-                    }
-                    wtab_a[l][t] = a;
-                    wtab_b[l][t] = b;
-                }
+                wtab_a[l][t] = a;
+                wtab_b[l][t] = b;
             }
         }
 #pragma unroll
         for (int k = 0; k < NK; ++k) {
-            const int vals[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+            T vals[N];
+            V16<T>::get(v[k], vals);
 #pragma unroll
-            for (int jj = 0; jj < 4; ++jj)
+            for (int jj = 0; jj < N; ++jj)
                 if (jj >= lo4[k] && jj < hi4[k]) s[ebase[k] + dirk[k] * jj] = vals[jj];
         }
     }
@@ -634,11 +733,11 @@ __global__ void __launch_bounds__(THREADS, 8) mergew_kernel(const int *__restric
     STAMP(4);
     RSTAMP(15);
 
-    const int c0 = lane_side(0), c1 = lane_side(1), c2 = lane_side(2), c3 = lane_side(3);
+    const T c0 = lane_side<T>(0), c1 = lane_side<T>(1), c2 = lane_side<T>(2), c3 = lane_side<T>(3);
     const int lo = out_lo(t);
     const uint64_t so = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(s_out >> 32)) << 32) |
                         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)s_out);
-    int *outp = out + so;
+    T *outp = out + so;
 #pragma unroll 1
     for (int l = 0; l < LOGF; ++l) {
         const bool last = l + 1 == LOGF;
@@ -655,7 +754,7 @@ __global__ void __launch_bounds__(THREADS, 8) mergew_kernel(const int *__restric
             win[h].cnt = __builtin_amdgcn_readfirstlane(b.y);
             win[h].desc = __builtin_amdgcn_readfirstlane(b.z);
         }
-        int x[MAXWIN][R];
+        T x[MAXWIN][R];
 #pragma unroll
         for (int h = 0; h < MAXWIN; ++h)
             if (win[h].cnt > 0) merge_window_desc(s, win[h], x[h], c0, c1, c2, c3);
@@ -683,35 +782,44 @@ static int ceil_log2(uint64_t x) {
     while ((1ull << p) < x) ++p;
     return p;
 }
+// log2(F) of each pass: as few passes as the cap allows (default F <= 16), the bits spread
+// evenly over them.
+template <typename T>
 static std::vector<int> plan_passes(const dsort_ctx *ctx, uint64_t runs) {
     std::vector<int> out;
     const int bits = ceil_log2(runs);
     if (bits == 0) return out;
-    const int cap = max_logf(ctx, 4, kWaveMaxLogF);
+    const int cap = max_logf(ctx, 4, WG<T>::MAXLOGF);
     const int P = (bits + cap - 1) / cap;
     for (int p = 0; p < P; ++p) out.push_back(bits / P + (p < bits % P ? 1 : 0));
     return out;
 }
 
-template <bool REG>
-static int launch_pass_w(dsort_ctx *ctx, const int *src, int *dst, const PassDesc &pd, int logf,
+template <typename T, bool REG>
+static int launch_pass_w(dsort_ctx *ctx, const T *src, T *dst, const PassDesc &pd, int logf,
                          uint64_t ntiles, hipStream_t s, bool timed) {
     int rc = ensure(ctx, &ctx->splits, &ctx->splits_bytes,
                     (size_t)(ntiles + 1) * (size_t)(1 << logf) * sizeof(uint32_t), "split vectors");
     if (rc) return rc;
     uint32_t *sp = static_cast<uint32_t *>(ctx->splits);
-    hipLaunchKernelGGL((partk_kernel<int32_t, REG>), dim3((unsigned)ceil_div(ntiles, 4)), dim3(256), 0,
-                       s, src, pd, TNOM, SLACK, sp, ntiles);
+    constexpr int TN = MTNOM_OF<T>;
+    hipLaunchKernelGGL((partk_kernel<T, REG>), dim3((unsigned)ceil_div(ntiles, 4)), dim3(256), 0, s, src, pd,
+                       TN, MSLACK_OF<T>, sp, ntiles);
     DSORT_HIP(ctx, hipGetLastError());
     const bool kt = timed && ctx->ev_ok && ctx->kev_used + 2 <= dsort_ctx::kMaxKev;
     if (kt) DSORT_HIP(ctx, hipEventRecord(ctx->kev[ctx->kev_used], s));
-    const dim3 grid((unsigned)ntiles), block(THREADS);
+    const dim3 grid((unsigned)ntiles), block(64 * WG<T>::MWAVES);
     switch (logf) {
-        case 1: hipLaunchKernelGGL((mergew_kernel<1, REG>), grid, block, 0, s, src, dst, pd, TNOM, sp); break;
-        case 2: hipLaunchKernelGGL((mergew_kernel<2, REG>), grid, block, 0, s, src, dst, pd, TNOM, sp); break;
-        case 3: hipLaunchKernelGGL((mergew_kernel<3, REG>), grid, block, 0, s, src, dst, pd, TNOM, sp); break;
-        case 4: hipLaunchKernelGGL((mergew_kernel<4, REG>), grid, block, 0, s, src, dst, pd, TNOM, sp); break;
-        case 5: hipLaunchKernelGGL((mergew_kernel<5, REG>), grid, block, 0, s, src, dst, pd, TNOM, sp); break;
+        case 1: hipLaunchKernelGGL((mergew_kernel<T, 1, REG>), grid, block, 0, s, src, dst, pd, TN, sp); break;
+        case 2: hipLaunchKernelGGL((mergew_kernel<T, 2, REG>), grid, block, 0, s, src, dst, pd, TN, sp); break;
+        case 3: hipLaunchKernelGGL((mergew_kernel<T, 3, REG>), grid, block, 0, s, src, dst, pd, TN, sp); break;
+        case 4: hipLaunchKernelGGL((mergew_kernel<T, 4, REG>), grid, block, 0, s, src, dst, pd, TN, sp); break;
+        case 5:
+            if constexpr (WG<T>::MAXLOGF >= 5) {
+                hipLaunchKernelGGL((mergew_kernel<T, 5, REG>), grid, block, 0, s, src, dst, pd, TN, sp);
+                break;
+            }
+            return set_err(ctx, DSORT_EINVAL, "bad pass fan-in");
         default: return set_err(ctx, DSORT_EINVAL, "bad pass fan-in");
     }
     DSORT_HIP(ctx, hipGetLastError());
@@ -723,12 +831,12 @@ static int launch_pass_w(dsort_ctx *ctx, const int *src, int *dst, const PassDes
 }
 
 // ---- bucketed sort (dsort_bucket.h) ------------------------------------------------------
-// Buckets of about 2^20 keys (64 tiles): at most 1024, and none below 2^25 keys
-// (DSORT_OPT_BUCKETS = 0 turns the partition off, B forces B buckets, DSORT_OPT_BUCKET_KEYS sets
-// the nominal bucket size).  At 2^30 keys the largest of the 1024 buckets stays below 128 tiles
-// (7 merge levels: F = 16, then F = 8), and the buckets of <= 64 runs take F = 8 twice
-// (per-bucket fan-in, below).  768 buckets of 1.4 M keys: 15.49-15.53 ms; 1024: 15.32-15.37 ms
-// (profiles/r1_bucket_fanin_ab.txt).  A nested sort (the splitter samples) never buckets.
+// Buckets of about 2^20 keys: at most 1024, and none below 2^25 keys (DSORT_OPT_BUCKETS = 0
+// turns the partition off, B forces B buckets, DSORT_OPT_BUCKET_KEYS sets the nominal bucket
+// size).  int32 at 2^30 keys: 1024 buckets of about 64 16K-key tiles; the largest stays below 128
+// tiles (7 merge levels: F = 16, then F = 8), and the buckets of <= 64 runs take F = 8 twice
+// (per-bucket fan-in, below).  int64: 1024 buckets of about 128 8K-key tiles.  A nested sort (the
+// splitter samples) never buckets.
 static int bucket_count(const dsort_ctx *ctx, uint64_t n) {
     if (ctx->nested) return 0;
     const int64_t forced = ctx->opt.buckets;
@@ -748,17 +856,17 @@ static int bucket_os(const dsort_ctx *ctx) {
     return v < 1 ? 1 : (v > 4096 ? 4096 : (int)v);
 }
 
-// Skewed bucket sizes.  When the mean bucket holds about 64 tiles (2^30 keys in 1024 buckets),
-// about half the buckets land above 64 runs and merge F = 16 then F = 8, the rest F = 8 twice.
-// Instead the first k buckets get 56 tiles' worth of samples (below 64 runs despite the sampling
-// spread) and the others share the rest, about 104 tiles each (below 128): most keys then take
-// the cheaper F = 8 first pass (profiles/r1_bucket_skew_sweep.txt: 52:100 .. 60:112 all within
-// 0.06 ms of 56:104).  Returns k and the samples per small / large bucket; DSORT_OPT_BUCKET_SKEW
-// = 0 turns it off.
+// Skewed bucket sizes (int32).  When the mean bucket holds about 64 tiles (2^30 keys in 1024
+// buckets), about half the buckets land above 64 runs and merge F = 16 then F = 8, the rest
+// F = 8 twice.  Instead the first k buckets get 56 tiles' worth of samples (below 64 runs despite
+// the sampling spread) and the others share the rest, about 104 tiles each (below 128): most keys
+// then take the cheaper F = 8 first pass (profiles/r1_bucket_skew_sweep.txt: 52:100 .. 60:112
+// all within 0.06 ms of 56:104).  Returns k and the samples per small / large bucket;
+// DSORT_OPT_BUCKET_SKEW = 0 turns it off.
 struct Skew { int k, kos, los; };
-static Skew bucket_skew(const dsort_ctx *ctx, uint64_t n, int B, int os) {
+static Skew bucket_skew(const dsort_ctx *ctx, uint64_t n, int B, int os, int tile) {
     if (!ctx->opt.bucket_skew) return Skew{0, 0, 0};
-    const double R = (double)n / ((double)B * TILE);  // mean tiles per bucket
+    const double R = (double)n / ((double)B * tile);  // mean tiles per bucket
     if (B < 16 || R <= 56.0 || R > 72.0) return Skew{0, 0, 0};
     const double small = 56.0, large = 104.0;
     const int k = (int)((double)B * (large - R) / (large - small));
@@ -770,7 +878,7 @@ static Skew bucket_skew(const dsort_ctx *ctx, uint64_t n, int B, int os) {
     return Skew{k, kos, los};
 }
 
-// Group tables of the merge passes inside buckets: pass p merges groups of up to 16
+// Group tables of the merge passes inside buckets: pass p merges groups of up to 2^bits
 // consecutive runs of one bucket; a bucket with a single run left is carried as a 1-run group.
 struct BucketPass {
     int logf;
@@ -778,55 +886,63 @@ struct BucketPass {
     size_t group_off, tile_off;  // in the group / tile_group staging
 };
 
-static int bucket_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys, size_t n,
-                           hipStream_t s, bool timed, int B) {
+template <typename T>
+static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipStream_t s, bool timed, int B) {
     using namespace bk;
+    using C = typename Comp<T>::C;
+    constexpr int TILE = TILE_OF<T>;
+    constexpr uint64_t ALIGN = KPC<T>;
     const int BP = 1 << ceil_log2((uint64_t)B);
-    const int subs = bucket_wg_subs<int32_t>(n);
-    const uint64_t G = ceil_div(n, (uint64_t)subs * BK_T * Geo<int32_t>::KPT);
+    const int subs = bucket_wg_subs<T>(n);
+    const uint64_t G = ceil_div(n, (uint64_t)subs * BK_T * Geo<T>::KPT);
     const uint64_t nchunk = ceil_div(G, BK_CHUNK);
-    const int os = bucket_os(ctx);
+    const int os = std::is_same<T, int32_t>::value ? bucket_os(ctx) : BK_OS;
     const uint32_t S = (uint32_t)B * (uint32_t)os;
     const uint64_t tmax = ceil_div(n, TILE) + 2 * (uint64_t)B;  // + a head and a tail per bucket
     // device arena: samples, splitters, counts, chunk sums, offsets, bucket starts, tile table
     size_t off = 0;
     auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
-    const size_t o_smp = take((size_t)S * 8), o_spl = take((size_t)BP * 8),
+    const size_t o_smp = take((size_t)S * sizeof(C)), o_spl = take((size_t)BP * sizeof(C)),
                  o_cnt = take((size_t)G * B * 4), o_part = take((size_t)nchunk * B * 8),
                  o_offs = take((size_t)G * B * 8), o_bst = take((size_t)(B + 1) * 8),
                  o_tt = take((size_t)tmax * sizeof(TileRef)), o_nt = take(4);
     int rc = ensure(ctx, &ctx->bucket, &ctx->bucket_bytes, off, "bucket partition");
     if (rc) return rc;
     char *a = static_cast<char *>(ctx->bucket);
-    int64_t *smp = reinterpret_cast<int64_t *>(a + o_smp);
-    int64_t *spl = reinterpret_cast<int64_t *>(a + o_spl);
+    C *smp = reinterpret_cast<C *>(a + o_smp);
+    C *spl = reinterpret_cast<C *>(a + o_spl);
     uint32_t *cnt = reinterpret_cast<uint32_t *>(a + o_cnt);
     uint64_t *part = reinterpret_cast<uint64_t *>(a + o_part);
     uint64_t *offs = reinterpret_cast<uint64_t *>(a + o_offs);
     uint64_t *bst = reinterpret_cast<uint64_t *>(a + o_bst);
     TileRef *tt = reinterpret_cast<TileRef *>(a + o_tt);
     uint32_t *ntl = reinterpret_cast<uint32_t *>(a + o_nt);
-    rc = ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, n * sizeof(int32_t), "sort scratch");
+    rc = ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, n * sizeof(T), "sort scratch");
     if (rc) return rc;
-    int32_t *scratch = static_cast<int32_t *>(ctx->scratch);
-    if (ctx->bucket_host_bytes < (size_t)(B + 1) * 8) {
+    T *scratch = static_cast<T *>(ctx->scratch);
+    const size_t hbytes = (std::is_same<T, int64_t>::value ? (size_t)BK_MAXB * BK_OS * sizeof(C) : 0) +
+                          (size_t)(BK_MAXB + 1) * 8;
+    if (ctx->bucket_host_bytes < hbytes) {
         if (ctx->bucket_host) (void)hipHostFree(ctx->bucket_host);
         ctx->bucket_host = nullptr;
         ctx->bucket_host_bytes = 0;
-        DSORT_HIP(ctx, hipHostMalloc(&ctx->bucket_host, (size_t)BK_MAXB * 8 + 8, hipHostMallocDefault));
-        ctx->bucket_host_bytes = (size_t)BK_MAXB * 8 + 8;
+        DSORT_HIP(ctx, hipHostMalloc(&ctx->bucket_host, hbytes, hipHostMallocDefault));
+        ctx->bucket_host_bytes = hbytes;
     }
     if (!ctx->bucket_ev && hipEventCreateWithFlags(&ctx->bucket_ev, hipEventDisableTiming) != hipSuccess)
         return set_err(ctx, DSORT_EHIP, "hipEventCreate");
-
-    // 1. splitters from a regular sample, sorted in (key, index) order by the int64 sort
-    hipLaunchKernelGGL(bucket_sample_kernel<int32_t>, dim3(ceil_div(S, 256)), dim3(256), 0, s, d_in, (uint64_t)n, smp, S);
+    uint64_t *hb;
+    // 1. splitters from a regular sample in (key, input index) order
+    hipLaunchKernelGGL(bucket_sample_kernel<T>, dim3(ceil_div(S, 256)), dim3(256), 0, s, d_in, (uint64_t)n, smp, S);
     DSORT_HIP(ctx, hipGetLastError());
-    ++ctx->nested;  // the sample sort never buckets and never fires the fault injection
-    rc = sort_device<int64_t>(ctx, smp, smp, S, s, false);
-    --ctx->nested;
-    if (rc) return rc;
-    // (the int64 sort reset the statistics and events; the int32 sort's start from here)
+    if constexpr (std::is_same<T, int32_t>::value) {
+        // int32 composites are int64 (key * 2^32 + index): sorted on the GPU by the int64 sort
+        ++ctx->nested;  // the sample sort never buckets and never fires the fault injection
+        rc = sort_device<int64_t>(ctx, smp, smp, S, s, false);
+        --ctx->nested;
+        if (rc) return rc;
+    }
+    // (the nested sort reset the statistics and events; this sort's start from here)
     ctx->stats = dsort_stats{};
     ctx->stats.keys_in = ctx->stats.keys_out = n;
     ctx->stats.tile_keys = TILE;
@@ -837,53 +953,65 @@ static int bucket_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys,
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[0], s));
         ctx->ev_mask |= 1u;
     }
-    const Skew sk = bucket_skew(ctx, n, B, os);
-    hipLaunchKernelGGL(bucket_splitter_kernel<int32_t>, dim3(1), dim3(BK_MAXB), 0, s, smp, B, BP, os, spl,
-                       sk.k, sk.kos, sk.los);
+    if constexpr (std::is_same<T, int32_t>::value) {
+        const Skew sk = bucket_skew(ctx, n, B, os, TILE);
+        hipLaunchKernelGGL(bucket_splitter_kernel<int32_t>, dim3(1), dim3(BK_MAXB), 0, s, smp, B, BP, os, spl,
+                           sk.k, sk.kos, sk.los);
+        hb = static_cast<uint64_t *>(ctx->bucket_host);
+    } else {
+        // int64 composites are 16-byte (key, index) pairs: the 32 B samples are sorted on the host
+        C *hs = static_cast<C *>(ctx->bucket_host);
+        DSORT_HIP(ctx, hipMemcpyAsync(hs, smp, (size_t)S * sizeof(C), hipMemcpyDeviceToHost, s));
+        DSORT_HIP(ctx, hipStreamSynchronize(s));
+        std::sort(hs, hs + S, [](const C &x, const C &y) { return Comp<T>::lt(x, y); });
+        for (int b = 0; b < BP; ++b) hs[b] = b < B - 1 ? hs[(size_t)(b + 1) * BK_OS - 1] : Comp<T>::inf();
+        DSORT_HIP(ctx, hipMemcpyAsync(spl, hs, (size_t)BP * sizeof(C), hipMemcpyHostToDevice, s));
+        hb = reinterpret_cast<uint64_t *>(hs + BK_MAXB * BK_OS);
+    }
     // 2. histograms, their scan, the scatter
-    hipLaunchKernelGGL(bucket_hist_kernel<int32_t>, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, B, BP, subs, cnt);
+    hipLaunchKernelGGL(bucket_hist_kernel<T>, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, B, BP, subs, cnt);
     hipLaunchKernelGGL(bucket_colsum_kernel, dim3((unsigned)nchunk), dim3(BK_MAXB), 0, s, cnt, (uint32_t)G, B, part);
     hipLaunchKernelGGL(bucket_scan_kernel, dim3(1), dim3(BK_MAXB), 0, s, part, (uint32_t)nchunk, B,
-                       (uint32_t)TILE, 4u, bst, tt, ntl);
+                       (uint32_t)TILE, (uint32_t)ALIGN, bst, tt, ntl);
     hipLaunchKernelGGL(bucket_offsets_kernel, dim3((unsigned)nchunk), dim3(BK_MAXB), 0, s, cnt, part, bst, (uint32_t)G, B, offs);
     DSORT_HIP(ctx, hipGetLastError());
     // bucket starts to the host (the pass plan depends on the bucket sizes); the host waits for
     // them while the scatter runs.  The scatter always writes the scratch buffer (never the
     // input: the context owns it); the tile sort then writes whichever buffer makes the last
     // pass land in d_keys.
-    uint64_t *hb = static_cast<uint64_t *>(ctx->bucket_host);
     DSORT_HIP(ctx, hipMemcpyAsync(hb, bst, (size_t)(B + 1) * 8, hipMemcpyDeviceToHost, s));
     DSORT_HIP(ctx, hipEventRecord(ctx->bucket_ev, s));
-    int32_t *part_out = scratch;
-#if DSORT_BK_LINES
-    hipLaunchKernelGGL(bucket_scatter_lines_kernel, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, B, BP, subs, offs, part_out);
-#else
-    hipLaunchKernelGGL(bucket_scatter_kernel<int32_t>, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, B, BP, subs, offs, part_out);
-#endif
+    T *part_out = scratch;
+    if constexpr (std::is_same<T, int32_t>::value && DSORT_BK_LINES) {
+        hipLaunchKernelGGL(bucket_scatter_lines_kernel, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl,
+                           B, BP, subs, offs, part_out);
+    } else {
+        hipLaunchKernelGGL(bucket_scatter_kernel<T>, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, B,
+                           BP, subs, offs, part_out);
+    }
     DSORT_HIP(ctx, hipGetLastError());
     DSORT_HIP(ctx, hipEventSynchronize(ctx->bucket_ev));
-    std::vector<uint64_t> bsz(B);
-    for (int b = 0; b < B; ++b) bsz[b] = hb[b + 1] - hb[b];
     if (hb[B] != n) return set_err(ctx, DSORT_EHIP, "bucket partition lost keys");
     // pass plan: the runs of every bucket; the largest bucket's run count R sets the merge
     // levels L = ceil(log2 R), split into the fewest passes of <= max_logf levels (larger passes
-    // first).  Pass p merges groups of 2^bits[p] consecutive runs inside each bucket.
+    // first).
     std::vector<std::vector<uint64_t>> runs(B);
     uint64_t maxruns = 1;
     for (int b = 0; b < B; ++b) {
-        // the tile sort's runs of bucket b (bucket_tiles: a 0..3-key head, then TILE-key tiles)
-        const uint64_t h = bucket_head(hb[b], bsz[b], 4);
+        // the tile sort's runs of bucket b (bucket_tiles: a head up to 16-byte alignment, then
+        // TILE-key tiles)
+        const uint64_t len = hb[b + 1] - hb[b], h = bucket_head(hb[b], len, ALIGN);
         if (h) runs[b].push_back(h);
-        for (uint64_t o = h; o < bsz[b]; o += TILE) runs[b].push_back(bsz[b] - o < (uint64_t)TILE ? bsz[b] - o : TILE);
+        for (uint64_t o = h; o < len; o += TILE) runs[b].push_back(len - o < (uint64_t)TILE ? len - o : TILE);
         maxruns = runs[b].size() > maxruns ? runs[b].size() : maxruns;
     }
-    const std::vector<int> pbits = plan_passes(ctx, maxruns);
+    const std::vector<int> pbits = plan_passes<T>(ctx, maxruns);
     const int passes = (int)pbits.size();
     ctx->stats.merge_passes = passes;
-    int32_t *bufs[2] = {d_keys, scratch};
+    T *bufs[2] = {d_keys, scratch};
     int cur = (passes % 2 == 0) ? 0 : 1;  // tile sort output; the passes end in d_keys
     // 3. tile sort inside the buckets
-    hipLaunchKernelGGL(block_sort_w_kernel, dim3((unsigned)tmax), dim3(THREADS), 0, s, part_out,
+    hipLaunchKernelGGL(block_sort_w_kernel<T>, dim3((unsigned)tmax), dim3(64 * WG<T>::WAVES), 0, s, part_out,
                        bufs[cur], (uint64_t)n, reinterpret_cast<const uint4 *>(tt), ntl);
     DSORT_HIP(ctx, hipGetLastError());
     if (timed && ctx->ev_ok) {
@@ -903,6 +1031,7 @@ static int bucket_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys,
     for (int p = passes - 1; p >= 0; --p) tail[p] = tail[p + 1] + pbits[p];
     std::vector<int> blev(B);
     for (int b = 0; b < B; ++b) blev[b] = ceil_log2((uint64_t)runs[b].size());
+    constexpr uint64_t MTN = MTNOM_OF<T>;
     for (int p = 0; p < passes; ++p) {
         std::vector<GroupK> pg;       // this pass's groups (base = global key position)
         std::vector<int> pk;          // kernel log2 fan-in of every group
@@ -947,7 +1076,7 @@ static int bucket_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys,
                 if (pk[g] != l) continue;
                 GroupK gk = pg[g];
                 gk.first_tile = tiles;
-                const uint64_t gt = ceil_div(gk.total, (uint64_t)TNOM);
+                const uint64_t gt = ceil_div(gk.total, MTN);
                 for (uint64_t k = 0; k < gt; ++k) tgroup.push_back((uint32_t)(groups.size() - bp.group_off));
                 tiles += gt;
                 groups.push_back(gk);
@@ -986,7 +1115,7 @@ static int bucket_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys,
         for (size_t q = 0; q < plan.size(); ++q) {
             PassDesc pd{(uint64_t)n, 0, 1 << plan[q].logf, (int)plan[q].ngroups, dg + plan[q].group_off};
             pd.tile_group = dt + plan[q].tile_off;
-            rc = launch_pass_w<false>(ctx, bufs[cur], bufs[cur ^ 1], pd, plan[q].logf, plan[q].ntiles, s, timed);
+            rc = launch_pass_w<T, false>(ctx, bufs[cur], bufs[cur ^ 1], pd, plan[q].logf, plan[q].ntiles, s, timed);
             if (rc) return rc;
             if (q + 1 == plan.size() || plan_pass[q + 1] != plan_pass[q]) {  // pass complete
                 cur ^= 1;
@@ -1001,17 +1130,9 @@ static int bucket_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys,
     return DSORT_OK;
 }
 
-}  // namespace wv
-
-#ifdef DSORT_STAMPS
-extern "C" int dsort_debug_stamps(void *host, size_t bytes) {
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(wv::g_stamps), bytes) == hipSuccess ? 0 : -1;
-}
-#endif
-
-int wave_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys, size_t n, hipStream_t s,
-                  bool timed) {
-    using namespace wv;
+template <typename T>
+static int wave_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipStream_t s, bool timed) {
+    constexpr int TILE = TILE_OF<T>;
     ctx->stats = dsort_stats{};
     ctx->stats.keys_in = n;
     ctx->stats.keys_out = n;
@@ -1021,41 +1142,44 @@ int wave_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys, size_t n
     ctx->last_stream = s;
     if (n < 2) {
         if (n == 1 && d_in != d_keys)
-            DSORT_HIP(ctx, hipMemcpyAsync(d_keys, d_in, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+            DSORT_HIP(ctx, hipMemcpyAsync(d_keys, d_in, sizeof(T), hipMemcpyDeviceToDevice, s));
         return DSORT_OK;
     }
-    if (const int B = bucket_count(ctx, n)) return bucket_sort_i32(ctx, d_in, d_keys, n, s, timed, B);
+    if (const int B = bucket_count(ctx, n)) return bucket_sort<T>(ctx, d_in, d_keys, n, s, timed, B);
     const uint64_t tiles = ceil_div(n, TILE);
-    const std::vector<int> plan = plan_passes(ctx, tiles);
+    const std::vector<int> plan = plan_passes<T>(ctx, tiles);
     const int passes = (int)plan.size();
     ctx->stats.merge_passes = passes;
-    int32_t *scratch = nullptr;
+    T *scratch = nullptr;
     if (passes > 0) {
-        int rc = ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, n * sizeof(int32_t), "sort scratch");
+        int rc = ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, n * sizeof(T), "sort scratch");
         if (rc) return rc;
-        scratch = static_cast<int32_t *>(ctx->scratch);
+        scratch = static_cast<T *>(ctx->scratch);
     }
-    int32_t *bufs[2] = {d_keys, scratch};
+    // ping-pong so that the last pass lands in d_keys; the tile sort reads d_in (which may alias
+    // d_keys)
+    T *bufs[2] = {d_keys, scratch};
     int cur = (passes % 2 == 0) ? 0 : 1;
     if (timed && ctx->ev_ok) {
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[0], s));
         ctx->ev_mask |= 1u;
     }
-    hipLaunchKernelGGL(block_sort_w_kernel, dim3((unsigned)tiles), dim3(THREADS), 0, s, d_in,
+    hipLaunchKernelGGL(block_sort_w_kernel<T>, dim3((unsigned)tiles), dim3(64 * WG<T>::WAVES), 0, s, d_in,
                        bufs[cur], (uint64_t)n, nullptr, nullptr);
     DSORT_HIP(ctx, hipGetLastError());
     if (timed && ctx->ev_ok) {
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[1], s));
         ctx->ev_mask |= 2u;
     }
+    constexpr uint64_t MTN = MTNOM_OF<T>;
     uint64_t Rr = TILE;
     for (int p = 0; p < passes; ++p) {
         PassDesc pd{(uint64_t)n, Rr, 1 << plan[p], 0, nullptr};
         const uint64_t gsize = Rr << plan[p];
         const uint64_t ngroups = ceil_div(n, gsize);
-        const uint64_t tpg = ceil_div(gsize, (uint64_t)TNOM);
-        const uint64_t mtiles = (ngroups - 1) * tpg + ceil_div(n - (ngroups - 1) * gsize, (uint64_t)TNOM);
-        int rc = launch_pass_w<true>(ctx, bufs[cur], bufs[cur ^ 1], pd, plan[p], mtiles, s, timed);
+        const uint64_t tpg = ceil_div(gsize, MTN);
+        const uint64_t mtiles = (ngroups - 1) * tpg + ceil_div(n - (ngroups - 1) * gsize, MTN);
+        int rc = launch_pass_w<T, true>(ctx, bufs[cur], bufs[cur ^ 1], pd, plan[p], mtiles, s, timed);
         if (rc) return rc;
         Rr <<= plan[p];
         cur ^= 1;
@@ -1068,10 +1192,13 @@ int wave_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys, size_t n
     return DSORT_OK;
 }
 
-int wave_merge_i32(dsort_ctx *ctx, const int32_t *d_in, const size_t *lens, int k, int32_t *d_out,
-                   hipStream_t s, bool keep_stats) {
-    using namespace wv;
-    constexpr int MAXF = 1 << kWaveMaxLogF;
+// k-way merge of back-to-back runs of arbitrary lengths (the master merge, server.c:481-515, and
+// the multi-GPU receive merge).  Up to 32 runs (int64: 16) merge in one pass; more runs merge in
+// levels of such groups.  Lower runs win ties at every level.
+template <typename T>
+static int wave_merge(dsort_ctx *ctx, const T *d_in, const size_t *lens, int k, T *d_out, hipStream_t s,
+                      bool keep_stats) {
+    constexpr int MAXF = 1 << WG<T>::MAXLOGF;
     if (!keep_stats) {
         ctx->stats = dsort_stats{};
         ctx->kev_used = 0;
@@ -1082,11 +1209,11 @@ int wave_merge_i32(dsort_ctx *ctx, const int32_t *d_in, const size_t *lens, int 
     for (int j = 0; j < k; ++j) n += lens[j];
     if (!keep_stats) {
         ctx->stats.keys_in = ctx->stats.keys_out = n;
-        ctx->stats.tile_keys = TILE;
+        ctx->stats.tile_keys = TILE_OF<T>;
     }
     if (n == 0) return DSORT_OK;
     if (k == 1) {
-        DSORT_HIP(ctx, hipMemcpyAsync(d_out, d_in, n * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+        DSORT_HIP(ctx, hipMemcpyAsync(d_out, d_in, n * sizeof(T), hipMemcpyDeviceToDevice, s));
         return DSORT_OK;
     }
     int levels = 0;
@@ -1094,14 +1221,15 @@ int wave_merge_i32(dsort_ctx *ctx, const int32_t *d_in, const size_t *lens, int 
     if (!keep_stats) ctx->stats.merge_passes = levels;
     int rc;
     if (levels > 1) {
-        rc = ensure(ctx, &ctx->scratch2, &ctx->scratch2_bytes, n * sizeof(int32_t), "merge scratch");
+        rc = ensure(ctx, &ctx->scratch2, &ctx->scratch2_bytes, n * sizeof(T), "merge scratch");
         if (rc) return rc;
     }
-    int32_t *dsts[2] = {d_out, static_cast<int32_t *>(ctx->scratch2)};
+    T *dsts[2] = {d_out, static_cast<T *>(ctx->scratch2)};
     int which = (levels % 2 == 1) ? 0 : 1;
-    const int32_t *src = d_in;
+    const T *src = d_in;
     if (!ctx->groups_ev && hipEventCreateWithFlags(&ctx->groups_ev, hipEventDisableTiming) != hipSuccess)
         return set_err(ctx, DSORT_EHIP, "hipEventCreate");
+    constexpr uint64_t MTN = MTNOM_OF<T>;
     for (int l = 0; l < levels; ++l) {
         const int nr = (int)rl.size();
         const int per = nr < MAXF ? nr : MAXF;
@@ -1136,7 +1264,7 @@ int wave_merge_i32(dsort_ctx *ctx, const int32_t *d_in, const size_t *lens, int 
             }
             for (int r = (int)gk.nruns + 1; r <= kMaxF; ++r) gk.roff[r] = tot;
             gk.total = tot;
-            tiles += ceil_div(tot, (uint64_t)TNOM);
+            tiles += ceil_div(tot, MTN);
             base += tot;
             next.push_back(tot);
         }
@@ -1144,14 +1272,37 @@ int wave_merge_i32(dsort_ctx *ctx, const int32_t *d_in, const size_t *lens, int 
         DSORT_HIP(ctx, hipEventRecord(ctx->groups_ev, s));
         ctx->groups_ev_pending = true;
         PassDesc pd{n, 0, 1 << logf, ng, static_cast<const GroupK *>(ctx->groups)};
-        int32_t *dst = dsts[which];
-        rc = launch_pass_w<false>(ctx, src, dst, pd, logf, tiles, s, false);
+        T *dst = dsts[which];
+        rc = launch_pass_w<T, false>(ctx, src, dst, pd, logf, tiles, s, false);
         if (rc) return rc;
         rl.swap(next);
         src = dst;
         which ^= 1;
     }
     return DSORT_OK;
+}
+
+}  // namespace wv
+
+#ifdef DSORT_STAMPS
+extern "C" int dsort_debug_stamps(void *host, size_t bytes) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(wv::g_stamps), bytes) == hipSuccess ? 0 : -1;
+}
+#endif
+
+int wave_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys, size_t n, hipStream_t s, bool timed) {
+    return wv::wave_sort<int32_t>(ctx, d_in, d_keys, n, s, timed);
+}
+int wave_sort_i64(dsort_ctx *ctx, const int64_t *d_in, int64_t *d_keys, size_t n, hipStream_t s, bool timed) {
+    return wv::wave_sort<int64_t>(ctx, d_in, d_keys, n, s, timed);
+}
+int wave_merge_i32(dsort_ctx *ctx, const int32_t *d_in, const size_t *lens, int k, int32_t *d_out, hipStream_t s,
+                   bool keep_stats) {
+    return wv::wave_merge<int32_t>(ctx, d_in, lens, k, d_out, s, keep_stats);
+}
+int wave_merge_i64(dsort_ctx *ctx, const int64_t *d_in, const size_t *lens, int k, int64_t *d_out, hipStream_t s,
+                   bool keep_stats) {
+    return wv::wave_merge<int64_t>(ctx, d_in, lens, k, d_out, s, keep_stats);
 }
 
 }  // namespace dsort

@@ -217,7 +217,7 @@ int samplesort_master(int argc, char **argv, const char *argv0) {
         o.key_bytes = 4;
     }
     const size_t kb = (size_t)o.key_bytes;
-    const size_t shm_bytes = (o.keys * kb) ? o.keys * kb : 1;
+    const size_t shm_bytes = o.keys > 0 ? o.keys * kb : 1;
     char shm_name[64];
     static int shm_seq;
     snprintf(shm_name, sizeof shm_name, "/dsort-ss-%d-%d", (int)getpid(), shm_seq++);
@@ -351,7 +351,7 @@ int samplesort_master(int argc, char **argv, const char *argv0) {
             alive[r] = 1;
         }
         uint32_t epoch = 0;
-        int go_sent = 0, finished = 0, world = o.n;
+        int go_sent = 0, finished = 0;
         double t_go = 0, t_fault = -1, t_plan = -1, t_end = 0;
         for (;;) {
             struct pollfd pf[SS_MAX_WORKERS];
@@ -447,7 +447,6 @@ int samplesort_master(int argc, char **argv, const char *argv0) {
                     }
                     reassign(o.n, alive, owner, o.next_live);
                     ++epoch;
-                    world = live;
                     char uid[DSORT_UNIQUE_ID_BYTES];
                     memset(uid, 0, sizeof uid);
                     if (o.transport == 0 && dsort_comm_unique_id(uid)) goto fail;

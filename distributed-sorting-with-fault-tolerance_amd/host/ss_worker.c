@@ -182,7 +182,7 @@ static int relay_alltoallv(void *user, const void *send, const size_t *sc, const
     const int P = w->world;
     uint64_t tot = 0;
     for (int d = 0; d < P; ++d) tot += sc[d];
-    char *req = (char *)malloc((size_t)P * 8 + tot);
+    char *req = (char *)calloc(1, (size_t)P * 8 + tot);
     if (!req) return 1;
     uint64_t off = (uint64_t)P * 8;
     for (int d = 0; d < P; ++d) {
@@ -279,7 +279,7 @@ int samplesort_worker(const char *host, int port, int device, int verbose) {
     const size_t kb = job.key_bytes;
     const int i64 = kb == 8;
     /* the master's chunk replicas: shared memory, pinned here for DMA */
-    const size_t shm_bytes = (job.n_total * kb) ? job.n_total * kb : 1;
+    const size_t shm_bytes = job.n_total > 0 ? job.n_total * kb : 1;
     int sfd = shm_open(job.shm_name, O_RDWR, 0600);
     char *rep = sfd < 0 ? MAP_FAILED : (char *)mmap(NULL, shm_bytes, PROT_READ | PROT_WRITE, MAP_SHARED, sfd, 0);
     if (rep == MAP_FAILED) {
