@@ -680,7 +680,7 @@ int dsort_finalize(dsort_ctx *ctx) {
     }
     void *bufs[] = {ctx->scratch, ctx->scratch2, ctx->splits, ctx->groups, ctx->io, ctx->io2, ctx->red,
                     ctx->local, ctx->recv, ctx->recv2, ctx->small, ctx->text_status,
-                    ctx->bucket};
+                    ctx->bucket, ctx->sub};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (ctx->red_host) (void)hipHostFree(ctx->red_host);
@@ -691,6 +691,8 @@ int dsort_finalize(dsort_ctx *ctx) {
     if (ctx->groups_ev) (void)hipEventDestroy(ctx->groups_ev);
     if (ctx->bucket_host) (void)hipHostFree(ctx->bucket_host);
     if (ctx->bucket_ev) (void)hipEventDestroy(ctx->bucket_ev);
+    if (ctx->sub_host) (void)hipHostFree(ctx->sub_host);
+    if (ctx->sub_ev) (void)hipEventDestroy(ctx->sub_ev);
     for (auto &e : ctx->ev)
         if (e) (void)hipEventDestroy(e);
     for (auto &e : ctx->kev)
@@ -718,10 +720,6 @@ int dsort_set_option(dsort_ctx *ctx, int option, int64_t v) {
             if (v < 1 || v > 4096) return set_err(ctx, DSORT_EINVAL, "DSORT_OPT_BUCKET_OVERSAMPLE: 1..4096");
             o.bucket_os = v;
             return DSORT_OK;
-        case DSORT_OPT_BUCKET_SKEW:
-            if (v != 0 && v != 1) return set_err(ctx, DSORT_EINVAL, "DSORT_OPT_BUCKET_SKEW: 0 or 1");
-            o.bucket_skew = v;
-            return DSORT_OK;
         case DSORT_OPT_MAX_FANIN_LOG2:
             if (v != -1 && (v < 1 || v > kMaxLogF)) return set_err(ctx, DSORT_EINVAL, "DSORT_OPT_MAX_FANIN_LOG2: -1 or 1..5");
             o.max_logf = v;
@@ -733,6 +731,18 @@ int dsort_set_option(dsort_ctx *ctx, int option, int64_t v) {
         case DSORT_OPT_KILL_IN_EXCHANGE:
             if (v != -1 && v != 1 && v != 2) return set_err(ctx, DSORT_EINVAL, "DSORT_OPT_KILL_IN_EXCHANGE: -1, 1 or 2");
             o.kill_in_exchange = v;
+            return DSORT_OK;
+        case DSORT_OPT_SUB_KEYS:
+            if (v < -1) return set_err(ctx, DSORT_EINVAL, "DSORT_OPT_SUB_KEYS: -1, 0 or >= 1");
+            ctx->opt.sub_keys = v;
+            return DSORT_OK;
+        case DSORT_OPT_SUB_OVERSAMPLE:
+            if (v != -1 && (v < 1 || v > 64)) return set_err(ctx, DSORT_EINVAL, "DSORT_OPT_SUB_OVERSAMPLE: -1 or 1..64");
+            ctx->opt.sub_os = v;
+            return DSORT_OK;
+        case DSORT_OPT_SUB_GATHER:
+            if (v != 0 && v != 1) return set_err(ctx, DSORT_EINVAL, "DSORT_OPT_SUB_GATHER: 0 or 1");
+            ctx->opt.sub_gather = v;
             return DSORT_OK;
         case DSORT_OPT_COMM_TIMEOUT_MS:
             if (v < 0) return set_err(ctx, DSORT_EINVAL, "DSORT_OPT_COMM_TIMEOUT_MS: >= 0");
@@ -750,11 +760,13 @@ int dsort_get_option(const dsort_ctx *ctx, int option, int64_t *v) {
         case DSORT_OPT_BUCKETS: *v = o.buckets; return DSORT_OK;
         case DSORT_OPT_BUCKET_KEYS: *v = o.bucket_keys; return DSORT_OK;
         case DSORT_OPT_BUCKET_OVERSAMPLE: *v = o.bucket_os; return DSORT_OK;
-        case DSORT_OPT_BUCKET_SKEW: *v = o.bucket_skew; return DSORT_OK;
         case DSORT_OPT_MAX_FANIN_LOG2: *v = o.max_logf; return DSORT_OK;
         case DSORT_OPT_KILL_AFTER_PASS: *v = o.kill_after_pass; return DSORT_OK;
         case DSORT_OPT_KILL_IN_EXCHANGE: *v = o.kill_in_exchange; return DSORT_OK;
         case DSORT_OPT_COMM_TIMEOUT_MS: *v = o.comm_timeout_ms; return DSORT_OK;
+        case DSORT_OPT_SUB_KEYS: *v = o.sub_keys; return DSORT_OK;
+        case DSORT_OPT_SUB_OVERSAMPLE: *v = o.sub_os; return DSORT_OK;
+        case DSORT_OPT_SUB_GATHER: *v = o.sub_gather; return DSORT_OK;
         default: return DSORT_EINVAL;
     }
 }

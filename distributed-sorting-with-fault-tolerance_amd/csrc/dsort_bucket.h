@@ -157,17 +157,13 @@ __global__ void __launch_bounds__(256) bucket_sample_kernel(const T *__restrict_
 }
 
 // splitter b = sample (b+1)*os - 1 of the sorted samples (os samples per bucket), b < B-1;
-// +inf up to BP.  With k > 0 the first k buckets take kos samples each and the rest los each
-// (skewed bucket sizes, see bucket_skew in dsort_wave.hip).
+// +inf up to BP
 template <typename T>
 __global__ void __launch_bounds__(BK_MAXB) bucket_splitter_kernel(const typename Comp<T>::C *__restrict__ smp,
                                                                  int B, int BP, int os,
-                                                                 typename Comp<T>::C *__restrict__ spl,
-                                                                 int k = 0, int kos = 0, int los = 0) {
+                                                                 typename Comp<T>::C *__restrict__ spl) {
     const int b = threadIdx.x;
-    const uint64_t idx = k == 0 ? (uint64_t)(b + 1) * os
-                       : b < k ? (uint64_t)(b + 1) * kos : (uint64_t)k * kos + (uint64_t)(b + 1 - k) * los;
-    if (b < BP) spl[b] = b < B - 1 ? smp[idx - 1] : Comp<T>::inf();
+    if (b < BP) spl[b] = b < B - 1 ? smp[(uint64_t)(b + 1) * os - 1] : Comp<T>::inf();
 }
 
 template <typename T>
@@ -335,18 +331,19 @@ static __global__ void __launch_bounds__(BK_MAXB) bucket_scan_kernel(uint64_t *_
 }
 
 // offs[g * B + b] = global position of workgroup g's first key of bucket b
-static __global__ void __launch_bounds__(BK_MAXB) bucket_offsets_kernel(const uint32_t *__restrict__ counts,
+template <typename O>
+__global__ void __launch_bounds__(BK_MAXB) bucket_offsets_kernel(const uint32_t *__restrict__ counts,
                                                                 const uint64_t *__restrict__ part,
                                                                 const uint64_t *__restrict__ bstart,
                                                                 uint32_t G, int B,
-                                                                uint64_t *__restrict__ offs) {
+                                                                O *__restrict__ offs) {
     const int b = threadIdx.x;
     if (b >= B) return;
     const uint32_t g0 = blockIdx.x * BK_CHUNK;
     const uint32_t g1 = g0 + BK_CHUNK < G ? g0 + BK_CHUNK : G;
     uint64_t run = bstart[b] + part[(uint64_t)blockIdx.x * B + b];
     for (uint32_t g = g0; g < g1; ++g) {
-        offs[(uint64_t)g * B + b] = run;
+        offs[(uint64_t)g * B + b] = (O)run;
         run += counts[(uint64_t)g * B + b];
     }
 }

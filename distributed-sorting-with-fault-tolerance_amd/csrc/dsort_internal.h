@@ -48,13 +48,15 @@ struct PassDesc {
 // Per-context options (dsort_set_option; defaults = the tuned values).
 struct dsort_opts {
     int64_t buckets = -1;           // DSORT_OPT_BUCKETS: -1 auto, 0 off, B forced
-    int64_t bucket_keys = 1 << 20;  // DSORT_OPT_BUCKET_KEYS (int32)
-    int64_t bucket_os = 256;        // DSORT_OPT_BUCKET_OVERSAMPLE (int32)
-    int64_t bucket_skew = 1;        // DSORT_OPT_BUCKET_SKEW (int32)
+    int64_t bucket_keys = 1 << 20;  // DSORT_OPT_BUCKET_KEYS
+    int64_t bucket_os = 256;        // DSORT_OPT_BUCKET_OVERSAMPLE
     int64_t max_logf = -1;          // DSORT_OPT_MAX_FANIN_LOG2: -1 = per key type default
     int64_t kill_after_pass = -1;   // DSORT_OPT_KILL_AFTER_PASS
     int64_t kill_in_exchange = -1;  // DSORT_OPT_KILL_IN_EXCHANGE
     int64_t comm_timeout_ms = 0;    // DSORT_OPT_COMM_TIMEOUT_MS
+    int64_t sub_keys = -1;          // DSORT_OPT_SUB_KEYS: -1 = TILE / 8, 0 = no second level
+    int64_t sub_os = -1;            // DSORT_OPT_SUB_OVERSAMPLE: -1 = 4
+    int64_t sub_gather = 1;         // DSORT_OPT_SUB_GATHER
 };
 
 // The context.  One per host thread, bound to one device.
@@ -88,6 +90,11 @@ struct dsort_ctx {
     void *bucket_host = nullptr;  // pinned: bucket starts
     size_t bucket_host_bytes = 0;
     hipEvent_t bucket_ev = nullptr;
+    void *sub = nullptr;          // second partition level (dsort_sub.h)
+    size_t sub_bytes = 0;
+    void *sub_host = nullptr;     // pinned: bucket table, chunk table, tile / merge-record counts
+    size_t sub_host_bytes = 0;
+    hipEvent_t sub_ev = nullptr;
     void *text_status = nullptr;  // per-tile look-back status words of the text codec
     size_t text_status_bytes = 0;
     void *red = nullptr;       // 64 B of reduction accumulators

@@ -1,0 +1,655 @@
+// dsort_sub.h -- the second partition level of the bucketed sort (namespace dsort::sb; included
+// by dsort_wave.hip).
+//
+// The first level (dsort_bucket.h) cuts the keys into B <= 1024 buckets of about 2^20 keys.  In
+// round 1 every bucket was then tile-sorted and merged in two k-way passes (64..128 tiles per
+// bucket), and those passes were half of the sort's time.  Here every bucket is cut once more,
+// into `nsub` sub-buckets of about TILE / 8 keys by splitters from a sample of the bucket, and
+// consecutive sub-buckets are packed into tiles of at most TILE keys.  A tile then holds exactly
+// the keys of its output range, so the tile sort finishes the sort: no merge pass at all.  A
+// sub-bucket that alone exceeds a tile (not expected from the sampling; possible for adversarial
+// inputs) is tile-sorted in pieces and merged afterwards (merge records, host side).
+//
+// Order: keys are compared as composites (key, position in the first level's output) and the
+// splitters are sampled composites, so equal keys spread over sub-buckets like any other
+// (DESIGN.md §3.2).
+//
+// Kernels:
+//   sb_sample_kernel    per bucket: ns = nsub * os keys at regular positions
+//   (the samples of all buckets sorted by (key, position) in one nested int64 sort of
+//   composites -- int64 keys first sort the keys and rank them, sb_rank_kernel -- bucket b's
+//   samples keep their range [soff, soff + ns) since the buckets are ordered)
+//   sb_splitter_kernel  per bucket: nsub - 1 splitters (key, position) + the slot table
+//   sb_hist_kernel      per chunk (<= SB_CH keys of one bucket): keys per sub-bucket
+//   sb_scan_kernel      per bucket: sub-bucket starts, per-chunk offsets, tile packing
+//   sb_scatter_kernel   per chunk: keys grouped by sub-bucket in LDS, written to their places
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dsort_bucket.h"
+
+namespace dsort {
+namespace sb {
+
+constexpr int SB_T = 256;              // threads of the per-chunk kernels
+constexpr int SB_MAXS = 1024;          // sub-buckets per bucket at most
+constexpr int SB_SLOTB = 10;           // slot table: 1024 key slots per bucket
+constexpr int SB_SLOTS = 1 << SB_SLOTB;
+constexpr int SB_ST = 4;               // sub-tiles per chunk
+#ifndef DSORT_SB_KPT32
+#define DSORT_SB_KPT32 16
+#endif
+#ifndef DSORT_SB_KPT64
+#define DSORT_SB_KPT64 8
+#endif
+template <typename T> constexpr int SB_KPT = sizeof(T) == 4 ? DSORT_SB_KPT32 : DSORT_SB_KPT64;  // keys per thread per sub-tile
+template <typename T> constexpr int SB_SUB = SB_T * SB_KPT<T>;   // keys of a sub-tile
+template <typename T> constexpr int SB_CH = SB_ST * SB_SUB<T>;   // keys of a chunk
+
+struct BInfo {       // one first-level bucket (host-built)
+    uint64_t start;  // first key (position in the first level's output)
+    uint64_t soff;   // first sample
+    uint32_t len;    // keys
+    uint32_t nsub;   // sub-buckets, 1..SB_MAXS
+    uint32_t ns;     // samples (0 when nsub == 1)
+    uint32_t c0, c1; // chunks [c0, c1)
+    uint32_t pad;
+};
+
+struct Chunk {
+    uint64_t start;
+    uint32_t len;
+    uint32_t b;
+};
+
+// Chunk c: from the table, or (ch == NULL: the first level, one segment) SB_CH<T>-key pieces of
+// segment 0 in order.
+template <typename T>
+__device__ __forceinline__ Chunk chunk_of(const Chunk *ch, const BInfo *bi, uint32_t c) {
+    if (ch) return ch[c];
+    const uint64_t o = (uint64_t)c * SB_CH<T>, len = bi[0].len;
+    return Chunk{bi[0].start + o, (uint32_t)(len - o < (uint64_t)SB_CH<T> ? len - o : (uint64_t)SB_CH<T>), 0u};
+}
+
+template <typename T> struct KeyU;
+template <> struct KeyU<int32_t> { using U = uint32_t; };
+template <> struct KeyU<int64_t> { using U = uint64_t; };
+
+template <typename T>
+struct SlotFn {      // slot(key) = (clamp(key, klo, ..) - klo) >> sh, capped at SB_SLOTS - 1
+    T klo;
+    uint32_t sh;
+    uint32_t pad;
+};
+
+template <typename T>
+__host__ __device__ __forceinline__ uint32_t slot_of(T key, T klo, uint32_t sh) {
+    using U = typename KeyU<T>::U;
+    const U d = key < klo ? (U)0 : (U)((U)key - (U)klo);
+    const U s = d >> sh;
+    return s > (U)(SB_SLOTS - 1) ? (uint32_t)(SB_SLOTS - 1) : (uint32_t)s;
+}
+
+// A splitter: key and position (8 bytes for int32 keys, 16 for int64: one LDS read).
+template <typename T> struct Spl;
+template <> struct __attribute__((aligned(8))) Spl<int32_t> {
+    int32_t k;
+    uint32_t p;
+};
+template <> struct __attribute__((aligned(16))) Spl<int64_t> {
+    int64_t k;
+    uint32_t p, pad;
+};
+
+// splitter s lies below key `key` at position `pos`
+template <typename T>
+__device__ __forceinline__ bool below(const Spl<T> &s, T key, uint32_t pos) {
+    return s.k < key || (s.k == key && s.p <= pos);
+}
+
+// sub-bucket of (key, pos): the number of splitters below it.  Splitters outside the key's
+// slot are below it iff their slot is lower (slot_of is monotone), so only the slot's own
+// splitters are searched -- usually none or one.
+template <typename T>
+__device__ __forceinline__ int sub_of(const Spl<T> *spl, const uint32_t *rng, T klo, uint32_t sh, T key,
+                                      uint32_t pos) {
+    const uint32_t r = rng[slot_of<T>(key, klo, sh)];
+    int lo = (int)(r & 0xFFFF);
+    const int hi = (int)(r >> 16);
+    // the first two splitters of the slot without a branch (the table holds SB_MAXS entries, so
+    // the reads stay inside it), then the rare crowded slot
+    const Spl<T> a = spl[lo], b = spl[lo + 1];
+    const int j = lo + (lo < hi && below<T>(a, key, pos) ? 1 + (lo + 1 < hi && below<T>(b, key, pos)) : 0);
+    if (j < lo + 2 || j >= hi) return j;
+    lo = j;
+    int h = hi;
+    while (lo < h) {
+        const int mid = (lo + h) >> 1;
+        if (below<T>(spl[mid], key, pos)) lo = mid + 1;
+        else h = mid;
+    }
+    return lo;
+}
+
+// Sample g (global index, bucket b's samples at [soff, soff + ns)) = the key at position
+// start + ((2k + 1) * len) / (2 ns), k = g - soff.  Written as the key (smp) and, for int32, as
+// the composite key * 2^32 + g (cmp), whose sort orders the samples by (key, position).
+__host__ __device__ __forceinline__ uint64_t sample_pos(const BInfo &b, uint64_t k) {
+    return b.start + ((2 * k + 1) * b.len) / (2 * (uint64_t)b.ns);
+}
+template <typename T>
+__global__ void __launch_bounds__(SB_T) sb_sample_kernel(const T *__restrict__ src, const BInfo *__restrict__ bi,
+                                                         T *__restrict__ smp, int64_t *__restrict__ cmp) {
+    const BInfo b = bi[blockIdx.x];
+    for (uint32_t k = threadIdx.x; k < b.ns; k += SB_T) {
+        const T key = src[sample_pos(b, k)];
+        const uint64_t g = b.soff + k;
+        smp[g] = key;
+        if constexpr (sizeof(T) == 4) cmp[g] = (int64_t)((uint64_t)(int64_t)key << 32 | (uint32_t)g);
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ uint32_t lower_bound_k(const T *a, uint32_t n, T k) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a[mid] < k) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+template <typename T>
+__device__ __forceinline__ uint32_t upper_bound_k(const T *a, uint32_t n, T k) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (!(k < a[mid])) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// int64 keys do not fit a composite with the sample index: once the keys are sorted (srt), the
+// composite of sample g is (index of the first sample equal to its key in srt) * 2^32 + g, whose
+// sort orders the samples by (key, position) as well.
+__global__ void __launch_bounds__(SB_T) sb_rank_kernel(const int64_t *__restrict__ smp, const int64_t *__restrict__ srt,
+                                                       const BInfo *__restrict__ bi, int64_t *__restrict__ cmp) {
+    const BInfo b = bi[blockIdx.x];
+    for (uint32_t k = threadIdx.x; k < b.ns; k += SB_T) {
+        const uint64_t g = b.soff + k;
+        const uint64_t lo = b.soff + lower_bound_k<int64_t>(srt + b.soff, b.ns, smp[g]);
+        cmp[g] = (int64_t)(lo << 32 | (uint32_t)g);
+    }
+}
+
+// Splitter j of bucket b (j < nsub - 1) = the sample of rank (j + 1) * os - 1 in (key, position)
+// order: its key and position.  Keys are compared as (key, position in the first level's
+// output), so duplicates split over sub-buckets exactly like distinct keys (sizes depend on the
+// sample positions only).  Then the slot table: rng[s] = (splitters with slot < s) |
+// (splitters with slot <= s) << 16.
+template <typename T>
+__global__ void __launch_bounds__(SB_MAXS) sb_splitter_kernel(const int64_t *__restrict__ cmp, const T *__restrict__ smp,
+                                                              const BInfo *__restrict__ bi, int os, int SS,
+                                                              Spl<T> *__restrict__ spl, uint32_t *__restrict__ rng,
+                                                              SlotFn<T> *__restrict__ sfn) {
+    using U = typename KeyU<T>::U;
+    __shared__ uint32_t sslot[SB_MAXS];
+    const BInfo b = bi[blockIdx.x];
+    const int tid = threadIdx.x;
+    const int nspl = (int)b.nsub - 1;
+    T klo = 0;
+    uint32_t sh = 0;
+    if (nspl > 0) {
+        const int64_t *cm = cmp + b.soff;
+        klo = smp[(uint32_t)cm[0]];
+        const U span = (U)((U)smp[(uint32_t)cm[b.ns - 1]] - (U)klo);
+        while (sh < 8 * sizeof(T) && (span >> sh) >= (U)SB_SLOTS) ++sh;
+        if (tid < nspl) {
+            const uint32_t g = (uint32_t)cm[(uint32_t)(tid + 1) * (uint32_t)os - 1];
+            const T K = smp[g];
+            Spl<T> sp{};
+            sp.k = K;
+            sp.p = (uint32_t)sample_pos(b, g - b.soff);
+            spl[(uint64_t)blockIdx.x * SS + tid] = sp;
+            sslot[tid] = slot_of<T>(K, klo, sh);
+        }
+    }
+    __syncthreads();
+    for (int s = tid; s < SB_SLOTS; s += SB_MAXS) {
+        uint32_t lo = 0, hi = (uint32_t)(nspl > 0 ? nspl : 0);
+        while (lo < hi) {  // first splitter with slot >= s
+            const uint32_t mid = (lo + hi) >> 1;
+            if (sslot[mid] < (uint32_t)s) lo = mid + 1;
+            else hi = mid;
+        }
+        uint32_t lo2 = lo, hi2 = (uint32_t)(nspl > 0 ? nspl : 0);
+        while (lo2 < hi2) {  // first splitter with slot > s
+            const uint32_t mid = (lo2 + hi2) >> 1;
+            if (sslot[mid] <= (uint32_t)s) lo2 = mid + 1;
+            else hi2 = mid;
+        }
+        rng[(uint64_t)blockIdx.x * SB_SLOTS + s] = lo | (lo2 << 16);
+    }
+    if (tid == 0) sfn[blockIdx.x] = SlotFn<T>{klo, sh, 0};
+}
+
+template <typename T>
+__device__ __forceinline__ void load_sub_tables(const BInfo &b, uint32_t bid, int SS, const Spl<T> *spl_g,
+                                                const uint32_t *rng_g, Spl<T> *spl, uint32_t *rng) {
+    const int nspl = (int)b.nsub - 1;
+    for (int j = threadIdx.x; j < nspl; j += blockDim.x) spl[j] = spl_g[(uint64_t)bid * SS + j];
+    for (int s = threadIdx.x; s < SB_SLOTS; s += blockDim.x) rng[s] = rng_g[(uint64_t)bid * SB_SLOTS + s];
+}
+
+// counts[c * SS + j] = keys of chunk c in sub-bucket j of its bucket
+template <typename T>
+__global__ void __launch_bounds__(SB_T) sb_hist_kernel(const T *__restrict__ src, const Chunk *__restrict__ ch,
+                                                       const BInfo *__restrict__ bi, int SS,
+                                                       const Spl<T> *__restrict__ spl_g,
+                                                       const uint32_t *__restrict__ rng_g,
+                                                       const SlotFn<T> *__restrict__ sfn,
+                                                       uint32_t *__restrict__ counts) {
+    __shared__ Spl<T> spl[SB_MAXS + 1];  // + 1: sub_of reads two entries
+    __shared__ uint32_t rng[SB_SLOTS];
+    __shared__ uint32_t hist[SB_MAXS];
+    const Chunk c = chunk_of<T>(ch, bi, blockIdx.x);
+    const BInfo b = bi[c.b];
+    uint32_t *out = counts + (uint64_t)blockIdx.x * SS;
+    if (b.nsub == 1) {
+        if (threadIdx.x == 0) out[0] = c.len;
+        return;
+    }
+    load_sub_tables<T>(b, c.b, SS, spl_g, rng_g, spl, rng);
+    for (int j = threadIdx.x; j < (int)b.nsub; j += SB_T) hist[j] = 0;
+    const SlotFn<T> f = sfn[c.b];
+    __syncthreads();
+    constexpr int UN = 8;
+#pragma unroll 1
+    for (uint32_t i0 = 0; i0 < c.len; i0 += UN * SB_T) {
+        T key[UN];
+#pragma unroll
+        for (int u = 0; u < UN; ++u) {
+            const uint32_t i = i0 + threadIdx.x + u * SB_T;
+            key[u] = i < c.len ? src[c.start + i] : T(0);
+        }
+#pragma unroll
+        for (int u = 0; u < UN; ++u) {
+            const uint32_t i = i0 + threadIdx.x + u * SB_T;
+            if (i < c.len)
+                atomicAdd(&hist[sub_of<T>(spl, rng, f.klo, f.sh, key[u], (uint32_t)(c.start + i))], 1u);
+        }
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < (int)b.nsub; j += SB_T) out[j] = hist[j];
+}
+
+// exclusive scan over a SB_MAXS-thread workgroup (one value per thread); `all` = total
+__device__ __forceinline__ uint32_t scan_excl_1024(uint32_t v, uint32_t *wsum, uint32_t &all) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t incl = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    __syncthreads();
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t off = 0;
+    all = 0;
+    for (int i = 0; i < SB_MAXS / 64; ++i) {
+        const uint32_t x = wsum[i];
+        off += i < w ? x : 0;
+        all += x;
+    }
+    return off + incl - v;
+}
+
+// Packing of sub-buckets into tiles (host mirror: sub_tile_runs in dsort_wave.hip).  A tile
+// starting at position p may hold TILE - off(p) keys, off(p) = (p + mis) mod ALIGN (the tile
+// sort loads 16-byte-aligned vectors from p - off(p)).  Tiles are greedy: a tile starting with
+// sub-bucket i takes i, i+1, .. while they fit.  A sub-bucket that alone exceeds its tile's room
+// becomes pieces: TILE - off(p) keys, then TILE-key pieces, merged afterwards (merge record).
+struct Ovf {
+    uint64_t start;
+    uint64_t len;
+};
+
+// A tile of the local-partition path: sub-buckets [j0, j1) of bucket b, `valid` keys, output
+// position `base`; the tile sort gathers one piece per chunk of the bucket.
+struct GTile {
+    uint64_t base;
+    uint32_t valid, b, j0, j1;
+    uint64_t pad;
+};
+
+// What the gathering tile sort needs (block_sort_w_kernel<T, true>): its tiles, the chunk and
+// bucket tables and the chunks' prefix tables (pref[c * (SS + 1) + j]).
+struct Gather {
+    const GTile *tiles;
+    const Chunk *ch;
+    const BInfo *bi;
+    const uint32_t *pref;
+    int SS;
+};
+
+// LOCAL: the chunk histograms are the prefix tables of sb_local_kernel (pref[c][j+1] -
+// pref[c][j]); tiles are GTiles and a tile has no alignment constraint (room = tile); an
+// oversized sub-bucket only counts in novf (the host then takes the scatter path).
+// SCATTER: counts[c][j]; the per-chunk offsets of the scatter are written too; tiles are
+// TileRefs.
+template <bool LOCAL>
+__global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restrict__ bi, int SS,
+                                                          const uint32_t *__restrict__ counts,
+                                                          uint32_t *__restrict__ offs, int tile, int align,
+                                                          uint32_t mis, void *__restrict__ tiles,
+                                                          uint32_t *__restrict__ ntiles, Ovf *__restrict__ ovf,
+                                                          uint32_t *__restrict__ novf) {
+    __shared__ uint32_t wsum[SB_MAXS / 64];
+    __shared__ uint32_t ss[SB_MAXS + 1];   // sub-bucket starts (positions)
+    __shared__ uint16_t nxt[SB_MAXS];      // first sub-bucket after the tile starting at i
+    __shared__ uint16_t chain[SB_MAXS];    // sub-buckets that start a tile
+    __shared__ uint32_t nchain, tbase;
+    const BInfo b = bi[blockIdx.x];
+    const int j = threadIdx.x;
+    const int ns = (int)b.nsub;
+    auto cnt = [&](uint32_t c) -> uint32_t {
+        if constexpr (LOCAL) {
+            const uint32_t *pc = counts + (uint64_t)c * (SS + 1);
+            return pc[j + 1] - pc[j];
+        } else {
+            return counts[(uint64_t)c * SS + j];
+        }
+    };
+    uint32_t tot = 0;
+    if (j < ns)
+        for (uint32_t c = b.c0; c < b.c1; ++c) tot += cnt(c);
+    uint32_t all;
+    const uint32_t ex = scan_excl_1024(tot, wsum, all);
+    const uint32_t st = (uint32_t)b.start + ex;
+    if (j < ns) {
+        if constexpr (!LOCAL) {
+            uint32_t run = st;
+            for (uint32_t c = b.c0; c < b.c1; ++c) {
+                offs[(uint64_t)c * SS + j] = run;
+                run += cnt(c);
+            }
+        }
+        ss[j] = st;
+    }
+    if (j == 0) ss[ns] = (uint32_t)b.start + b.len;
+    __syncthreads();
+    if (j < ns) {
+        const uint32_t p = ss[j];
+        const uint32_t room = (uint32_t)tile - ((p + mis) & (uint32_t)(align - 1));
+        // last e in (j, ns] with ss[e] - p <= room
+        int lo = j + 1, hi = ns;  // answer in [j, ns]; ss[j] - p = 0 <= room
+        int e = j;
+        while (lo <= hi) {
+            const int mid = (lo + hi) >> 1;
+            if (ss[mid] - p <= room) {
+                e = mid;
+                lo = mid + 1;
+            } else {
+                hi = mid - 1;
+            }
+        }
+        nxt[j] = (uint16_t)(e > j ? e : j + 1);  // e == j: sub-bucket j alone is too large
+    }
+    __syncthreads();
+    if (j == 0) {
+        int k = 0;
+        for (int i = 0; i < ns; i = nxt[i]) chain[k++] = (uint16_t)i;
+        nchain = (uint32_t)k;
+    }
+    __syncthreads();
+    const int nc = (int)nchain;
+    uint32_t nt = 0, i0 = 0, i1 = 0, room = 0;
+    bool over = false;
+    if (j < nc) {
+        i0 = chain[j];
+        i1 = nxt[i0];
+        const uint32_t p = ss[i0], len = ss[i1] - p;
+        room = (uint32_t)tile - ((p + mis) & (uint32_t)(align - 1));
+        over = len > room;
+        nt = len == 0 ? 0 : over ? (LOCAL ? 0 : 1 + (len - room + tile - 1) / tile) : 1;
+        if (LOCAL && over) atomicAdd(novf, 1u);
+    }
+    uint32_t tall;
+    const uint32_t tex = scan_excl_1024(nt, wsum, tall);
+    if (j == 0) tbase = tall ? atomicAdd(ntiles, tall) : 0;
+    __syncthreads();
+    if (j < nc && nt) {
+        const uint32_t p = ss[i0], len = ss[i1] - p;
+        uint32_t k = tbase + tex;
+        if constexpr (LOCAL) {
+            static_cast<GTile *>(tiles)[k] = GTile{p, len, blockIdx.x, i0, i1, 0};
+        } else {
+            bk::TileRef *tt = static_cast<bk::TileRef *>(tiles);
+            if (!over) {
+                tt[k] = bk::TileRef{p, len, 0};
+            } else {
+                tt[k++] = bk::TileRef{p, room, 0};
+                for (uint32_t q = room; q < len; q += (uint32_t)tile)
+                    tt[k++] = bk::TileRef{(uint64_t)p + q, len - q < (uint32_t)tile ? len - q : (uint32_t)tile, 0};
+                ovf[atomicAdd(novf, 1u)] = Ovf{p, len};
+            }
+        }
+    }
+}
+
+// Local partition (the default second level).  Chunk c (<= SB_LCH keys of one bucket) is loaded
+// whole, partitioned by sub-bucket in LDS and written back in place with coalesced stores;
+// pref[c][j] = keys of the chunk in sub-buckets below j (j = 0..nsub).  A tile (sub-buckets
+// [j0, j1) of a bucket) is then one contiguous piece of every chunk of the bucket,
+// [pref[c][j0], pref[c][j1]), gathered by the tile sort (about 1 KiB per piece) -- no
+// element-granular scatter to HBM.
+#ifndef DSORT_SB_LT
+#define DSORT_SB_LT 512
+#endif
+constexpr int SB_LT = DSORT_SB_LT;
+// keys per thread: the chunk (int32 62 KiB, int64 52 KiB) + tables fit two workgroups per CU
+template <typename T> constexpr int SB_LKPT = sizeof(T) == 4 ? 31 : 13;
+template <typename T> constexpr int SB_LCH = SB_LT * SB_LKPT<T>;
+
+template <typename T>
+__global__ void __launch_bounds__(SB_LT, 4) sb_local_kernel(T *__restrict__ buf, const Chunk *__restrict__ ch,
+                                                         const BInfo *__restrict__ bi, int SS,
+                                                         const Spl<T> *__restrict__ spl_g,
+                                                         const uint32_t *__restrict__ rng_g,
+                                                         const SlotFn<T> *__restrict__ sfn,
+                                                         uint32_t *__restrict__ pref) {
+    constexpr int KPT = SB_LKPT<T>, CHL = SB_LCH<T>, PER = SB_MAXS / SB_LT;
+    static_assert(SB_MAXS % SB_LT == 0, "sub-buckets per thread");
+    __shared__ Spl<T> spl[SB_MAXS + 1];
+    __shared__ uint32_t rng[SB_SLOTS];
+    __shared__ uint32_t hist[SB_MAXS];   // chunk histogram, then the LDS starts
+    __shared__ uint32_t wsum[SB_LT / 64];
+    __shared__ T lk[CHL];
+    const Chunk c = ch[blockIdx.x];
+    const BInfo b = bi[c.b];
+    uint32_t *pc = pref + (uint64_t)blockIdx.x * (SS + 1);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int ns = (int)b.nsub;
+    if (ns == 1) {
+        if (tid == 0) {
+            pc[0] = 0;
+            pc[1] = c.len;
+        }
+        return;
+    }
+    T *src = buf + c.start;
+    T key[KPT];
+#pragma unroll
+    for (int k = 0; k < KPT; ++k) {
+        const uint32_t i = tid + k * SB_LT;
+        key[k] = i < c.len ? src[i] : T(0);
+    }
+    load_sub_tables<T>(b, c.b, SS, spl_g, rng_g, spl, rng);
+#pragma unroll
+    for (int q = 0; q < PER; ++q) hist[PER * tid + q] = 0;
+    const SlotFn<T> f = sfn[c.b];
+    __syncthreads();
+    uint32_t pk[KPT];  // sub-bucket | rank << 10
+#pragma unroll
+    for (int k = 0; k < KPT; ++k) {
+        const uint32_t i = tid + k * SB_LT;
+        if (i < c.len) {
+            const int j = sub_of<T>(spl, rng, f.klo, f.sh, key[k], (uint32_t)(c.start + i));
+            pk[k] = (uint32_t)j | atomicAdd(&hist[j], 1u) << 10;
+        }
+    }
+    __syncthreads();
+    uint32_t h[PER], sum = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        h[q] = hist[PER * tid + q];
+        sum += h[q];
+    }
+    uint32_t incl = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t ex = incl - sum;
+#pragma unroll
+    for (int i = 0; i < SB_LT / 64; ++i) ex += i < w ? wsum[i] : 0u;
+    if (tid == 0) pc[ns] = c.len;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int j = PER * tid + q;
+        hist[j] = ex;
+        if (j < ns) pc[j] = ex;
+        ex += h[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < KPT; ++k) {
+        const uint32_t i = tid + k * SB_LT;
+        if (i < c.len) lk[hist[pk[k] & 1023] + (pk[k] >> 10)] = key[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < KPT; ++k) {
+        const uint32_t i = tid + k * SB_LT;
+        if (i < c.len) src[i] = lk[i];
+    }
+}
+
+// Workgroup -> chunk: every XCD takes a contiguous block of chunks, i.e. of buckets, so the
+// workgroups that write pieces of the same sub-buckets share an L2 (a bijection on [0, G)).
+__device__ __forceinline__ uint32_t sb_chunk_order(uint32_t bid, uint32_t G) {
+    constexpr uint32_t NX = 8;
+    const uint32_t q = G / NX, r = G % NX, x = bid % NX, i = bid / NX;
+    return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
+}
+
+// Per sub-tile (SB_SUB keys): sub-bucket and slot of every key (LDS atomic), scan, keys grouped
+// by sub-bucket in LDS, then consecutive threads write consecutive keys of a sub-bucket to
+// consecutive addresses.  Thread t owns sub-buckets 4t .. 4t+3 (their running global offsets).
+template <typename T>
+__global__ void __launch_bounds__(SB_T) sb_scatter_kernel(const T *__restrict__ src, T *__restrict__ dst,
+                                                          const Chunk *__restrict__ ch, uint32_t G,
+                                                          const BInfo *__restrict__ bi, int SS,
+                                                          const Spl<T> *__restrict__ spl_g,
+                                                          const uint32_t *__restrict__ rng_g,
+                                                          const SlotFn<T> *__restrict__ sfn,
+                                                          const uint32_t *__restrict__ offs) {
+    constexpr int KPT = SB_KPT<T>, SUB = SB_SUB<T>;
+    static_assert(SB_MAXS == 4 * SB_T, "4 sub-buckets per thread");
+    __shared__ Spl<T> spl[SB_MAXS + 1];  // + 1: sub_of reads two entries
+    __shared__ uint32_t rng[SB_SLOTS];
+    __shared__ uint32_t hist[SB_MAXS];   // sub-tile histogram, then the sub-tile's LDS starts
+    __shared__ uint32_t dl[SB_MAXS];     // global offset - LDS start, per sub-bucket
+    __shared__ uint32_t wsum[SB_T / 64];
+    __shared__ T lk[SUB];
+    __shared__ uint16_t lj[SUB];
+    const uint32_t cid = sb_chunk_order(blockIdx.x, G);
+    const Chunk c = chunk_of<T>(ch, bi, cid);
+    const BInfo b = bi[c.b];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (b.nsub == 1) {  // one sub-bucket: a plain copy
+        const uint32_t o = offs[(uint64_t)cid * SS];
+        for (uint32_t i = tid; i < c.len; i += SB_T) dst[o + i] = src[c.start + i];
+        return;
+    }
+    load_sub_tables<T>(b, c.b, SS, spl_g, rng_g, spl, rng);
+    const SlotFn<T> f = sfn[c.b];
+    const int ns = (int)b.nsub;
+    uint32_t gof[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int j = 4 * tid + q;
+        gof[q] = j < ns ? offs[(uint64_t)cid * SS + j] : 0u;
+        hist[j] = 0;
+    }
+#pragma unroll 1
+    for (uint32_t s0 = 0; s0 < c.len; s0 += SUB) {
+        const uint32_t cnt = c.len - s0 < (uint32_t)SUB ? c.len - s0 : (uint32_t)SUB;
+        T key[KPT];
+#pragma unroll
+        for (int k = 0; k < KPT; ++k) {
+            const uint32_t i = tid + k * SB_T;
+            key[k] = i < cnt ? src[c.start + s0 + i] : T(0);
+        }
+        __syncthreads();  // tables loaded / previous sub-tile written and its histogram cleared
+        int jj[KPT];
+        uint32_t slot[KPT];
+#pragma unroll
+        for (int k = 0; k < KPT; ++k) {
+            const uint32_t i = tid + k * SB_T;
+            jj[k] = -1;
+            if (i < cnt) {
+                jj[k] = sub_of<T>(spl, rng, f.klo, f.sh, key[k], (uint32_t)(c.start + s0 + i));
+                slot[k] = atomicAdd(&hist[jj[k]], 1u);
+            }
+        }
+        __syncthreads();
+        uint32_t h[4], sum = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            h[q] = hist[4 * tid + q];
+            sum += h[q];
+        }
+        uint32_t incl = sum;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) wsum[w] = incl;
+        __syncthreads();
+        uint32_t ex = incl - sum;
+#pragma unroll
+        for (int i = 0; i < SB_T / 64; ++i) ex += i < w ? wsum[i] : 0u;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            hist[4 * tid + q] = ex;
+            dl[4 * tid + q] = gof[q] - ex;
+            gof[q] += h[q];
+            ex += h[q];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < KPT; ++k) {
+            if (jj[k] >= 0) {
+                const uint32_t lp = hist[jj[k]] + slot[k];
+                lk[lp] = key[k];
+                lj[lp] = (uint16_t)jj[k];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < KPT; ++k) {
+            const uint32_t p = tid + k * SB_T;
+            if (p < cnt) dst[dl[lj[p]] + p] = lk[p];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) hist[4 * tid + q] = 0;
+    }
+}
+
+}  // namespace sb
+}  // namespace dsort

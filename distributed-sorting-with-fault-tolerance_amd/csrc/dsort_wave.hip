@@ -44,6 +44,7 @@
 #include "dsort_bucket.h"
 #include "dsort_internal.h"
 #include "dsort_part.h"
+#include "dsort_sub.h"
 
 namespace dsort {
 namespace wv {
@@ -59,8 +60,11 @@ constexpr int kWaveMaxF = 1 << kWaveMaxLogF;
 // Per key type: waves of the tile sort and of the merge tile, and the occupancy they are
 // compiled for (waves per SIMD: two workgroups per CU).
 template <typename T> struct WG;
+#ifndef DSORT_WAVES32
+#define DSORT_WAVES32 16
+#endif
 template <> struct WG<int32_t> {
-    static constexpr int WAVES = 16, MWAVES = DSORT_MWAVES, OCC = 8, MAXLOGF = 5;
+    static constexpr int WAVES = DSORT_WAVES32, MWAVES = DSORT_MWAVES, OCC = 8, MAXLOGF = 5;
 };
 template <> struct WG<int64_t> {
     // F = 32 would need 32 run heads of 64-bit keys per lane next to the window: it spills, so
@@ -491,9 +495,89 @@ template <> struct V16<int64_t> {
 // ------------------------------------------------------------------------------------------
 // tiles: NULL = tile j is keys [j * TILE, (j + 1) * TILE) of n; else tile j = tiles[j] (the
 // bucketed sort's tiles, which never cross a bucket), j < *ntiles.
+// Pieces of a gathered tile at most: the piece table (offsets + sources) lives in the slack.
+template <typename T> constexpr int kMaxPieces = WK * (int)sizeof(T) / 8 - 2;
+
+// The tile of a GTile (local-partition path, dsort_sub.h): one piece per chunk of its bucket.
+// The piece table (offsets in the tile, sources) goes to the LDS slack; then lane t of wave w
+// loads tile slots w * 1024 + 64 i + t straight into x[i] (the order before the sort does not
+// matter), walking the pieces upwards as i grows: consecutive lanes read consecutive keys of a
+// piece, and all R loads of a lane are in flight together.
 template <typename T>
+__device__ __forceinline__ void gather_tile(const sb::Gather &ga, const sb::GTile &gt, const T *in, T *s,
+                                            T (&x)[R]) {
+    constexpr int TILE = TILE_OF<T>, WAVES = WG<T>::WAVES, THREADS = 64 * WAVES;
+    static_assert(2 * THREADS >= kMaxPieces<T> + 1, "two pieces per thread");
+    uint32_t *poff = reinterpret_cast<uint32_t *>(s + TILE);  // kMaxPieces + 1 offsets
+    uint32_t *psrc = poff + kMaxPieces<T> + 1;                 // kMaxPieces sources
+    uint32_t *wsum = reinterpret_cast<uint32_t *>(s);          // per-wave sums
+    const sb::BInfo b = ga.bi[gt.b];
+    const int np = (int)(b.c1 - b.c0);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    uint32_t len[2], src[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int k = 2 * tid + q;
+        len[q] = 0;
+        src[q] = 0;
+        if (k < np) {
+            const uint32_t c = b.c0 + (uint32_t)k;
+            const uint32_t *pc = ga.pref + (uint64_t)c * (ga.SS + 1);
+            const uint32_t lo = pc[gt.j0];
+            len[q] = pc[gt.j1] - lo;
+            src[q] = (uint32_t)ga.ch[c].start + lo;
+        }
+    }
+    const uint32_t sum = len[0] + len[1];
+    uint32_t incl = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t ex = incl - sum;
+    for (int i = 0; i < w; ++i) ex += wsum[i];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int k = 2 * tid + q;
+        if (k < np) {
+            poff[k] = ex;
+            psrc[k] = src[q];
+        }
+        ex += len[q];
+    }
+    if (tid == 0) poff[np] = gt.valid;
+    __syncthreads();
+    const uint32_t valid = gt.valid, e0 = (uint32_t)(w * WK + lane);
+    // piece of slot e0: the last k with poff[k] <= e0
+    int lo = 0, hi = np;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (poff[mid] <= e0) lo = mid;
+        else hi = mid;
+    }
+    int k = lo;
+    uint32_t pend = poff[k + 1], pbase = psrc[k] - poff[k];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        const uint32_t e = e0 + 64 * i;
+        if (e < valid) {
+            while (e >= pend) {
+                ++k;
+                pend = poff[k + 1];
+                pbase = psrc[k] - poff[k];
+            }
+            x[i] = in[pbase + e];
+        } else {
+            x[i] = key_max<T>();
+        }
+    }
+}
+
+template <typename T, bool GATHER>
 __global__ void __launch_bounds__(64 * WG<T>::WAVES, WG<T>::OCC) block_sort_w_kernel(
-    const T *in, T *out, uint64_t n, const uint4 *tiles, const uint32_t *ntiles) {
+    const T *in, T *out, uint64_t n, const uint4 *tiles, const uint32_t *ntiles, sb::Gather ga) {
     constexpr int TILE = TILE_OF<T>, N = KPC<T>;
     using V = typename V16<T>::type;
     // `in` may alias `out`: every workgroup reads its tile before it writes it
@@ -502,7 +586,12 @@ __global__ void __launch_bounds__(64 * WG<T>::WAVES, WG<T>::OCC) block_sort_w_ke
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
     uint64_t base;
     int valid;
-    if (tiles) {
+    if constexpr (GATHER) {
+        if (blockIdx.x >= *ntiles) return;
+        const sb::GTile gt = ga.tiles[blockIdx.x];
+        base = gt.base;
+        valid = (int)gt.valid;
+    } else if (tiles) {
         if (blockIdx.x >= *ntiles) return;  // the grid is an upper bound
         const uint4 r = tiles[blockIdx.x];  // TileRef: base (2 words), valid
         base = (uint64_t)r.x | ((uint64_t)r.y << 32);
@@ -518,10 +607,26 @@ __global__ void __launch_bounds__(64 * WG<T>::WAVES, WG<T>::OCC) block_sort_w_ke
     // The wave's 1024 keys in any order (the order inside a wave is irrelevant before a sort):
     // register N q + j of lane t holds key N (64 q + t) + j of the wave's range.
     T x[R];
-    if (valid == TILE && (reinterpret_cast<uintptr_t>(in + base) & 15) == 0) {
-        const V *src = reinterpret_cast<const V *>(in + base) + w * (WK / N);
+    // off = keys between the 16-byte boundary below the tile and its first key
+    const int off = (int)((reinterpret_cast<uintptr_t>(in + base) / sizeof(T)) & (N - 1));
+    if constexpr (GATHER) {
+        gather_tile<T>(ga, ga.tiles[blockIdx.x], in, s, x);  // (the runs go to LDS, not the slack)
+    } else if (off + valid <= TILE) {
+        // 16-byte vectors from the boundary; entries outside [off, off + valid) become +inf.  A
+        // vector is loaded only when it holds a key of the tile (an aligned 16-byte block never
+        // crosses a page); the keys of a neighbouring tile it also holds are dropped.
+        const V *src = reinterpret_cast<const V *>(in + base - off) + w * (WK / N);
+        const int lim = off + valid;
 #pragma unroll
-        for (int q = 0; q < R / N; ++q) V16<T>::get(src[q * 64 + t], x + N * q);
+        for (int q = 0; q < R / N; ++q) {
+            const int e0 = w * WK + N * (q * 64 + t);
+            T vals[N];
+#pragma unroll
+            for (int j = 0; j < N; ++j) vals[j] = key_max<T>();
+            if (e0 < lim) V16<T>::get(src[q * 64 + t], vals);
+#pragma unroll
+            for (int j = 0; j < N; ++j) x[N * q + j] = (e0 + j >= off && e0 + j < lim) ? vals[j] : key_max<T>();
+        }
     } else {
 #pragma unroll
         for (int q = 0; q < R / N; ++q) {
@@ -856,28 +961,6 @@ static int bucket_os(const dsort_ctx *ctx) {
     return v < 1 ? 1 : (v > 4096 ? 4096 : (int)v);
 }
 
-// Skewed bucket sizes (int32).  When the mean bucket holds about 64 tiles (2^30 keys in 1024
-// buckets), about half the buckets land above 64 runs and merge F = 16 then F = 8, the rest
-// F = 8 twice.  Instead the first k buckets get 56 tiles' worth of samples (below 64 runs despite
-// the sampling spread) and the others share the rest, about 104 tiles each (below 128): most keys
-// then take the cheaper F = 8 first pass (profiles/r1_bucket_skew_sweep.txt: 52:100 .. 60:112
-// all within 0.06 ms of 56:104).  Returns k and the samples per small / large bucket;
-// DSORT_OPT_BUCKET_SKEW = 0 turns it off.
-struct Skew { int k, kos, los; };
-static Skew bucket_skew(const dsort_ctx *ctx, uint64_t n, int B, int os, int tile) {
-    if (!ctx->opt.bucket_skew) return Skew{0, 0, 0};
-    const double R = (double)n / ((double)B * tile);  // mean tiles per bucket
-    if (B < 16 || R <= 56.0 || R > 72.0) return Skew{0, 0, 0};
-    const double small = 56.0, large = 104.0;
-    const int k = (int)((double)B * (large - R) / (large - small));
-    if (k <= 0 || k >= B) return Skew{0, 0, 0};
-    const int kos = (int)((double)os * small / R);
-    const uint64_t S = (uint64_t)B * os, rem = S - (uint64_t)k * kos;
-    const int los = (int)((rem + (B - k) - 1) / (uint64_t)(B - k));  // the last bucket gets less
-    if (kos < 1 || los < kos || (uint64_t)k * kos + (uint64_t)(B - 1 - k) * los >= S) return Skew{0, 0, 0};
-    return Skew{k, kos, los};
-}
-
 // Group tables of the merge passes inside buckets: pass p merges groups of up to 2^bits
 // consecutive runs of one bucket; a bucket with a single run left is carried as a 1-run group.
 struct BucketPass {
@@ -885,6 +968,232 @@ struct BucketPass {
     uint64_t ngroups, ntiles;
     size_t group_off, tile_off;  // in the group / tile_group staging
 };
+
+template <typename T>
+static int wave_merge(dsort_ctx *ctx, const T *d_in, const size_t *lens, int k, T *d_out, hipStream_t s,
+                      bool keep_stats);
+
+// ---- second partition level (dsort_sub.h) -------------------------------------------------
+// Nominal keys per sub-bucket: TILE / 8 unless DSORT_OPT_SUB_KEYS says otherwise (0 = off).
+template <typename T>
+static uint64_t sub_keys(const dsort_ctx *ctx) {
+    const int64_t v = ctx->opt.sub_keys;
+    return v < 0 ? (uint64_t)TILE_OF<T> / 8 : (uint64_t)v;
+}
+
+// Runs of an oversized sub-bucket as the packer cut it (sb_scan_kernel): the room of the first
+// tile, then whole tiles.
+static std::vector<size_t> sub_tile_runs(uint64_t p, uint64_t len, uint64_t tile, uint64_t align, uint64_t mis) {
+    std::vector<size_t> r;
+    const uint64_t room = tile - ((p + mis) & (align - 1));
+    r.push_back(room);
+    for (uint64_t q = room; q < len; q += tile) r.push_back(len - q < tile ? len - q : tile);
+    return r;
+}
+
+// Sub-buckets of every bucket (src = the first level's output), packed into tiles and
+// tile-sorted in d_keys.  Called from bucket_sort once the bucket starts hb[0..B] are on the
+// host (the first level's scatter is still running).
+//
+// Two ways to form the tiles (DSORT_OPT_SUB_GATHER): local (default) -- every chunk of a bucket
+// is partitioned by sub-bucket in place (sb_local_kernel) and the tile sort gathers a tile's
+// piece of every chunk; scatter -- histograms, then every key is scattered to its sub-bucket in
+// d_keys (sb_scatter_kernel) and the tile sort reads contiguous tiles.  Local needs no oversized
+// sub-bucket and at most kMaxPieces chunks per bucket; otherwise the scatter path runs (on the
+// locally partitioned keys, if the local pass already ran: still the same buckets).
+template <typename T>
+static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_t *hb, int B, uint64_t m,
+                    hipStream_t s, bool timed, bool local) {
+    using namespace sb;
+    constexpr int TILE = TILE_OF<T>;
+    constexpr uint64_t ALIGN = KPC<T>;
+    for (int b = 0; b < B && local; ++b)
+        if (ceil_div(hb[b + 1] - hb[b], (uint64_t)SB_LCH<T>) > (uint64_t)kMaxPieces<T>) local = false;
+    const uint64_t CH = local ? SB_LCH<T> : SB_CH<T>;
+    // samples per sub-bucket; a bucket's samples (<= SB_MAXS * 8) fit one int64 tile
+    constexpr int kMaxOs = TILE_OF<int64_t> / SB_MAXS;
+    const int os = ctx->opt.sub_os > 0 ? (ctx->opt.sub_os < kMaxOs ? (int)ctx->opt.sub_os : kMaxOs) : 4;
+    // bucket and chunk tables
+    std::vector<BInfo> bi((size_t)B);
+    uint64_t nsmp = 0, nch = 0, nsubs = 0;
+    int SS = 1;
+    for (int b = 0; b < B; ++b) {
+        const uint64_t len = hb[b + 1] - hb[b];
+        uint64_t ns = len <= (uint64_t)TILE ? 1 : ceil_div(len, m);
+        ns = ns > (uint64_t)SB_MAXS ? SB_MAXS : ns;
+        const uint64_t nc = ceil_div(len, CH);
+        bi[b] = BInfo{hb[b], nsmp, (uint32_t)len, (uint32_t)ns, ns > 1 ? (uint32_t)(ns * os) : 0u, (uint32_t)nch,
+                      (uint32_t)(nch + nc), 0};
+        nsmp += bi[b].ns;
+        nch += nc;
+        nsubs += ns;
+        SS = (int)ns > SS ? (int)ns : SS;
+    }
+    SS = (SS + 63) & ~63;
+    const uint64_t tmax = nsubs + ceil_div(n, TILE) + (uint64_t)B;  // tiles, bound (sb_scan_kernel)
+    size_t off = 0;
+    auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
+    const size_t o_bi = take(B * sizeof(BInfo)), o_ch = take(nch * sizeof(Chunk)), o_smp = take(nsmp * sizeof(T)),
+                 o_cmp = take(nsmp * 8), o_srt = take(sizeof(T) == 8 ? nsmp * 8 : 0),
+                 o_spl = take((size_t)B * SS * sizeof(Spl<T>)),
+                 o_rng = take((size_t)B * SB_SLOTS * 4), o_sfn = take(B * sizeof(SlotFn<T>)),
+                 o_cnt = take(nch * (SS + 1) * 4), o_offs = take(local ? 0 : nch * SS * 4),
+                 o_tt = take(tmax * sizeof(GTile)),
+                 o_ovf = take(nsubs * sizeof(Ovf)), o_num = take(8), o_stl = take(B * sizeof(bk::TileRef) + 16);
+    int rc = ensure(ctx, &ctx->sub, &ctx->sub_bytes, off, "sub-bucket partition");
+    if (rc) return rc;
+    char *a = static_cast<char *>(ctx->sub);
+    BInfo *dbi = reinterpret_cast<BInfo *>(a + o_bi);
+    Chunk *dch = reinterpret_cast<Chunk *>(a + o_ch);
+    T *smp = reinterpret_cast<T *>(a + o_smp);
+    int64_t *cmp = reinterpret_cast<int64_t *>(a + o_cmp), *srt = reinterpret_cast<int64_t *>(a + o_srt);
+    Spl<T> *spl = reinterpret_cast<Spl<T> *>(a + o_spl);
+    uint32_t *rng = reinterpret_cast<uint32_t *>(a + o_rng);
+    SlotFn<T> *sfn = reinterpret_cast<SlotFn<T> *>(a + o_sfn);
+    uint32_t *cnt = reinterpret_cast<uint32_t *>(a + o_cnt), *offs = reinterpret_cast<uint32_t *>(a + o_offs);
+    void *tt = a + o_tt;  // GTile (local) or TileRef (scatter)
+    Ovf *ovf = reinterpret_cast<Ovf *>(a + o_ovf);
+    uint32_t *num = reinterpret_cast<uint32_t *>(a + o_num);  // tiles, merge records
+    bk::TileRef *stl = reinterpret_cast<bk::TileRef *>(a + o_stl);  // sample tiles, then their count
+    // pinned staging: the two tables, the sample tiles + count, then the two counters read back
+    const size_t h_ch = (B * sizeof(BInfo) + 15) & ~(size_t)15, h_stl = h_ch + nch * sizeof(Chunk);
+    const size_t h_num = h_stl + B * sizeof(bk::TileRef) + 16;
+    const size_t hbytes = h_num + 16;
+    if (ctx->sub_host_bytes < hbytes) {
+        if (ctx->sub_host) (void)hipHostFree(ctx->sub_host);
+        ctx->sub_host = nullptr;
+        ctx->sub_host_bytes = 0;
+        DSORT_HIP(ctx, hipHostMalloc(&ctx->sub_host, hbytes, hipHostMallocDefault));
+        ctx->sub_host_bytes = hbytes;
+    }
+    if (!ctx->sub_ev && hipEventCreateWithFlags(&ctx->sub_ev, hipEventDisableTiming) != hipSuccess)
+        return set_err(ctx, DSORT_EHIP, "hipEventCreate");
+    DSORT_HIP(ctx, hipEventSynchronize(ctx->sub_ev));  // the previous call's read-back is done with the staging
+    char *h = static_cast<char *>(ctx->sub_host);
+    std::memcpy(h, bi.data(), B * sizeof(BInfo));
+    Chunk *hc = reinterpret_cast<Chunk *>(h + h_ch);
+    for (int b = 0; b < B; ++b)
+        for (uint64_t o = 0; o < bi[b].len; o += CH)
+            *hc++ = Chunk{bi[b].start + o, (uint32_t)(bi[b].len - o < CH ? bi[b].len - o : CH), (uint32_t)b};
+    bk::TileRef *hst = reinterpret_cast<bk::TileRef *>(h + h_stl);
+    uint32_t nst = 0;
+    for (int b = 0; b < B; ++b)
+        if (bi[b].ns) hst[nst++] = bk::TileRef{bi[b].soff, bi[b].ns, 0};
+    *reinterpret_cast<uint32_t *>(hst + B) = nst;
+    DSORT_HIP(ctx, hipMemcpyAsync(dbi, h, B * sizeof(BInfo), hipMemcpyHostToDevice, s));
+    if (nch) DSORT_HIP(ctx, hipMemcpyAsync(dch, h + h_ch, nch * sizeof(Chunk), hipMemcpyHostToDevice, s));
+    DSORT_HIP(ctx, hipMemcpyAsync(stl, hst, B * sizeof(bk::TileRef) + 16, hipMemcpyHostToDevice, s));
+    DSORT_HIP(ctx, hipMemsetAsync(num, 0, 8, s));
+    // 1. splitters of every bucket from a regular sample.  A bucket's samples fit one int64 tile,
+    // so the tile sort alone sorts them, one workgroup per bucket.
+    if (nsmp) {
+        hipLaunchKernelGGL(sb_sample_kernel<T>, dim3((unsigned)B), dim3(SB_T), 0, s, src, dbi, smp, cmp);
+        DSORT_HIP(ctx, hipGetLastError());
+        const uint4 *stl4 = reinterpret_cast<const uint4 *>(stl);
+        const uint32_t *pnst = reinterpret_cast<const uint32_t *>(stl + B);
+        const dim3 sblk(64 * WG<int64_t>::WAVES);
+        if constexpr (sizeof(T) == 8) {  // int64: sort the keys, rank them, then the composites
+            hipLaunchKernelGGL((block_sort_w_kernel<int64_t, false>), dim3(nst), sblk, 0, s, smp, srt, nsmp, stl4, pnst,
+                               sb::Gather{});
+            hipLaunchKernelGGL(sb_rank_kernel, dim3((unsigned)B), dim3(SB_T), 0, s, smp, srt, dbi, cmp);
+        }
+        hipLaunchKernelGGL((block_sort_w_kernel<int64_t, false>), dim3(nst), sblk, 0, s, cmp, cmp, nsmp, stl4, pnst,
+                           sb::Gather{});
+        DSORT_HIP(ctx, hipGetLastError());
+        hipLaunchKernelGGL(sb_splitter_kernel<T>, dim3((unsigned)B), dim3(SB_MAXS), 0, s, cmp, smp, dbi, os, SS, spl,
+                           rng, sfn);
+        DSORT_HIP(ctx, hipGetLastError());
+    }
+    const uint32_t mis = (uint32_t)((reinterpret_cast<uintptr_t>(d_keys) / sizeof(T)) & (ALIGN - 1));
+    uint32_t *hn = reinterpret_cast<uint32_t *>(h + h_num);
+    if (local) {
+        // 2. every chunk partitioned in place (cnt = the prefix tables), sub-bucket starts, tiles
+        if (nch) {
+            hipLaunchKernelGGL(sb_local_kernel<T>, dim3((unsigned)nch), dim3(SB_LT), 0, s, src, dch, dbi, SS, spl, rng,
+                               sfn, cnt);
+            DSORT_HIP(ctx, hipGetLastError());
+        }
+        hipLaunchKernelGGL(sb_scan_kernel<true>, dim3((unsigned)B), dim3(SB_MAXS), 0, s, dbi, SS, cnt, nullptr, TILE, 1,
+                           0u, tt, num, nullptr, num + 1);
+        DSORT_HIP(ctx, hipGetLastError());
+        DSORT_HIP(ctx, hipMemcpyAsync(hn, num, 8, hipMemcpyDeviceToHost, s));
+        DSORT_HIP(ctx, hipEventRecord(ctx->sub_ev, s));
+        DSORT_HIP(ctx, hipEventSynchronize(ctx->sub_ev));
+        const uint32_t ntiles = hn[0], novf = hn[1];
+        if (novf) return sub_sort<T>(ctx, src, d_keys, n, hb, B, m, s, timed, false);
+        if (ntiles > tmax) return set_err(ctx, DSORT_EHIP, "sub-bucket packing overflow");
+        ctx->stats.merge_passes = 0;
+        // 3. tile sort: gathered from the chunks into d_keys
+        if (ntiles) {
+            const Gather ga{static_cast<const GTile *>(tt), dch, dbi, cnt, SS};
+            hipLaunchKernelGGL((block_sort_w_kernel<T, true>), dim3(ntiles), dim3(64 * WG<T>::WAVES), 0, s, src, d_keys,
+                               (uint64_t)n, nullptr, num, ga);
+            DSORT_HIP(ctx, hipGetLastError());
+        }
+        if (timed && ctx->ev_ok) {
+            DSORT_HIP(ctx, hipEventRecord(ctx->ev[1], s));
+            DSORT_HIP(ctx, hipEventRecord(ctx->ev[2], s));
+            ctx->ev_mask |= 6u;
+        }
+        fault_point(ctx, s, 0);  // the tile sort is the last stage: it counts as pass 0
+        return DSORT_OK;
+    }
+    // 2. histograms, sub-bucket starts, tiles
+    if (nch) {
+        hipLaunchKernelGGL(sb_hist_kernel<T>, dim3((unsigned)nch), dim3(SB_T), 0, s, src, dch, dbi, SS, spl, rng,
+                           sfn, cnt);
+        DSORT_HIP(ctx, hipGetLastError());
+    }
+    hipLaunchKernelGGL(sb_scan_kernel<false>, dim3((unsigned)B), dim3(SB_MAXS), 0, s, dbi, SS, cnt, offs, TILE,
+                       (int)ALIGN, mis, tt, num, ovf, num + 1);
+    DSORT_HIP(ctx, hipGetLastError());
+    DSORT_HIP(ctx, hipMemcpyAsync(hn, num, 8, hipMemcpyDeviceToHost, s));
+    DSORT_HIP(ctx, hipEventRecord(ctx->sub_ev, s));
+    // 3. scatter into d_keys (the host reads the tile count meanwhile), tile sort in place
+    if (nch) {
+        hipLaunchKernelGGL(sb_scatter_kernel<T>, dim3((unsigned)nch), dim3(SB_T), 0, s, src, d_keys, dch,
+                           (uint32_t)nch, dbi, SS, spl, rng, sfn, offs);
+        DSORT_HIP(ctx, hipGetLastError());
+    }
+    DSORT_HIP(ctx, hipEventSynchronize(ctx->sub_ev));
+    const uint32_t ntiles = hn[0], novf = hn[1];
+    if (ntiles > tmax || novf > nsubs) return set_err(ctx, DSORT_EHIP, "sub-bucket packing overflow");
+    ctx->stats.merge_passes = 0;
+    if (ntiles) {
+        hipLaunchKernelGGL((block_sort_w_kernel<T, false>), dim3(ntiles), dim3(64 * WG<T>::WAVES), 0, s, d_keys,
+                           d_keys, (uint64_t)n, static_cast<const uint4 *>(tt), num, Gather{});
+        DSORT_HIP(ctx, hipGetLastError());
+    }
+    if (timed && ctx->ev_ok) {
+        DSORT_HIP(ctx, hipEventRecord(ctx->ev[1], s));
+        ctx->ev_mask |= 2u;
+    }
+    fault_point(ctx, s, 0);  // the tile sort is the last stage: it counts as pass 0
+    // 4. oversized sub-buckets: their tile-sorted pieces merged (src is free scratch now)
+    if (novf) {
+        std::vector<Ovf> ov(novf);
+        DSORT_HIP(ctx, hipMemcpyAsync(ov.data(), ovf, novf * sizeof(Ovf), hipMemcpyDeviceToHost, s));
+        DSORT_HIP(ctx, hipStreamSynchronize(s));
+        T *tmp = src;
+        int lv = 0;
+        for (const Ovf &o : ov) {
+            const std::vector<size_t> runs = sub_tile_runs(o.start, o.len, TILE, ALIGN, mis);
+            rc = wave_merge<T>(ctx, d_keys + o.start, runs.data(), (int)runs.size(), tmp + o.start, s, true);
+            if (rc) return rc;
+            DSORT_HIP(ctx, hipMemcpyAsync(d_keys + o.start, tmp + o.start, o.len * sizeof(T),
+                                          hipMemcpyDeviceToDevice, s));
+            int l = 0;
+            for (uint64_t r = runs.size(); r > 1; r = ceil_div(r, (uint64_t)1 << WG<T>::MAXLOGF)) ++l;
+            lv = l > lv ? l : lv;
+        }
+        ctx->stats.merge_passes = lv;
+    }
+    if (timed && ctx->ev_ok) {
+        DSORT_HIP(ctx, hipEventRecord(ctx->ev[2], s));
+        ctx->ev_mask |= 4u;
+    }
+    return DSORT_OK;
+}
 
 template <typename T>
 static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipStream_t s, bool timed, int B) {
@@ -954,9 +1263,7 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
         ctx->ev_mask |= 1u;
     }
     if constexpr (std::is_same<T, int32_t>::value) {
-        const Skew sk = bucket_skew(ctx, n, B, os, TILE);
-        hipLaunchKernelGGL(bucket_splitter_kernel<int32_t>, dim3(1), dim3(BK_MAXB), 0, s, smp, B, BP, os, spl,
-                           sk.k, sk.kos, sk.los);
+        hipLaunchKernelGGL(bucket_splitter_kernel<int32_t>, dim3(1), dim3(BK_MAXB), 0, s, smp, B, BP, os, spl);
         hb = static_cast<uint64_t *>(ctx->bucket_host);
     } else {
         // int64 composites are 16-byte (key, index) pairs: the 32 B samples are sorted on the host
@@ -973,7 +1280,7 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
     hipLaunchKernelGGL(bucket_colsum_kernel, dim3((unsigned)nchunk), dim3(BK_MAXB), 0, s, cnt, (uint32_t)G, B, part);
     hipLaunchKernelGGL(bucket_scan_kernel, dim3(1), dim3(BK_MAXB), 0, s, part, (uint32_t)nchunk, B,
                        (uint32_t)TILE, (uint32_t)ALIGN, bst, tt, ntl);
-    hipLaunchKernelGGL(bucket_offsets_kernel, dim3((unsigned)nchunk), dim3(BK_MAXB), 0, s, cnt, part, bst, (uint32_t)G, B, offs);
+    hipLaunchKernelGGL(bucket_offsets_kernel<uint64_t>, dim3((unsigned)nchunk), dim3(BK_MAXB), 0, s, cnt, part, bst, (uint32_t)G, B, offs);
     DSORT_HIP(ctx, hipGetLastError());
     // bucket starts to the host (the pass plan depends on the bucket sizes); the host waits for
     // them while the scatter runs.  The scatter always writes the scratch buffer (never the
@@ -992,6 +1299,8 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
     DSORT_HIP(ctx, hipGetLastError());
     DSORT_HIP(ctx, hipEventSynchronize(ctx->bucket_ev));
     if (hb[B] != n) return set_err(ctx, DSORT_EHIP, "bucket partition lost keys");
+    if (const uint64_t m = sub_keys<T>(ctx))
+        return sub_sort<T>(ctx, part_out, d_keys, n, hb, B, m, s, timed, ctx->opt.sub_gather != 0);
     // pass plan: the runs of every bucket; the largest bucket's run count R sets the merge
     // levels L = ceil(log2 R), split into the fewest passes of <= max_logf levels (larger passes
     // first).
@@ -1011,8 +1320,8 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
     T *bufs[2] = {d_keys, scratch};
     int cur = (passes % 2 == 0) ? 0 : 1;  // tile sort output; the passes end in d_keys
     // 3. tile sort inside the buckets
-    hipLaunchKernelGGL(block_sort_w_kernel<T>, dim3((unsigned)tmax), dim3(64 * WG<T>::WAVES), 0, s, part_out,
-                       bufs[cur], (uint64_t)n, reinterpret_cast<const uint4 *>(tt), ntl);
+    hipLaunchKernelGGL((block_sort_w_kernel<T, false>), dim3((unsigned)tmax), dim3(64 * WG<T>::WAVES), 0, s, part_out,
+                       bufs[cur], (uint64_t)n, reinterpret_cast<const uint4 *>(tt), ntl, sb::Gather{});
     DSORT_HIP(ctx, hipGetLastError());
     if (timed && ctx->ev_ok) {
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[1], s));
@@ -1152,9 +1461,12 @@ static int wave_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipStre
     ctx->stats.merge_passes = passes;
     T *scratch = nullptr;
     if (passes > 0) {
-        int rc = ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, n * sizeof(T), "sort scratch");
+        // a nested sort (splitter samples) runs while the scratch holds the partitioned keys
+        void **sb = ctx->nested ? &ctx->scratch2 : &ctx->scratch;
+        size_t *sbb = ctx->nested ? &ctx->scratch2_bytes : &ctx->scratch_bytes;
+        int rc = ensure(ctx, sb, sbb, n * sizeof(T), "sort scratch");
         if (rc) return rc;
-        scratch = static_cast<T *>(ctx->scratch);
+        scratch = static_cast<T *>(*sb);
     }
     // ping-pong so that the last pass lands in d_keys; the tile sort reads d_in (which may alias
     // d_keys)
@@ -1164,8 +1476,8 @@ static int wave_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipStre
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[0], s));
         ctx->ev_mask |= 1u;
     }
-    hipLaunchKernelGGL(block_sort_w_kernel<T>, dim3((unsigned)tiles), dim3(64 * WG<T>::WAVES), 0, s, d_in,
-                       bufs[cur], (uint64_t)n, nullptr, nullptr);
+    hipLaunchKernelGGL((block_sort_w_kernel<T, false>), dim3((unsigned)tiles), dim3(64 * WG<T>::WAVES), 0, s, d_in,
+                       bufs[cur], (uint64_t)n, nullptr, nullptr, sb::Gather{});
     DSORT_HIP(ctx, hipGetLastError());
     if (timed && ctx->ev_ok) {
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[1], s));

@@ -45,8 +45,9 @@ EXPORTS = [
 
 
 # dsort_set_option / dsort_get_option (include/dsort.h)
-OPTIONS = {"buckets": 1, "bucket_keys": 2, "bucket_oversample": 3, "bucket_skew": 4,
-           "max_fanin_log2": 5, "kill_after_pass": 6, "kill_in_exchange": 7, "comm_timeout_ms": 8}
+OPTIONS = {"buckets": 1, "bucket_keys": 2, "bucket_oversample": 3,
+           "max_fanin_log2": 5, "kill_after_pass": 6, "kill_in_exchange": 7, "comm_timeout_ms": 8,
+           "sub_keys": 9, "sub_oversample": 10, "sub_gather": 11}
 
 
 class DsortError(RuntimeError):

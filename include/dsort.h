@@ -82,10 +82,9 @@ int dsort_synchronize(dsort_ctx *ctx);
  * option or a value out of range. */
 #define DSORT_OPT_BUCKETS 1           /* partition pass: -1 automatic (default), 0 off, B >= 2 forces B
                                          buckets at any size (<= 1024)                               */
-#define DSORT_OPT_BUCKET_KEYS 2       /* int32: nominal keys per bucket (default 2^20)                 */
-#define DSORT_OPT_BUCKET_OVERSAMPLE 3 /* int32: splitter samples per bucket, 1..4096 (default 256)     */
-#define DSORT_OPT_BUCKET_SKEW 4       /* int32: 1 = skewed bucket sizes where they save a merge level
-                                         (default), 0 = equal buckets                                  */
+#define DSORT_OPT_BUCKET_KEYS 2       /* nominal keys per bucket (default 2^20)                        */
+#define DSORT_OPT_BUCKET_OVERSAMPLE 3 /* splitter samples per bucket, 1..4096 (default 256)            */
+/* 4: retired (skewed bucket sizes of the round-1 merge plan); rejected as unknown               */
 #define DSORT_OPT_MAX_FANIN_LOG2 5    /* cap on log2(F) of one merge pass; -1 = per key type default   */
 #define DSORT_OPT_KILL_AFTER_PASS 6   /* fault injection (config C5): SIGKILL the calling process right
                                          after merge pass k of a local sort; -1 = off (default)        */
@@ -95,6 +94,13 @@ int dsort_synchronize(dsort_ctx *ctx);
 #define DSORT_OPT_COMM_TIMEOUT_MS 8   /* deadline of every wait inside one sample-sort exchange on
                                          RCCL (ms); on expiry the communicator is aborted and the call
                                          returns DSORT_ETIMEOUT.  0 = no deadline (default)            */
+#define DSORT_OPT_SUB_KEYS 9          /* second partition level: nominal keys per sub-bucket inside
+                                         every bucket; consecutive sub-buckets are packed into tiles
+                                         and the tile sort finishes the sort (no merge pass).  -1 =
+                                         tile/8 (default), 0 = off (k-way merge passes in buckets) */
+#define DSORT_OPT_SUB_OVERSAMPLE 10   /* splitter samples per sub-bucket, 1..64; -1 = 4 (default)       */
+#define DSORT_OPT_SUB_GATHER 11       /* second level: 1 = chunks partitioned in place and gathered by
+                                         the tile sort (default), 0 = keys scattered to sub-buckets  */
 int dsort_set_option(dsort_ctx *ctx, int option, int64_t value);
 int dsort_get_option(const dsort_ctx *ctx, int option, int64_t *value);
 

@@ -10,4 +10,4 @@ done
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 120 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/ab_def -o run -- python3 $R/scripts/dev/ktime.py --reps 5 "$@" > /dev/null 2>&1 || exit $?
 DSORT_LIB=$R/build_variants/$V/libdsort.so timeout -k 10 120 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/ab_var -o run -- python3 $R/scripts/dev/ktime.py --reps 5 "$@" > /dev/null 2>&1 || exit $?
-for d in ab_def ab_var; do echo "== $d"; grep -h "bucket\|block_sort_w\|mergew" $R/gpurun_out/$d/run_kernel_stats.csv | cut -d, -f1-4 | sed 's/(.*)//'; done
+for d in ab_def ab_var; do echo "== $d"; grep -h "bucket\|block_sort_w\|mergew\|sb_" $R/gpurun_out/$d/run_kernel_stats.csv | cut -d, -f1-4 | sed 's/(.*)//'; done

@@ -1,8 +1,10 @@
-"""The bucketed int32 sort (dsort_bucket.h: sample-splitter partition pass, then the tile sort and
-the k-way merge passes inside every bucket) against numpy on the MI355X.  The option
+"""The bucketed sort against numpy on the MI355X: the sample-splitter partition (dsort_bucket.h,
+dsort_sub.h), then either the second partition level + tile packing (default: no merge pass) or,
+with DSORT_OPT_SUB_KEYS = 0, the tile sort and k-way merge passes inside every bucket.  The option
 DSORT_OPT_BUCKETS forces a bucket count at any size, so small inputs exercise the same kernels as
-the 2^30-key bench: empty buckets, single-run buckets, 0..3-key head tiles, heavy duplicates split
-across buckets by the (key, index) composite."""
+the 2^30-key bench: empty buckets and sub-buckets, single-tile buckets, unaligned tiles, heavy
+duplicates split across buckets and sub-buckets by the (key, position) composite, oversized
+sub-buckets (merged afterwards)."""
 import numpy as np
 import pytest
 
@@ -48,19 +50,25 @@ def _sort(ctx, a, inplace):
 @pytest.mark.parametrize("B,n", [(2, 100_003), (3, 17), (7, 3 * TILE + 5), (33, 1_000_003),
                                  (64, 4 * TILE), (1024, 500_000)])
 @pytest.mark.parametrize("inplace", [False, True])
-def test_bucketed_sort_vs_numpy(gpu_ctx, kind, B, n, inplace):
+@pytest.mark.parametrize("sub", [-1, 0])
+def test_bucketed_sort_vs_numpy(gpu_ctx, kind, B, n, inplace, sub):
     a = _keys(np.random.default_rng(B * 131 + n), kind, n)
-    with gpu_ctx.options(buckets=B):
+    with gpu_ctx.options(buckets=B, sub_keys=sub):
         assert np.array_equal(_sort(gpu_ctx, a, inplace), np.sort(a))
 
 
 @pytest.mark.parametrize("tiles,passes", [(200, 2), (300, 3)])
 def test_bucketed_sort_multi_pass_buckets(gpu_ctx, tiles, passes):
-    """Few buckets of many tiles: more than 16 (256) runs per bucket -> 2 (3) merge passes."""
+    """Few buckets of many tiles: more than 16 (256) runs per bucket -> 2 (3) merge passes on the
+    merge path; the sub-bucket path needs none (its 1024 sub-buckets per bucket are still below a
+    tile)."""
     a = _keys(np.random.default_rng(tiles), "uniform", 2 * tiles * TILE + 777)
-    with gpu_ctx.options(buckets=2):
+    with gpu_ctx.options(buckets=2, sub_keys=0):
         assert np.array_equal(_sort(gpu_ctx, a, False), np.sort(a))
         assert gpu_ctx.stats()["merge_passes"] == passes
+    with gpu_ctx.options(buckets=2):
+        assert np.array_equal(_sort(gpu_ctx, a, False), np.sort(a))
+        assert gpu_ctx.stats()["merge_passes"] == 0
 
 
 @pytest.mark.parametrize("dtype", ["i32", "i64"])
@@ -78,7 +86,7 @@ def test_bucketed_sort_mixed_fanin(gpu_ctx, dtype, B):
     a = rng.permutation(np.concatenate([dense, tail])).astype(np.int32 if dtype == "i32" else np.int64)
     t = torch.from_numpy(a).cuda()
     out = torch.empty_like(t)
-    with gpu_ctx.options(buckets=B):
+    with gpu_ctx.options(buckets=B, sub_keys=0):
         gpu_ctx.sort_dev(t, out)
         torch.cuda.synchronize()
         assert gpu_ctx.stats()["merge_passes"] >= 1
@@ -103,26 +111,34 @@ def test_forced_buckets_small_input_matches_unforced(gpu_ctx):
         assert np.array_equal(o1.cpu().numpy(), np.sort(a))
 
 
-@pytest.mark.parametrize("skew", [0, 1])
+@pytest.mark.parametrize("dtype", ["i32", "i64"])
 @pytest.mark.parametrize("kind", ["uniform", "few", "zipfish"])
-@pytest.mark.parametrize("R", [57, 64, 71])
-def test_skewed_buckets_on_and_off(gpu_ctx, skew, kind, R):
-    """ADVICE r1 (low): skewed bucket sizes engage for B >= 16 buckets of 56 < R <= 72 mean tiles;
-    on and off, at the edges of that window, for uniform, few-distinct and duplicate-heavy int32."""
+@pytest.mark.parametrize("sub_keys,os,merged", [(-1, -1, False), (300, 1, None), (40_000, 4, True)])
+def test_sub_buckets(gpu_ctx, dtype, kind, sub_keys, os, merged):
+    """Second partition level: default sub-buckets (no merge pass), tiny ones with one sample each
+    (crowded slot tables, many empty sub-buckets), and ones larger than a tile (every sub-bucket
+    is tile-sorted in pieces and merged: merge_passes >= 1).  Duplicate-heavy keys split over
+    sub-buckets by (key, position)."""
     import torch
     B = 16
-    n = B * R * TILE + 101
-    rng = np.random.default_rng(R * 10 + skew)
+    n = B * 40 * TILE + 101
+    rng = np.random.default_rng(len(kind) * 10 + os)
     if kind == "zipfish":
-        a = (rng.zipf(1.3, n) % 100_003).astype(np.int32) * 7919 - 40_000_000
+        a = (rng.zipf(1.3, n) % 100_003) * 7919 - 40_000_000
+    elif kind == "few":
+        a = rng.integers(0, 4, n) * 1000 - 1500
     else:
-        a = _keys(rng, kind, n)
+        a = rng.integers(INT_MIN, INT_MAX, n, endpoint=True)
+    a = a.astype(np.int32 if dtype == "i32" else np.int64)
     t = torch.from_numpy(a).cuda()
     out = torch.empty_like(t)
-    with gpu_ctx.options(buckets=B, bucket_skew=skew):
+    with gpu_ctx.options(buckets=B, sub_keys=sub_keys, sub_oversample=os):
         gpu_ctx.sort_dev(t, out)
         torch.cuda.synchronize()
+        passes = gpu_ctx.stats()["merge_passes"]
     assert np.array_equal(out.cpu().numpy(), np.sort(a))
+    if merged is not None:
+        assert (passes >= 1) == merged
 
 
 def test_bucketed_default_at_2p26_matches_regular_path(gpu_ctx):
@@ -135,7 +151,7 @@ def test_bucketed_default_at_2p26_matches_regular_path(gpu_ctx):
     fp = gpu_ctx.fingerprint(t)
     o1, o2 = torch.empty_like(t), torch.empty_like(t)
     gpu_ctx.sort_dev(t, o1)
-    assert gpu_ctx.stats()["merge_passes"] == 2  # 64 buckets of ~2^20 keys: ~64 runs each
+    assert gpu_ctx.stats()["merge_passes"] == 0  # 64 buckets of ~2^20 keys, sub-buckets in tiles
     with gpu_ctx.options(buckets=0):
         gpu_ctx.sort_dev(t, o2)
     torch.cuda.synchronize()
