@@ -20,9 +20,10 @@ The sorted output is verified outside the timed region (ascending + multiset fin
 boundaries).
 
 Rank 0 prints ONE JSON line with two extra objects:
-  roofline      live HIP-event timing of the dominant kernel (the merge-path merge pass; at N > 1
-                the local sort's, slowest rank) against 8 TB/s, and at N > 1 the key exchange's
-                bytes over xGMI against (N-1) links x 153 GB/s;
+  roofline      live HIP-event timing of the dominant kernel (the tile sort, one launch over all
+                tiles: 2 x key bytes per key; at N > 1 the local sort's, slowest rank) against
+                8 TB/s, and at N > 1 the key exchange's bytes over xGMI against (N-1) links x
+                153 GB/s;
   cpu_baseline  the reference's own algorithm (client.c merge_sort on 4 threads + server.c
                 merge_chunks, compiled from the reference sources into oracle/_ref) on a bounded
                 sample, plus the reference's TCP server + 4 clients on input.txt (config C1),
@@ -367,9 +368,9 @@ def cpu_baseline(sample_keys, target_keys):
 
 
 def pmc_traffic(kernel, n, w):
-    """HBM bytes per merge pass from the newest committed rocprofv3 PMC passes (FETCH_SIZE x2 +
-    WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md), scaled to this run's key count;
-    None when absent or measured on another key width."""
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC passes
+    (FETCH_SIZE x2 + WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md), scaled to this run's
+    key count; None when absent or measured on another key width."""
     for name in ("r2_pmc_traffic.json", "r1_pmc_traffic.json"):
         path = os.path.join(REPO, "profiles", name)
         try:
@@ -380,7 +381,8 @@ def pmc_traffic(kernel, n, w):
             continue
         if w != doc.get("key_bytes", 4):
             return None
-        return round(rec.get("traffic_bytes_per_pass", rec["traffic_bytes"]) * n / doc.get("keys", 1 << 30))
+        return round(rec.get("traffic_bytes_per_launch", rec.get("traffic_bytes_per_pass", rec.get("traffic_bytes")))
+                     * n / doc.get("keys", 1 << 30))
     return None
 
 
@@ -421,7 +423,7 @@ def run_single(args):
     if not ok:
         raise SystemExit("bench: sorted output failed verification")
     torch.cuda.synchronize()
-    kms, klaunch, bms, tot, npass = 0.0, 0, 0.0, 0.0, 0
+    kms, klaunch, bms, tot, npass, tsk, pms = 0.0, 0, 0.0, 0.0, 0, 0.0, 0.0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         ctx.sort_dev(t_in, out)
@@ -431,12 +433,15 @@ def run_single(args):
         bms += st["block_sort_ms"]
         tot += st["total_ms"]
         npass += st["merge_passes"]
+        tsk += st["tile_sort_kernel_ms"]
+        pms += st["partition_ms"]
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     stats = ctx.stats()
     ctx.close()
     return t1 - t0, {"kernel_ms": kms, "launches": klaunch, "block_ms": bms, "device_ms": tot,
-                     "passes": stats["merge_passes"], "npass": npass, "tile": stats["tile_keys"], "w": w}
+                     "passes": stats["merge_passes"], "npass": npass, "tile": stats["tile_keys"], "w": w,
+                     "tile_sort_ms": tsk, "partition_ms": pms}
 
 
 def run_multi(args, rank, world):
@@ -488,11 +493,11 @@ def run_multi(args, rank, world):
     dist.barrier()
     t0 = time.perf_counter()
     acc = {"exchange_ms": 0.0, "alltoall_ms": 0.0, "final_merge_ms": 0.0, "merge_kernel_ms": 0.0,
-           "merge_kernel_launches": 0, "merge_passes": 0, "sent": 0}
+           "merge_kernel_launches": 0, "merge_passes": 0, "sent": 0, "tile_sort_kernel_ms": 0.0}
     for _ in range(args.steps):
         ptr, nout = ctx.sample_sort_dev(t_in)
         st = ctx.stats()  # synchronizes this rank's stream
-        for k in ("exchange_ms", "alltoall_ms", "final_merge_ms", "merge_kernel_ms"):
+        for k in ("exchange_ms", "alltoall_ms", "final_merge_ms", "merge_kernel_ms", "tile_sort_kernel_ms"):
             acc[k] += st[k]
         acc["merge_kernel_launches"] += st["merge_kernel_launches"]
         acc["merge_passes"] += st["merge_passes"]
@@ -504,8 +509,7 @@ def run_multi(args, rank, world):
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
     # per-rank figures of the roofline, gathered (rank 0 reports the slowest rank)
     steps = max(args.steps, 1)
-    per_pass = acc["merge_kernel_ms"] / acc["merge_passes"] if acc["merge_passes"] else 0.0
-    mine = torch.tensor([per_pass, acc["alltoall_ms"] / steps, acc["exchange_ms"] / steps,
+    mine = torch.tensor([acc["tile_sort_kernel_ms"] / steps, acc["alltoall_ms"] / steps, acc["exchange_ms"] / steps,
                          acc["final_merge_ms"] / steps, acc["sent"] / steps, sz], dtype=torch.float64)
     everyone = [torch.zeros_like(mine) for _ in range(world)]
     dist.all_gather(everyone, mine)
@@ -540,23 +544,25 @@ def report_single(args, elapsed, k):
     n = args.keys
     step_ms = 1000.0 * elapsed / args.steps
     result.update({"value": n * args.steps / elapsed, "ms_per_step": step_ms})
-    # one merge pass = one read + one write of every key; a pass of the bucketed sort is one
-    # launch per kernel fan-in among its buckets, so time is summed per pass
+    # the dominant kernel is the tile sort: one launch reads and writes every key once (the
+    # sub-bucket path gathers its tiles from the locally partitioned chunks); merge passes only
+    # run for oversized sub-buckets or with DSORT_OPT_SUB_KEYS = 0
+    tile_ms = k["tile_sort_ms"] / args.steps
+    bytes_tile = 2 * k["w"] * n
+    achieved = bytes_tile / (tile_ms * 1e-3) / 1e9 if tile_ms > 0 else 0.0
     npass = k["npass"]
-    avg_pass_ms = k["kernel_ms"] / max(npass, 1)
-    bytes_per_pass = 2 * k["w"] * n
-    achieved = bytes_per_pass / (avg_pass_ms * 1e-3) / 1e9 if k["launches"] and npass else 0.0
     cfg = "C2-style" if args.dtype == "i32" else "C4-style"
     result["config"] = {"workload": f"{cfg} single-GPU sort of {n} {args.dist} {result['dtype']} keys "
                                     f"(BASELINE metric size); tile {k['tile']} keys, {k['passes']} merge passes",
                         "keys": n, "parallelism": "1 GPU"}
     result["roofline"] = {
-        "bound": "hbm", "kernel": "mergew_kernel (k-way merge-path pass)", "achieved": round(achieved, 1),
-        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-        "traffic": pmc_traffic("mergew_kernel", n, k["w"]), "avg_pass_ms": round(avg_pass_ms, 4),
-        "algorithmic_bytes_per_pass": bytes_per_pass,
-        "launches_per_pass": round(k["launches"] / max(npass, 1), 2),
-        "partition_and_tile_sort_ms": round(k["block_ms"] / args.steps, 3),
+        "bound": "hbm", "kernel": "block_sort_w_kernel (tile sort, one launch over all tiles)",
+        "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("block_sort_w_kernel", n, k["w"]),
+        "avg_launch_ms": round(tile_ms, 4), "algorithmic_bytes_per_launch": bytes_tile,
+        "partition_ms": round(k["partition_ms"] / args.steps, 3),
+        "merge_passes": npass // max(args.steps, 1),
+        "merge_kernel_ms": round(k["kernel_ms"] / args.steps, 4),
         "whole_sort_single_pass_bound_frac": round(2 * k["w"] * n / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
     }
     if not args.no_cpu_baseline and args.dtype == "i32":
@@ -573,15 +579,15 @@ def report_multi(args, world, elapsed, per_rank, w):
                                     "(equal contiguous chunks, splitters, RCCL all-to-all over xGMI, merge)",
                         "keys": n, "keys_per_gpu": n // world, "parallelism": f"samplesort x{world}"}
     slow = int(np.argmax(per_rank[:, 0]))
-    pass_ms = float(per_rank[slow, 0])
+    tile_ms = float(per_rank[slow, 0])
     n_gpu = float(per_rank[slow, 5])
-    bpl = 2 * w * n_gpu  # one read + one write of the rank's chunk per merge pass
-    ach = bpl / (pass_ms * 1e-3) / 1e9 if pass_ms > 0 else None
-    roof = {"bound": "hbm", "kernel": "mergew_kernel (local-sort merge pass, slowest rank)",
+    bpl = 2 * w * n_gpu  # the local tile sort reads and writes the rank's chunk once
+    ach = bpl / (tile_ms * 1e-3) / 1e9 if tile_ms > 0 else None
+    roof = {"bound": "hbm", "kernel": "block_sort_w_kernel (local tile sort, slowest rank)",
             "achieved": round(ach, 1) if ach else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None,
-            "traffic": pmc_traffic("mergew_kernel", int(n_gpu), w), "avg_pass_ms": round(pass_ms, 4),
-            "algorithmic_bytes_per_pass": int(bpl),
+            "traffic": pmc_traffic("block_sort_w_kernel", int(n_gpu), w), "avg_launch_ms": round(tile_ms, 4),
+            "algorithmic_bytes_per_launch": int(bpl),
             "whole_sort_single_pass_bound_frac": round(
                 2 * w * n / (step_ms * 1e-3) / 1e9 / (HBM_PEAK_GBS * world), 4)}
     if world > 1:

@@ -793,6 +793,8 @@ int dsort_get_stats(const dsort_ctx *cctx, dsort_stats *out) {
     }
     out->block_sort_ms = el(0, 1);
     out->merge_ms = el(1, 2);
+    out->tile_sort_kernel_ms = el(7, 8);
+    out->partition_ms = el(0, 7);
     if (ctx->ev_mask & 16u) {
         out->exchange_ms = el(2, 3);
         out->final_merge_ms = el(3, 4);

@@ -120,8 +120,9 @@ struct dsort_ctx {
     void *small_host = nullptr;  // pinned
     size_t small_host_bytes = 0;
     // stage timing
-    hipEvent_t ev[8] = {};  // 0 start, 1 tile sort done, 2 local sort done, 3 exchange done,
-                            // 4 final merge done, 5/6 around the key all-to-all
+    hipEvent_t ev[9] = {};  // 0 start, 1 tile sort done, 2 local sort done, 3 exchange done,
+                            // 4 final merge done, 5/6 around the key all-to-all, 7/8 around the
+                            // tile sort kernel
     unsigned ev_mask = 0;             // events recorded by the last call (bit i = ev[i])
     hipStream_t last_stream = nullptr;  // stream of the last asynchronous call
     static constexpr int kMaxKev = 128;  // per-launch events of the merge kernel (2 per pass)

@@ -900,6 +900,14 @@ static std::vector<int> plan_passes(const dsort_ctx *ctx, uint64_t runs) {
     return out;
 }
 
+// Events 7 / 8 around the tile sort kernel (dsort_stats.tile_sort_kernel_ms, partition_ms).
+static int tile_sort_event(dsort_ctx *ctx, hipStream_t s, bool timed, int which) {
+    if (!timed || !ctx->ev_ok) return DSORT_OK;
+    DSORT_HIP(ctx, hipEventRecord(ctx->ev[7 + which], s));
+    ctx->ev_mask |= 1u << (7 + which);
+    return DSORT_OK;
+}
+
 template <typename T, bool REG>
 static int launch_pass_w(dsort_ctx *ctx, const T *src, T *dst, const PassDesc &pd, int logf,
                          uint64_t ntiles, hipStream_t s, bool timed) {
@@ -1126,9 +1134,13 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         // 3. tile sort: gathered from the chunks into d_keys
         if (ntiles) {
             const Gather ga{static_cast<const GTile *>(tt), dch, dbi, cnt, SS};
+            rc = tile_sort_event(ctx, s, timed, 0);
+            if (rc) return rc;
             hipLaunchKernelGGL((block_sort_w_kernel<T, true>), dim3(ntiles), dim3(64 * WG<T>::WAVES), 0, s, src, d_keys,
                                (uint64_t)n, nullptr, num, ga);
             DSORT_HIP(ctx, hipGetLastError());
+            rc = tile_sort_event(ctx, s, timed, 1);
+            if (rc) return rc;
         }
         if (timed && ctx->ev_ok) {
             DSORT_HIP(ctx, hipEventRecord(ctx->ev[1], s));
@@ -1160,9 +1172,13 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
     if (ntiles > tmax || novf > nsubs) return set_err(ctx, DSORT_EHIP, "sub-bucket packing overflow");
     ctx->stats.merge_passes = 0;
     if (ntiles) {
+        rc = tile_sort_event(ctx, s, timed, 0);
+        if (rc) return rc;
         hipLaunchKernelGGL((block_sort_w_kernel<T, false>), dim3(ntiles), dim3(64 * WG<T>::WAVES), 0, s, d_keys,
                            d_keys, (uint64_t)n, static_cast<const uint4 *>(tt), num, Gather{});
         DSORT_HIP(ctx, hipGetLastError());
+        rc = tile_sort_event(ctx, s, timed, 1);
+        if (rc) return rc;
     }
     if (timed && ctx->ev_ok) {
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[1], s));
@@ -1320,9 +1336,13 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
     T *bufs[2] = {d_keys, scratch};
     int cur = (passes % 2 == 0) ? 0 : 1;  // tile sort output; the passes end in d_keys
     // 3. tile sort inside the buckets
+    rc = tile_sort_event(ctx, s, timed, 0);
+    if (rc) return rc;
     hipLaunchKernelGGL((block_sort_w_kernel<T, false>), dim3((unsigned)tmax), dim3(64 * WG<T>::WAVES), 0, s, part_out,
                        bufs[cur], (uint64_t)n, reinterpret_cast<const uint4 *>(tt), ntl, sb::Gather{});
     DSORT_HIP(ctx, hipGetLastError());
+    rc = tile_sort_event(ctx, s, timed, 1);
+    if (rc) return rc;
     if (timed && ctx->ev_ok) {
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[1], s));
         ctx->ev_mask |= 2u;
@@ -1476,9 +1496,13 @@ static int wave_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipStre
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[0], s));
         ctx->ev_mask |= 1u;
     }
+    int rc = tile_sort_event(ctx, s, timed, 0);
+    if (rc) return rc;
     hipLaunchKernelGGL((block_sort_w_kernel<T, false>), dim3((unsigned)tiles), dim3(64 * WG<T>::WAVES), 0, s, d_in,
                        bufs[cur], (uint64_t)n, nullptr, nullptr, sb::Gather{});
     DSORT_HIP(ctx, hipGetLastError());
+    rc = tile_sort_event(ctx, s, timed, 1);
+    if (rc) return rc;
     if (timed && ctx->ev_ok) {
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[1], s));
         ctx->ev_mask |= 2u;

@@ -61,7 +61,8 @@ class Stats(ctypes.Structure):
                 ("merge_kernel_launches", ctypes.c_int), ("merge_passes", ctypes.c_int),
                 ("tile_keys", ctypes.c_int), ("keys_in", ctypes.c_size_t),
                 ("keys_out", ctypes.c_size_t), ("alltoall_ms", ctypes.c_double),
-                ("keys_sent", ctypes.c_size_t)]
+                ("keys_sent", ctypes.c_size_t), ("tile_sort_kernel_ms", ctypes.c_double),
+                ("partition_ms", ctypes.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

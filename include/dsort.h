@@ -65,6 +65,8 @@ typedef struct dsort_stats {
     size_t keys_out;        /* keys produced (multi-GPU: this rank's key range)           */
     double alltoall_ms;     /* multi-GPU: the key all-to-all alone (grouped send/recv)    */
     size_t keys_sent;       /* multi-GPU: keys this rank shipped to other ranks           */
+    double tile_sort_kernel_ms; /* the tile sort kernel alone (HIP events around its launch) */
+    double partition_ms;    /* bucketed sort: the partition passes before the tile sort   */
 } dsort_stats;
 
 /* ---------------------------------------------------------------- lifecycle ---------- */

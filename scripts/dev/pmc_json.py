@@ -1,0 +1,40 @@
+#!/usr/bin/env python3
+"""profiles/r2_pmc_traffic.json from the rocprofv3 databases of scripts/gpu_profile_r2.sh: per
+kernel and launch, HBM traffic = (2 x FETCH_SIZE + WRITE_SIZE) x 1 KiB (FETCH_SIZE doubled: the
+gfx950 correction of MI355X_MICROARCH.md § HBM), for the 2^30 int32 sort; the int64 Zipf sort's
+figures under "int64"."""
+import glob
+import json
+import sqlite3
+import sys
+
+
+def per_launch(tag):
+    out = {}
+    for db in sorted(glob.glob(f"gpurun_out/{tag}pmc*/**/*.db", recursive=True)):
+        c = sqlite3.connect(db)
+        q = ("select kernel_name, counter_name, sum(value), count(distinct dispatch_id) from counters_collection "
+             "group by kernel_name, counter_name")
+        for k, cn, v, nd in c.execute(q):
+            name = k.split("(")[0].replace("void ", "").split("::")[-1]
+            out.setdefault(name, {})[cn] = v / max(nd, 1)
+    res = {}
+    for k, d in out.items():
+        if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+            rec = {"fetch_kib": d["FETCH_SIZE"], "write_kib": d["WRITE_SIZE"],
+                   "traffic_bytes_per_launch": int((2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024)}
+            for extra in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_WAIT_INST_LDS",
+                          "TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum"):
+                if extra in d:
+                    rec[extra] = d[extra]
+            res[k] = rec
+    return res
+
+
+doc = {"source": "rocprofv3 --pmc (separate passes) over scripts/dev/ktime.py --reps 1, 2^30 keys",
+       "keys": 1 << 30, "key_bytes": 4, "kernels": per_launch("i32_"),
+       "int64": {"keys": 1 << 30, "key_bytes": 8, "dist": "zipf", "kernels": per_launch("i64_")}}
+json.dump(doc, open(sys.argv[1] if len(sys.argv) > 1 else "profiles/r2_pmc_traffic.json", "w"), indent=1)
+for t, ks in (("int32", doc["kernels"]), ("int64", doc["int64"]["kernels"])):
+    for k, r in ks.items():
+        print(f"{t} {k:34s} {r['traffic_bytes_per_launch'] / 1e9:8.3f} GB")

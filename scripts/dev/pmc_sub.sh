@@ -1,5 +1,6 @@
 #!/bin/bash
-# PMC passes over one 2^30 int32 sort (ktime.py --reps 1): one rocprofv3 run per counter set.
+# PMC passes over one 2^30 sort (ktime.py): one rocprofv3 run per counter set, databases under
+# gpurun_out/${TAG}pmc<i>.  ARGS = ktime arguments, TAG = output prefix.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd /tmp && export TMPDIR=/tmp
 ARGS=${ARGS:-"--reps 1"}
@@ -8,5 +9,5 @@ for set in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE
            "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_EA0_RDREQ_sum" \
            "WRITE_SIZE" "FETCH_SIZE"; do
   i=$((i+1))
-  timeout -s KILL 90 rocprofv3 --pmc $set -d $R/gpurun_out/pmc$i -o run -- python3 $R/scripts/dev/ktime.py $ARGS > $R/gpurun_out/pmc$i.log 2>&1 || exit $?
+  timeout -s KILL 90 rocprofv3 --pmc $set -d $R/gpurun_out/${TAG}pmc$i -o run -- python3 $R/scripts/dev/ktime.py $ARGS > $R/gpurun_out/${TAG}pmc$i.log 2>&1 || exit $?
 done
