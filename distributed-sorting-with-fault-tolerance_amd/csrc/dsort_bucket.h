@@ -166,6 +166,45 @@ __global__ void __launch_bounds__(BK_MAXB) bucket_splitter_kernel(const typename
     if (b < BP) spl[b] = b < B - 1 ? smp[(uint64_t)(b + 1) * os - 1] : Comp<T>::inf();
 }
 
+// int64 keys: the (key, index) pairs are sorted on the GPU in two int64 sorts -- the sampled keys
+// (keys -> srt), then composites (index of the first equal key in srt) * 2^32 + sample index,
+// whose order is the pair order -- and splitter b is the pair of composite (b+1)*os - 1.
+__device__ __forceinline__ uint64_t sample_pos(uint64_t k, uint64_t n, uint32_t s) {
+    return ((2 * k + 1) * n) / (2 * (uint64_t)s);
+}
+__global__ void __launch_bounds__(256) pair_sample_keys_kernel(const int64_t *__restrict__ in, uint64_t n,
+                                                               int64_t *__restrict__ keys, uint32_t s) {
+    const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+    if (k < s) keys[k] = in[sample_pos(k, n, s)];
+}
+__global__ void __launch_bounds__(256) pair_rank_kernel(const int64_t *__restrict__ keys,
+                                                        const int64_t *__restrict__ srt, uint32_t s,
+                                                        int64_t *__restrict__ cmp) {
+    const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= s) return;
+    const int64_t x = keys[k];
+    uint32_t lo = 0, hi = s;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (srt[mid] < x) lo = mid + 1;
+        else hi = mid;
+    }
+    cmp[k] = (int64_t)((uint64_t)lo << 32 | k);
+}
+__global__ void __launch_bounds__(BK_MAXB) pair_splitter_kernel(const int64_t *__restrict__ cmp,
+                                                                const int64_t *__restrict__ keys, uint64_t n,
+                                                                uint32_t s, int B, int BP, int os,
+                                                                Pair *__restrict__ spl) {
+    const int b = threadIdx.x;
+    if (b >= BP) return;
+    if (b < B - 1) {
+        const uint32_t g = (uint32_t)cmp[(uint64_t)(b + 1) * os - 1];
+        spl[b] = Pair{keys[g], (uint32_t)sample_pos(g, n, s), 0};
+    } else {
+        spl[b] = Comp<int64_t>::inf();
+    }
+}
+
 template <typename T>
 __device__ __forceinline__ void load_splitters(const typename Comp<T>::C *spl_g, int BP,
                                                typename Comp<T>::C *spl) {

@@ -1221,13 +1221,14 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
     const int subs = bucket_wg_subs<T>(n);
     const uint64_t G = ceil_div(n, (uint64_t)subs * BK_T * Geo<T>::KPT);
     const uint64_t nchunk = ceil_div(G, BK_CHUNK);
-    const int os = std::is_same<T, int32_t>::value ? bucket_os(ctx) : BK_OS;
+    const int os = bucket_os(ctx);
     const uint32_t S = (uint32_t)B * (uint32_t)os;
     const uint64_t tmax = ceil_div(n, TILE) + 2 * (uint64_t)B;  // + a head and a tail per bucket
     // device arena: samples, splitters, counts, chunk sums, offsets, bucket starts, tile table
     size_t off = 0;
     auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
-    const size_t o_smp = take((size_t)S * sizeof(C)), o_spl = take((size_t)BP * sizeof(C)),
+    // samples: int32 composites; int64 keys, sorted keys and composites (3 x 8 bytes)
+    const size_t o_smp = take((size_t)S * (sizeof(T) == 8 ? 24 : sizeof(C))), o_spl = take((size_t)BP * sizeof(C)),
                  o_cnt = take((size_t)G * B * 4), o_part = take((size_t)nchunk * B * 8),
                  o_offs = take((size_t)G * B * 8), o_bst = take((size_t)(B + 1) * 8),
                  o_tt = take((size_t)tmax * sizeof(TileRef)), o_nt = take(4);
@@ -1245,8 +1246,7 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
     rc = ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, n * sizeof(T), "sort scratch");
     if (rc) return rc;
     T *scratch = static_cast<T *>(ctx->scratch);
-    const size_t hbytes = (std::is_same<T, int64_t>::value ? (size_t)BK_MAXB * BK_OS * sizeof(C) : 0) +
-                          (size_t)(BK_MAXB + 1) * 8;
+    const size_t hbytes = (size_t)(BK_MAXB + 1) * 8;
     if (ctx->bucket_host_bytes < hbytes) {
         if (ctx->bucket_host) (void)hipHostFree(ctx->bucket_host);
         ctx->bucket_host = nullptr;
@@ -1256,17 +1256,27 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
     }
     if (!ctx->bucket_ev && hipEventCreateWithFlags(&ctx->bucket_ev, hipEventDisableTiming) != hipSuccess)
         return set_err(ctx, DSORT_EHIP, "hipEventCreate");
-    uint64_t *hb;
-    // 1. splitters from a regular sample in (key, input index) order
-    hipLaunchKernelGGL(bucket_sample_kernel<T>, dim3(ceil_div(S, 256)), dim3(256), 0, s, d_in, (uint64_t)n, smp, S);
-    DSORT_HIP(ctx, hipGetLastError());
+    uint64_t *hb = static_cast<uint64_t *>(ctx->bucket_host);
+    // 1. splitters from a regular sample in (key, input index) order, sorted on the GPU (the
+    // sample sorts never bucket and never fire the fault injection)
+    int64_t *pk = reinterpret_cast<int64_t *>(smp), *psrt = pk + S, *pcmp = pk + 2 * (size_t)S;
+    ++ctx->nested;
     if constexpr (std::is_same<T, int32_t>::value) {
-        // int32 composites are int64 (key * 2^32 + index): sorted on the GPU by the int64 sort
-        ++ctx->nested;  // the sample sort never buckets and never fires the fault injection
-        rc = sort_device<int64_t>(ctx, smp, smp, S, s, false);
-        --ctx->nested;
-        if (rc) return rc;
+        // int32 composites are int64 (key * 2^32 + index): one int64 sort
+        hipLaunchKernelGGL(bucket_sample_kernel<T>, dim3(ceil_div(S, 256)), dim3(256), 0, s, d_in, (uint64_t)n, smp, S);
+        rc = hipGetLastError() == hipSuccess ? sort_device<int64_t>(ctx, smp, smp, S, s, false)
+                                             : set_err(ctx, DSORT_EHIP, "bucket_sample_kernel launch");
+    } else {
+        // int64: the keys, then the composites (pair_rank_kernel)
+        hipLaunchKernelGGL(pair_sample_keys_kernel, dim3(ceil_div(S, 256)), dim3(256), 0, s, d_in, (uint64_t)n, pk, S);
+        rc = sort_device<int64_t>(ctx, pk, psrt, S, s, false);
+        if (!rc) {
+            hipLaunchKernelGGL(pair_rank_kernel, dim3(ceil_div(S, 256)), dim3(256), 0, s, pk, psrt, S, pcmp);
+            rc = sort_device<int64_t>(ctx, pcmp, pcmp, S, s, false);
+        }
     }
+    --ctx->nested;
+    if (rc) return rc;
     // (the nested sort reset the statistics and events; this sort's start from here)
     ctx->stats = dsort_stats{};
     ctx->stats.keys_in = ctx->stats.keys_out = n;
@@ -1280,16 +1290,9 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
     }
     if constexpr (std::is_same<T, int32_t>::value) {
         hipLaunchKernelGGL(bucket_splitter_kernel<int32_t>, dim3(1), dim3(BK_MAXB), 0, s, smp, B, BP, os, spl);
-        hb = static_cast<uint64_t *>(ctx->bucket_host);
     } else {
-        // int64 composites are 16-byte (key, index) pairs: the 32 B samples are sorted on the host
-        C *hs = static_cast<C *>(ctx->bucket_host);
-        DSORT_HIP(ctx, hipMemcpyAsync(hs, smp, (size_t)S * sizeof(C), hipMemcpyDeviceToHost, s));
-        DSORT_HIP(ctx, hipStreamSynchronize(s));
-        std::sort(hs, hs + S, [](const C &x, const C &y) { return Comp<T>::lt(x, y); });
-        for (int b = 0; b < BP; ++b) hs[b] = b < B - 1 ? hs[(size_t)(b + 1) * BK_OS - 1] : Comp<T>::inf();
-        DSORT_HIP(ctx, hipMemcpyAsync(spl, hs, (size_t)BP * sizeof(C), hipMemcpyHostToDevice, s));
-        hb = reinterpret_cast<uint64_t *>(hs + BK_MAXB * BK_OS);
+        hipLaunchKernelGGL(pair_splitter_kernel, dim3(1), dim3(BK_MAXB), 0, s, pcmp, pk, (uint64_t)n, S, B, BP, os,
+                           spl);
     }
     // 2. histograms, their scan, the scatter
     hipLaunchKernelGGL(bucket_hist_kernel<T>, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, B, BP, subs, cnt);
