@@ -50,10 +50,13 @@ def _sort(ctx, a, inplace):
 @pytest.mark.parametrize("B,n", [(2, 100_003), (3, 17), (7, 3 * TILE + 5), (33, 1_000_003),
                                  (64, 4 * TILE), (1024, 500_000)])
 @pytest.mark.parametrize("inplace", [False, True])
-@pytest.mark.parametrize("sub", [-1, 0])
-def test_bucketed_sort_vs_numpy(gpu_ctx, kind, B, n, inplace, sub):
+@pytest.mark.parametrize("mode", ["local", "scatter", "merge"])
+def test_bucketed_sort_vs_numpy(gpu_ctx, kind, B, n, inplace, mode):
+    """Every second-level path: local partition + gathering tile sort (default), scatter to
+    sub-buckets, and round 1's merge passes inside the buckets."""
     a = _keys(np.random.default_rng(B * 131 + n), kind, n)
-    with gpu_ctx.options(buckets=B, sub_keys=sub):
+    opts = {"local": dict(), "scatter": dict(sub_gather=0), "merge": dict(sub_keys=0)}[mode]
+    with gpu_ctx.options(buckets=B, **opts):
         assert np.array_equal(_sort(gpu_ctx, a, inplace), np.sort(a))
 
 
@@ -179,9 +182,10 @@ def _keys64(rng, kind, n):
 @pytest.mark.parametrize("kind", ["uniform", "equal", "few", "extremes", "small"])
 @pytest.mark.parametrize("B,n", [(2, 50_001), (5, 4096 * 3 + 1), (64, 1_000_003), (1024, 300_000)])
 @pytest.mark.parametrize("inplace", [False, True])
-def test_bucketed_sort_i64_vs_numpy(gpu_ctx, kind, B, n, inplace):
+@pytest.mark.parametrize("mode", ["local", "scatter"])
+def test_bucketed_sort_i64_vs_numpy(gpu_ctx, kind, B, n, inplace, mode):
     a = _keys64(np.random.default_rng(B * 7 + n), kind, n)
-    with gpu_ctx.options(buckets=B):
+    with gpu_ctx.options(buckets=B, sub_gather=1 if mode == "local" else 0):
         assert np.array_equal(_sort(gpu_ctx, a, inplace), np.sort(a))
 
 
