@@ -1020,7 +1020,12 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
     const uint64_t CH = local ? SB_LCH<T> : SB_CH<T>;
     // samples per sub-bucket; a bucket's samples (<= SB_MAXS * 8) fit one int64 tile
     constexpr int kMaxOs = TILE_OF<int64_t> / SB_MAXS;
-    const int os = ctx->opt.sub_os > 0 ? (ctx->opt.sub_os < kMaxOs ? (int)ctx->opt.sub_os : kMaxOs) : 4;
+    int os = ctx->opt.sub_os > 0 ? (ctx->opt.sub_os < kMaxOs ? (int)ctx->opt.sub_os : kMaxOs) : 4;
+    // buckets so large that even SB_MAXS sub-buckets average above a quarter tile: sample at the
+    // maximum rate, so the size spread (about 1/sqrt(os)) keeps every sub-bucket below a tile
+    if (ctx->opt.sub_os <= 0)
+        for (int b = 0; b < B; ++b)
+            if (hb[b + 1] - hb[b] > (uint64_t)SB_MAXS * TILE / 4) os = kMaxOs;
     // bucket and chunk tables
     std::vector<BInfo> bi((size_t)B);
     uint64_t nsmp = 0, nch = 0, nsubs = 0;
