@@ -680,7 +680,7 @@ int dsort_finalize(dsort_ctx *ctx) {
     }
     void *bufs[] = {ctx->scratch, ctx->scratch2, ctx->splits, ctx->groups, ctx->io, ctx->io2, ctx->red,
                     ctx->local, ctx->recv, ctx->recv2, ctx->small, ctx->text_status,
-                    ctx->bucket, ctx->sub};
+                    ctx->bucket, ctx->sub, ctx->tfb};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (ctx->red_host) (void)hipHostFree(ctx->red_host);
@@ -693,6 +693,8 @@ int dsort_finalize(dsort_ctx *ctx) {
     if (ctx->bucket_ev) (void)hipEventDestroy(ctx->bucket_ev);
     if (ctx->sub_host) (void)hipHostFree(ctx->sub_host);
     if (ctx->sub_ev) (void)hipEventDestroy(ctx->sub_ev);
+    if (ctx->tfb_host) (void)hipHostFree(ctx->tfb_host);
+    if (ctx->tfb_ev) (void)hipEventDestroy(ctx->tfb_ev);
     for (auto &e : ctx->ev)
         if (e) (void)hipEventDestroy(e);
     for (auto &e : ctx->kev)

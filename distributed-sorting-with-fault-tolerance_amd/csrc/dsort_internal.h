@@ -95,6 +95,10 @@ struct dsort_ctx {
     void *sub_host = nullptr;     // pinned: bucket table, chunk table, tile / merge-record counts
     size_t sub_host_bytes = 0;
     hipEvent_t sub_ev = nullptr;
+    void *tfb = nullptr;          // tiles the bin sort declined (+ their count)
+    size_t tfb_bytes = 0;
+    uint32_t *tfb_host = nullptr; // pinned: that count
+    hipEvent_t tfb_ev = nullptr;
     void *text_status = nullptr;  // per-tile look-back status words of the text codec
     size_t text_status_bytes = 0;
     void *red = nullptr;       // 64 B of reduction accumulators

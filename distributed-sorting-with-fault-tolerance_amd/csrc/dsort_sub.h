@@ -332,6 +332,7 @@ struct Gather {
     const BInfo *bi;
     const uint32_t *pref;
     int SS;
+    const void *spl;  // the splitters (Spl<T>, SS per bucket): equal neighbours = a duplicate run
 };
 
 // LOCAL: the chunk histograms are the prefix tables of sb_local_kernel (pref[c][j+1] -

@@ -284,6 +284,24 @@ __device__ __forceinline__ void sort16(T (&v)[R]) {  // Batcher odd-even merge s
     }
 }
 
+// Batcher odd-even merge sort of K keys in registers (K a power of two).
+template <int K, typename T>
+__device__ __forceinline__ void sort_net(T (&v)[K]) {
+#pragma unroll
+    for (int p = 1; p < K; p <<= 1) {
+#pragma unroll
+        for (int k = p; k >= 1; k >>= 1) {
+#pragma unroll
+            for (int j = k % p; j + k < K; j += 2 * k) {
+#pragma unroll
+                for (int i = 0; i < k; ++i) {
+                    if (i + j + k < K && (i + j) / (2 * p) == (i + j + k) / (2 * p)) cex(v[i + j], v[i + j + k]);
+                }
+            }
+        }
+    }
+}
+
 // Half-cleaner on element bit b of a lane-major wave (b <= 8).
 template <int B, typename T>
 __device__ __forceinline__ void hc_lane_major(T (&x)[R], const T (&c)[6]) {
@@ -491,6 +509,248 @@ template <> struct V16<int64_t> {
 };
 
 // ------------------------------------------------------------------------------------------
+// Bin sort of a tile.  After the two partition levels a tile covers a narrow key range that its
+// keys fill about evenly (they are a contiguous run of sampled sub-buckets), so binning them by
+// (key - min) over the tile's range into TILE/4 bins leaves about 4 keys per bin: a counting pass into
+// LDS (counts, then cursors) groups the keys by bin; three passes of 16-key sorting networks,
+// one window per thread in registers, at offsets 0, 8, 0, then sort every bin of at most 16 keys
+// (sorting a window of bin-grouped keys keeps them grouped, and inside one bin the passes are an
+// odd-even transposition sort of 8-key blocks).  About 60 operations per key instead of the ~180
+// of the bitonic tile sort.  Keys equal to key_max
+// (and the tile's padding, which is key_max) are not binned: the output ends with valid - M of
+// them, M = the binned keys.  A bin of more than 16 keys is only sorted by the window passes when
+// it holds one key value (a duplicate run, the usual case of a big bin); the result is checked at
+// the window boundaries, and on a descent the function returns false and the caller runs the
+// bitonic sort (x is left untouched).
+#ifndef DSORT_BIN_SORT
+#define DSORT_BIN_SORT 1
+#endif
+
+
+template <typename T>
+__device__ __forceinline__ T wave_min(T v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const T y = __shfl_xor(v, o);
+        v = y < v ? y : v;
+    }
+    return v;
+}
+template <typename T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const T y = __shfl_xor(v, o);
+        v = y > v ? y : v;
+    }
+    return v;
+}
+
+template <typename T>
+struct BinLds {
+    uint32_t hw[TILE_OF<T> / 8];  // 16-bit bin counters, then bin starts (two per word)
+    T mn[WG<T>::WAVES], mx[WG<T>::WAVES];
+    uint64_t wsum[WG<T>::WAVES];
+};
+
+// Bin of key offset `off` (key - min): the top 32 bits of the offset times a 32-bit reciprocal
+// of the range, so all NB bins are used (monotone in the key, < NB).
+template <typename T>
+struct BinMap {
+    using U = typename sb::KeyU<T>::U;
+    uint32_t pre;    // offsets are shifted right by pre first (int64 ranges above 2^32)
+    uint32_t scale;  // floor(NB * 2^32 / ((range >> pre) + 1)), capped
+    __device__ __forceinline__ uint32_t operator()(U off) const {
+        return __umulhi((uint32_t)(off >> pre), scale);
+    }
+};
+
+// The keys of one register slot into the bins.  HOT: the lanes whose bin is the first active
+// lane's add with one atomic (a duplicate run puts a whole wave into one bin).  SCATTER: the
+// atomic returns the bin's cursor and the key goes to s there; else it only counts.
+template <bool HOT, bool SCATTER, typename T>
+__device__ __forceinline__ void bin_put(T xv, T mn, const BinMap<T> &bm, uint32_t *hw, T *s, int lane) {
+    using U = typename sb::KeyU<T>::U;
+    const bool act = xv != key_max<T>();
+    const uint32_t b = bm((U)xv - (U)mn);
+    const uint32_t inc = (b & 1) ? 0x10000u : 1u;
+    if constexpr (!HOT) {
+        if (act) {
+            if constexpr (SCATTER) {
+                const uint32_t old = atomicAdd(&hw[b >> 1], inc);
+                s[(b & 1) ? old >> 16 : old & 0xFFFFu] = xv;
+            } else {
+                atomicAdd(&hw[b >> 1], inc);
+            }
+        }
+    } else {
+        const uint64_t am = __ballot(act);
+        if (!am) return;
+        const int first = (int)__ffsll((long long)am) - 1;
+        const uint32_t b0 = (uint32_t)__shfl((int)b, first);
+        const uint64_t same = __ballot(act && b == b0);
+        const uint32_t inc0 = ((b0 & 1) ? 0x10000u : 1u) * (uint32_t)__popcll(same);
+        if constexpr (SCATTER) {
+            uint32_t pos = 0;
+            if (act && b != b0) {
+                const uint32_t old = atomicAdd(&hw[b >> 1], inc);
+                pos = (b & 1) ? old >> 16 : old & 0xFFFFu;
+            }
+            uint32_t old0 = 0;
+            if (lane == first) old0 = atomicAdd(&hw[b0 >> 1], inc0);
+            old0 = (uint32_t)__shfl((int)old0, first);
+            if (act && b == b0)
+                pos = ((b0 & 1) ? old0 >> 16 : old0 & 0xFFFFu) + (uint32_t)__popcll(same & ((1ull << lane) - 1));
+            if (act) s[pos] = xv;
+        } else {
+            if (act && b != b0) atomicAdd(&hw[b >> 1], inc);
+            if (lane == first) atomicAdd(&hw[b0 >> 1], inc0);
+        }
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ bool bin_sort_tile(const T (&x)[R], int valid, T *s, BinLds<T> &L, T *out,
+                                              bool hot_hint) {
+    using U = typename sb::KeyU<T>::U;
+    constexpr int TILE = TILE_OF<T>, WAVES = WG<T>::WAVES, THREADS = 64 * WAVES, NB = TILE / 4;
+    constexpr int BPT = NB / THREADS;
+    static_assert(BPT == 4, "four bins per thread");
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    // 1. range of the keys below key_max
+    T mn = key_max<T>(), mx = key_min<T>();
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        if (x[i] != key_max<T>()) {
+            mn = x[i] < mn ? x[i] : mn;
+            mx = x[i] > mx ? x[i] : mx;
+        }
+    }
+    mn = wave_min(mn);
+    mx = wave_max(mx);
+    if (lane == 0) {
+        L.mn[w] = mn;
+        L.mx[w] = mx;
+    }
+    for (int q = tid; q < NB / 2; q += THREADS) L.hw[q] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < WAVES; ++i) {
+        mn = L.mn[i] < mn ? L.mn[i] : mn;
+        mx = L.mx[i] > mx ? L.mx[i] : mx;
+    }
+    if (mx < mn) {  // every key is key_max
+        for (int i = tid; i < valid; i += THREADS) out[i] = key_max<T>();
+        return true;
+    }
+    const U range = (U)mx - (U)mn;
+    BinMap<T> bm;
+    bm.pre = 0;
+    while ((range >> bm.pre) > (U)0xFFFFFFFFu) ++bm.pre;
+    const uint64_t den = (uint64_t)(uint32_t)(range >> bm.pre) + 1;
+    const uint64_t sc = ((uint64_t)NB << 32) / den;
+    bm.scale = sc > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)sc;
+    // a hot tile (some wave's first keys share a bin: a duplicate run) counts with aggregated
+    // atomics
+    const bool act0 = x[0] != key_max<T>();
+    const uint32_t bx = bm((U)x[0] - (U)mn);
+    const uint32_t bf = (uint32_t)__builtin_amdgcn_readfirstlane((int)bx);
+    const bool hot = __syncthreads_or(hot_hint || (lane == 0 && __popcll(__ballot(act0 && bx == bf)) >= 8));
+    // 2. counting (16-bit counters, two bins per word)
+    if (hot) {
+#pragma unroll
+        for (int i = 0; i < R; ++i) bin_put<true, false>(x[i], mn, bm, L.hw, s, lane);
+    } else {
+#pragma unroll
+        for (int i = 0; i < R; ++i) bin_put<false, false>(x[i], mn, bm, L.hw, s, lane);
+    }
+    __syncthreads();
+    // 3. my bins are tid + k * THREADS; bins in order = k-major, so one scan of the four 16-bit
+    // counts packed in a 64-bit word gives every bin's start
+    uint32_t cnt[BPT];
+#pragma unroll
+    for (int k = 0; k < BPT; ++k) {
+        const uint32_t b = (uint32_t)(tid + k * THREADS), wd = L.hw[b >> 1];
+        cnt[k] = (b & 1) ? wd >> 16 : wd & 0xFFFFu;
+    }
+    const uint64_t pv = (uint64_t)cnt[0] | (uint64_t)cnt[1] << 16 | (uint64_t)cnt[2] << 32 | (uint64_t)cnt[3] << 48;
+    uint64_t incl = pv;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) L.wsum[w] = incl;
+    __syncthreads();
+    uint64_t ex = incl - pv, tot = 0;
+#pragma unroll
+    for (int i = 0; i < WAVES; ++i) {
+        ex += i < w ? L.wsum[i] : 0;
+        tot += L.wsum[i];
+    }
+    uint32_t st[BPT];
+    uint32_t before = 0;  // keys in the bins of lower k
+#pragma unroll
+    for (int k = 0; k < BPT; ++k) {
+        st[k] = before + (uint32_t)((ex >> (16 * k)) & 0xFFFFu);
+        before += (uint32_t)((tot >> (16 * k)) & 0xFFFFu);
+    }
+    const uint32_t M = before;  // binned keys
+    __syncthreads();            // every count read before the starts overwrite them
+#pragma unroll
+    for (int k = 0; k < BPT; ++k) {  // bin b (even) and b + 1 sit in adjacent lanes: one word
+        const uint32_t nb = __shfl_down(st[k], 1);
+        if (!(tid & 1)) L.hw[(tid + k * THREADS) >> 1] = st[k] | nb << 16;
+    }
+    __syncthreads();
+    // 4. keys to their bins: the starts are cursors now
+    if (hot) {
+#pragma unroll
+        for (int i = 0; i < R; ++i) bin_put<true, true>(x[i], mn, bm, L.hw, s, lane);
+    } else {
+#pragma unroll
+        for (int i = 0; i < R; ++i) bin_put<false, true>(x[i], mn, bm, L.hw, s, lane);
+    }
+    __syncthreads();
+    // 5. three passes of 16-key windows, one per thread (offsets 0, 8, 0): within a bin of at most
+    // 16 keys (at most three 8-key blocks) this is an odd-even transposition of blocks, so every
+    // bin ends sorted.  Slots past the binned keys read as key_max and are not written back.
+#pragma unroll 1
+    for (int p = 0; p < 3; ++p) {
+        const int ws = 16 * tid + (p == 1 ? 8 : 0);
+        T v[16];
+        if (ws + 16 <= (int)M && !(ws & (KPC<T> - 1))) {
+            using V = typename V16<T>::type;
+            const V *src = reinterpret_cast<const V *>(s + ws);
+#pragma unroll
+            for (int q = 0; q < 16 / KPC<T>; ++q) V16<T>::get(src[q], v + KPC<T> * q);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) v[k] = ws + k < (int)M ? s[ws + k] : key_max<T>();
+        }
+        sort_net<16>(v);
+        __syncthreads();  // every window read before any is written (offset windows overlap)
+        if (ws + 16 <= (int)M && !(ws & (KPC<T> - 1))) {
+            using V = typename V16<T>::type;
+            V *dst = reinterpret_cast<V *>(s + ws);
+#pragma unroll
+            for (int q = 0; q < 16 / KPC<T>; ++q) dst[q] = V16<T>::make(v + KPC<T> * q);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if (ws + k < (int)M) s[ws + k] = v[k];
+        }
+        __syncthreads();
+    }
+    // 6. every window is sorted now; a bin of more than 16 keys holding more than one key value
+    // (rare: not a duplicate run) may still leave a descent at a window boundary
+    const bool bad = 16 * tid + 16 < (int)M && s[16 * tid + 15] > s[16 * tid + 16];
+    if (__syncthreads_or(bad)) return false;
+    // 7. out: the binned keys in order, then key_max
+    for (int i = tid; i < valid; i += THREADS) out[i] = (uint32_t)i < M ? s[i] : key_max<T>();
+    return true;
+}
+
+// ------------------------------------------------------------------------------------------
 // 1. Tile sort.
 // ------------------------------------------------------------------------------------------
 // tiles: NULL = tile j is keys [j * TILE, (j + 1) * TILE) of n; else tile j = tiles[j] (the
@@ -575,43 +835,37 @@ __device__ __forceinline__ void gather_tile(const sb::Gather &ga, const sb::GTil
     }
 }
 
+// Tile j's keys into x (any order; slots past `valid` are key_max).  Returns false when j is
+// past the tile count (the grid is an upper bound).
 template <typename T, bool GATHER>
-__global__ void __launch_bounds__(64 * WG<T>::WAVES, WG<T>::OCC) block_sort_w_kernel(
-    const T *in, T *out, uint64_t n, const uint4 *tiles, const uint32_t *ntiles, sb::Gather ga) {
+__device__ __forceinline__ bool load_tile(const T *in, uint64_t n, const uint4 *tiles, const uint32_t *ntiles,
+                                          const sb::Gather &ga, uint32_t j, T *s, T (&x)[R], uint64_t &base,
+                                          int &valid) {
     constexpr int TILE = TILE_OF<T>, N = KPC<T>;
     using V = typename V16<T>::type;
-    // `in` may alias `out`: every workgroup reads its tile before it writes it
-    __shared__ __attribute__((aligned(16))) T s[TILE + WK];  // + slack read by load_window
     const int t = lane_id();
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
-    uint64_t base;
-    int valid;
     if constexpr (GATHER) {
-        if (blockIdx.x >= *ntiles) return;
-        const sb::GTile gt = ga.tiles[blockIdx.x];
+        if (j >= *ntiles) return false;
+        const sb::GTile gt = ga.tiles[j];
         base = gt.base;
         valid = (int)gt.valid;
+        gather_tile<T>(ga, gt, in, s, x);  // (the piece table sits in the slack, not in the runs)
+        return true;
     } else if (tiles) {
-        if (blockIdx.x >= *ntiles) return;  // the grid is an upper bound
-        const uint4 r = tiles[blockIdx.x];  // TileRef: base (2 words), valid
+        if (j >= *ntiles) return false;
+        const uint4 r = tiles[j];  // TileRef: base (2 words), valid
         base = (uint64_t)r.x | ((uint64_t)r.y << 32);
         valid = (int)r.z;
     } else {
-        base = (uint64_t)blockIdx.x * TILE;
+        base = (uint64_t)j * TILE;
+        if (base >= n) return false;
         const uint64_t rem = n - base;
         valid = rem < (uint64_t)TILE ? (int)rem : TILE;
     }
-    const T c[6] = {lane_side<T>(0), lane_side<T>(1), lane_side<T>(2), lane_side<T>(3), lane_side<T>(4),
-                    lane_side<T>(5)};
-
-    // The wave's 1024 keys in any order (the order inside a wave is irrelevant before a sort):
-    // register N q + j of lane t holds key N (64 q + t) + j of the wave's range.
-    T x[R];
     // off = keys between the 16-byte boundary below the tile and its first key
     const int off = (int)((reinterpret_cast<uintptr_t>(in + base) / sizeof(T)) & (N - 1));
-    if constexpr (GATHER) {
-        gather_tile<T>(ga, ga.tiles[blockIdx.x], in, s, x);  // (the runs go to LDS, not the slack)
-    } else if (off + valid <= TILE) {
+    if (off + valid <= TILE) {
         // 16-byte vectors from the boundary; entries outside [off, off + valid) become +inf.  A
         // vector is loaded only when it holds a key of the tile (an aligned 16-byte block never
         // crosses a page); the keys of a neighbouring tile it also holds are dropped.
@@ -622,21 +876,75 @@ __global__ void __launch_bounds__(64 * WG<T>::WAVES, WG<T>::OCC) block_sort_w_ke
             const int e0 = w * WK + N * (q * 64 + t);
             T vals[N];
 #pragma unroll
-            for (int j = 0; j < N; ++j) vals[j] = key_max<T>();
+            for (int jj = 0; jj < N; ++jj) vals[jj] = key_max<T>();
             if (e0 < lim) V16<T>::get(src[q * 64 + t], vals);
 #pragma unroll
-            for (int j = 0; j < N; ++j) x[N * q + j] = (e0 + j >= off && e0 + j < lim) ? vals[j] : key_max<T>();
+            for (int jj = 0; jj < N; ++jj)
+                x[N * q + jj] = (e0 + jj >= off && e0 + jj < lim) ? vals[jj] : key_max<T>();
         }
     } else {
 #pragma unroll
         for (int q = 0; q < R / N; ++q) {
 #pragma unroll
-            for (int j = 0; j < N; ++j) {
-                const int e = w * WK + N * (q * 64 + t) + j;
-                x[N * q + j] = e < valid ? in[base + e] : key_max<T>();
+            for (int jj = 0; jj < N; ++jj) {
+                const int e = w * WK + N * (q * 64 + t) + jj;
+                x[N * q + jj] = e < valid ? in[base + e] : key_max<T>();
             }
         }
     }
+    return true;
+}
+
+// The bin sort of every tile (bin_sort_tile); a tile it declines is appended to fb (*nfb) for
+// the bitonic kernel.  Separate from the bitonic kernel so that each keeps its own registers.
+#ifndef DSORT_BIN_OCC
+#define DSORT_BIN_OCC WG<T>::OCC
+#endif
+template <typename T, bool GATHER>
+__global__ void __launch_bounds__(64 * WG<T>::WAVES, DSORT_BIN_OCC) bin_sort_kernel(const T *in, T *out, uint64_t n,
+                                                                     const uint4 *tiles, const uint32_t *ntiles,
+                                                                     sb::Gather ga, uint32_t *fb, uint32_t *nfb) {
+    constexpr int TILE = TILE_OF<T>;
+    __shared__ __attribute__((aligned(16))) T s[TILE + WK];
+    __shared__ BinLds<T> bl;
+    T x[R];
+    uint64_t base;
+    int valid;
+    if (!load_tile<T, GATHER>(in, n, tiles, ntiles, ga, blockIdx.x, s, x, base, valid)) return;
+    if (valid == 0) return;
+    // a duplicate run inside a gathered tile shows as two equal neighbouring splitters
+    bool hint = false;
+    if constexpr (GATHER) {
+        const sb::GTile gt = ga.tiles[blockIdx.x];
+        const sb::Spl<T> *sp = static_cast<const sb::Spl<T> *>(ga.spl) + (uint64_t)gt.b * ga.SS;
+        const int jl = gt.j0 > 0 ? (int)gt.j0 - 1 : 0, jh = (int)gt.j1 - 1;  // splitters around the tile
+        const int nspl = (int)ga.bi[gt.b].nsub - 1;
+        const int j = jl + lane_id();
+        if (j < jh && j + 1 < nspl) hint = sp[j].k == sp[j + 1].k;
+        hint = __ballot(hint) != 0;
+    }
+    if (!bin_sort_tile<T>(x, valid, s, bl, out + base, hint) && threadIdx.x == 0) fb[atomicAdd(nfb, 1u)] = blockIdx.x;
+}
+
+// The bitonic tile sort: tile fb[blockIdx.x] (fb = the bin sort's declined tiles) or tile
+// blockIdx.x (fb = NULL).
+template <typename T, bool GATHER>
+__global__ void __launch_bounds__(64 * WG<T>::WAVES, WG<T>::OCC) block_sort_w_kernel(
+    const T *in, T *out, uint64_t n, const uint4 *tiles, const uint32_t *ntiles, sb::Gather ga,
+    const uint32_t *fb) {
+    constexpr int TILE = TILE_OF<T>, N = KPC<T>;
+    using V = typename V16<T>::type;
+    // `in` may alias `out`: every workgroup reads its tile before it writes it
+    __shared__ __attribute__((aligned(16))) T s[TILE + WK];  // + slack read by load_window
+    const int t = lane_id();
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
+    const T c[6] = {lane_side<T>(0), lane_side<T>(1), lane_side<T>(2), lane_side<T>(3), lane_side<T>(4),
+                    lane_side<T>(5)};
+    T x[R];
+    uint64_t base;
+    int valid;
+    const uint32_t j = fb ? fb[blockIdx.x] : blockIdx.x;
+    if (!load_tile<T, GATHER>(in, n, tiles, ntiles, ga, j, s, x, base, valid)) return;
     sort_wave(x, c);
     // lane-major run of the wave -> LDS; odd waves' runs (the B runs of the first level) are
     // stored descending
@@ -908,6 +1216,43 @@ static int tile_sort_event(dsort_ctx *ctx, hipStream_t s, bool timed, int which)
     return DSORT_OK;
 }
 
+// The tile sort of `grid` tiles (an upper bound when the count lives on the device): the bin
+// sort first, then the bitonic sort of the tiles it declined (their count read back: the host
+// waits for the bin sort, which is the last work queued).  Events 7 / 8 around both.
+template <typename T, bool GATHER>
+static int tile_sort(dsort_ctx *ctx, const T *in, T *out, uint64_t n, const uint4 *tiles, const uint32_t *ntiles,
+                     const sb::Gather &ga, uint32_t grid, hipStream_t s, bool timed) {
+    const dim3 blk(64 * WG<T>::WAVES);
+    int rc = tile_sort_event(ctx, s, timed, 0);
+    if (rc) return rc;
+    if (DSORT_BIN_SORT && grid) {
+        rc = ensure(ctx, &ctx->tfb, &ctx->tfb_bytes, ((size_t)grid + 1) * 4, "tile fallback list");
+        if (rc) return rc;
+        if (!ctx->tfb_host) DSORT_HIP(ctx, hipHostMalloc((void **)&ctx->tfb_host, 64, hipHostMallocDefault));
+        if (!ctx->tfb_ev && hipEventCreateWithFlags(&ctx->tfb_ev, hipEventDisableTiming) != hipSuccess)
+            return set_err(ctx, DSORT_EHIP, "hipEventCreate");
+        uint32_t *fb = static_cast<uint32_t *>(ctx->tfb), *nfb = fb + grid;
+        DSORT_HIP(ctx, hipMemsetAsync(nfb, 0, 4, s));
+        hipLaunchKernelGGL((bin_sort_kernel<T, GATHER>), dim3(grid), blk, 0, s, in, out, n, tiles, ntiles, ga, fb, nfb);
+        DSORT_HIP(ctx, hipGetLastError());
+        DSORT_HIP(ctx, hipMemcpyAsync(ctx->tfb_host, nfb, 4, hipMemcpyDeviceToHost, s));
+        DSORT_HIP(ctx, hipEventRecord(ctx->tfb_ev, s));
+        DSORT_HIP(ctx, hipEventSynchronize(ctx->tfb_ev));
+        const uint32_t nf = *ctx->tfb_host;
+        if (nf > grid) return set_err(ctx, DSORT_EHIP, "tile fallback overflow");
+        if (nf) {
+            hipLaunchKernelGGL((block_sort_w_kernel<T, GATHER>), dim3(nf), blk, 0, s, in, out, n, tiles, ntiles, ga,
+                               static_cast<const uint32_t *>(fb));
+            DSORT_HIP(ctx, hipGetLastError());
+        }
+    } else if (grid) {
+        hipLaunchKernelGGL((block_sort_w_kernel<T, GATHER>), dim3(grid), blk, 0, s, in, out, n, tiles, ntiles, ga,
+                           static_cast<const uint32_t *>(nullptr));
+        DSORT_HIP(ctx, hipGetLastError());
+    }
+    return tile_sort_event(ctx, s, timed, 1);
+}
+
 template <typename T, bool REG>
 static int launch_pass_w(dsort_ctx *ctx, const T *src, T *dst, const PassDesc &pd, int logf,
                          uint64_t ntiles, hipStream_t s, bool timed) {
@@ -1104,15 +1449,13 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         DSORT_HIP(ctx, hipGetLastError());
         const uint4 *stl4 = reinterpret_cast<const uint4 *>(stl);
         const uint32_t *pnst = reinterpret_cast<const uint32_t *>(stl + B);
-        const dim3 sblk(64 * WG<int64_t>::WAVES);
         if constexpr (sizeof(T) == 8) {  // int64: sort the keys, rank them, then the composites
-            hipLaunchKernelGGL((block_sort_w_kernel<int64_t, false>), dim3(nst), sblk, 0, s, smp, srt, nsmp, stl4, pnst,
-                               sb::Gather{});
+            rc = tile_sort<int64_t, false>(ctx, smp, srt, nsmp, stl4, pnst, sb::Gather{}, nst, s, false);
+            if (rc) return rc;
             hipLaunchKernelGGL(sb_rank_kernel, dim3((unsigned)B), dim3(SB_T), 0, s, smp, srt, dbi, cmp);
         }
-        hipLaunchKernelGGL((block_sort_w_kernel<int64_t, false>), dim3(nst), sblk, 0, s, cmp, cmp, nsmp, stl4, pnst,
-                           sb::Gather{});
-        DSORT_HIP(ctx, hipGetLastError());
+        rc = tile_sort<int64_t, false>(ctx, cmp, cmp, nsmp, stl4, pnst, sb::Gather{}, nst, s, false);
+        if (rc) return rc;
         hipLaunchKernelGGL(sb_splitter_kernel<T>, dim3((unsigned)B), dim3(SB_MAXS), 0, s, cmp, smp, dbi, os, SS, spl,
                            rng, sfn);
         DSORT_HIP(ctx, hipGetLastError());
@@ -1138,13 +1481,8 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         ctx->stats.merge_passes = 0;
         // 3. tile sort: gathered from the chunks into d_keys
         if (ntiles) {
-            const Gather ga{static_cast<const GTile *>(tt), dch, dbi, cnt, SS};
-            rc = tile_sort_event(ctx, s, timed, 0);
-            if (rc) return rc;
-            hipLaunchKernelGGL((block_sort_w_kernel<T, true>), dim3(ntiles), dim3(64 * WG<T>::WAVES), 0, s, src, d_keys,
-                               (uint64_t)n, nullptr, num, ga);
-            DSORT_HIP(ctx, hipGetLastError());
-            rc = tile_sort_event(ctx, s, timed, 1);
+            const Gather ga{static_cast<const GTile *>(tt), dch, dbi, cnt, SS, spl};
+            rc = tile_sort<T, true>(ctx, src, d_keys, n, nullptr, num, ga, ntiles, s, timed);
             if (rc) return rc;
         }
         if (timed && ctx->ev_ok) {
@@ -1177,12 +1515,8 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
     if (ntiles > tmax || novf > nsubs) return set_err(ctx, DSORT_EHIP, "sub-bucket packing overflow");
     ctx->stats.merge_passes = 0;
     if (ntiles) {
-        rc = tile_sort_event(ctx, s, timed, 0);
-        if (rc) return rc;
-        hipLaunchKernelGGL((block_sort_w_kernel<T, false>), dim3(ntiles), dim3(64 * WG<T>::WAVES), 0, s, d_keys,
-                           d_keys, (uint64_t)n, static_cast<const uint4 *>(tt), num, Gather{});
-        DSORT_HIP(ctx, hipGetLastError());
-        rc = tile_sort_event(ctx, s, timed, 1);
+        rc = tile_sort<T, false>(ctx, d_keys, d_keys, n, static_cast<const uint4 *>(tt), num, Gather{}, ntiles, s,
+                                 timed);
         if (rc) return rc;
     }
     if (timed && ctx->ev_ok) {
@@ -1344,12 +1678,8 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
     T *bufs[2] = {d_keys, scratch};
     int cur = (passes % 2 == 0) ? 0 : 1;  // tile sort output; the passes end in d_keys
     // 3. tile sort inside the buckets
-    rc = tile_sort_event(ctx, s, timed, 0);
-    if (rc) return rc;
-    hipLaunchKernelGGL((block_sort_w_kernel<T, false>), dim3((unsigned)tmax), dim3(64 * WG<T>::WAVES), 0, s, part_out,
-                       bufs[cur], (uint64_t)n, reinterpret_cast<const uint4 *>(tt), ntl, sb::Gather{});
-    DSORT_HIP(ctx, hipGetLastError());
-    rc = tile_sort_event(ctx, s, timed, 1);
+    rc = tile_sort<T, false>(ctx, part_out, bufs[cur], n, reinterpret_cast<const uint4 *>(tt), ntl, sb::Gather{},
+                             (uint32_t)tmax, s, timed);
     if (rc) return rc;
     if (timed && ctx->ev_ok) {
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[1], s));
@@ -1504,12 +1834,7 @@ static int wave_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipStre
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[0], s));
         ctx->ev_mask |= 1u;
     }
-    int rc = tile_sort_event(ctx, s, timed, 0);
-    if (rc) return rc;
-    hipLaunchKernelGGL((block_sort_w_kernel<T, false>), dim3((unsigned)tiles), dim3(64 * WG<T>::WAVES), 0, s, d_in,
-                       bufs[cur], (uint64_t)n, nullptr, nullptr, sb::Gather{});
-    DSORT_HIP(ctx, hipGetLastError());
-    rc = tile_sort_event(ctx, s, timed, 1);
+    int rc = tile_sort<T, false>(ctx, d_in, bufs[cur], n, nullptr, nullptr, sb::Gather{}, (uint32_t)tiles, s, timed);
     if (rc) return rc;
     if (timed && ctx->ev_ok) {
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[1], s));

@@ -16,11 +16,16 @@ ap.add_argument("--reps", type=int, default=4)
 ap.add_argument("--dtype", choices=["i32", "i64"], default="i32")
 ap.add_argument("--dist", choices=["uniform", "zipf", "sorted", "reverse", "equal", "few", "byte"],
                 default="uniform")
+ap.add_argument("--opt", action="append", default=[], help="dsort option name=value (repeatable)")
 a = ap.parse_args()
 tag = os.environ.get("DSORT_LIB")
 tag = os.path.basename(os.path.dirname(tag)) if tag else "default"
 tag = f"{tag} {a.dtype} {a.dist}"
 ctx = dsort.Context(0)
+for kv in a.opt:
+    k, v = kv.split("=")
+    ctx.set_option(k, int(eval(v, {}, {})))
+    tag += f" {k}={v}"
 t = torch.empty(a.keys, dtype=torch.int32 if a.dtype == "i32" else torch.int64, device="cuda")
 if a.dist == "zipf":
     ctx.gen_zipf_i64(t, 0x5EED2026)
