@@ -367,6 +367,10 @@ def cpu_baseline(sample_keys, target_keys):
     }
 
 
+# the tile sort kernel of the default (gathering) path, as rocprofv3 names it
+TILE_SORT_KERNEL = {4: "bin_sort_kernel<int, true>", 8: "bin_sort_kernel<long, true>"}
+
+
 def pmc_traffic(kernel, n, w):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC passes
     (FETCH_SIZE x2 + WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md), scaled to this run's
@@ -376,6 +380,8 @@ def pmc_traffic(kernel, n, w):
         try:
             with open(path) as f:
                 doc = json.load(f)
+            if w != doc.get("key_bytes", 4) and "int64" in doc:
+                doc = doc["int64"]
             rec = doc["kernels"][kernel]
         except (OSError, KeyError, ValueError):
             continue
@@ -556,9 +562,10 @@ def report_single(args, elapsed, k):
                                     f"(BASELINE metric size); tile {k['tile']} keys, {k['passes']} merge passes",
                         "keys": n, "parallelism": "1 GPU"}
     result["roofline"] = {
-        "bound": "hbm", "kernel": "block_sort_w_kernel (tile sort, one launch over all tiles)",
+        "bound": "hbm", "kernel": "bin_sort_kernel (tile sort, one launch over all tiles; bitonic "
+                                  "block_sort_w_kernel for the tiles it declines)",
         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("block_sort_w_kernel", n, k["w"]),
+        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(TILE_SORT_KERNEL[k["w"]], n, k["w"]),
         "avg_launch_ms": round(tile_ms, 4), "algorithmic_bytes_per_launch": bytes_tile,
         "partition_ms": round(k["partition_ms"] / args.steps, 3),
         "merge_passes": npass // max(args.steps, 1),
@@ -583,10 +590,10 @@ def report_multi(args, world, elapsed, per_rank, w):
     n_gpu = float(per_rank[slow, 5])
     bpl = 2 * w * n_gpu  # the local tile sort reads and writes the rank's chunk once
     ach = bpl / (tile_ms * 1e-3) / 1e9 if tile_ms > 0 else None
-    roof = {"bound": "hbm", "kernel": "block_sort_w_kernel (local tile sort, slowest rank)",
+    roof = {"bound": "hbm", "kernel": "bin_sort_kernel (local tile sort, slowest rank)",
             "achieved": round(ach, 1) if ach else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None,
-            "traffic": pmc_traffic("block_sort_w_kernel", int(n_gpu), w), "avg_launch_ms": round(tile_ms, 4),
+            "traffic": pmc_traffic(TILE_SORT_KERNEL[w], int(n_gpu), w), "avg_launch_ms": round(tile_ms, 4),
             "algorithmic_bytes_per_launch": int(bpl),
             "whole_sort_single_pass_bound_frac": round(
                 2 * w * n / (step_ms * 1e-3) / 1e9 / (HBM_PEAK_GBS * world), 4)}
