@@ -511,17 +511,12 @@ template <> struct V16<int64_t> {
 // ------------------------------------------------------------------------------------------
 // Bin sort of a tile.  After the two partition levels a tile covers a narrow key range that its
 // keys fill about evenly (they are a contiguous run of sampled sub-buckets), so binning them by
-// (key - min) over the tile's range into TILE/4 bins leaves about 4 keys per bin: a counting pass into
-// LDS (counts, then cursors) groups the keys by bin; three passes of 16-key sorting networks,
-// one window per thread in registers, at offsets 0, 8, 0, then sort every bin of at most 16 keys
-// (sorting a window of bin-grouped keys keeps them grouped, and inside one bin the passes are an
-// odd-even transposition sort of 8-key blocks).  About 60 operations per key instead of the ~180
-// of the bitonic tile sort.  Keys equal to key_max
-// (and the tile's padding, which is key_max) are not binned: the output ends with valid - M of
-// them, M = the binned keys.  A bin of more than 16 keys is only sorted by the window passes when
-// it holds one key value (a duplicate run, the usual case of a big bin); the result is checked at
-// the window boundaries, and on a descent the function returns false and the caller runs the
-// bitonic sort (x is left untouched).
+// (key - min) over the tile's range into TILE/2 bins leaves about 2 keys per bin: a counting pass
+// into LDS (counts, then cursors) groups the keys by bin, and 16-key window networks (one window
+// per thread, in registers) sort inside the bins: a sort at offset 0 and a merge of the sorted
+// halves at offset 8, a second merge at offset 0 only when a bin of more than 9 keys left a
+// descent.  About 45 compare-exchange operations per key instead of the ~180 of the bitonic tile
+// sort.  Details and the fallback: bin_sort_tile.
 #ifndef DSORT_BIN_SORT
 #define DSORT_BIN_SORT 1
 #endif
@@ -546,12 +541,31 @@ __device__ __forceinline__ T wave_max(T v) {
     return v;
 }
 
+// Bins per tile: two keys per bin on average.  The counters (16-bit, two per word) and the tile
+// fill exactly 80 KiB of LDS for int32 (64 + 16), so two workgroups share a CU.
+template <typename T> constexpr int BIN_NB = TILE_OF<T> / 2;
+
+// Per-wave scratch of the bin sort; it lives at the start of the tile array s, which is free
+// until the keys are placed (step 4).
 template <typename T>
-struct BinLds {
-    uint32_t hw[TILE_OF<T> / 8];  // 16-bit bin counters, then bin starts (two per word)
+struct BinSm {
     T mn[WG<T>::WAVES], mx[WG<T>::WAVES];
-    uint64_t wsum[WG<T>::WAVES];
+    uint32_t wsum[WG<T>::WAVES];
+    uint32_t flag[WG<T>::WAVES];
 };
+
+// __syncthreads_or with the caller's scratch (one word per wave): HIP's own reserves 256 bytes of
+// LDS of its own, which would leave the int32 bin sort 256 bytes short of two workgroups per CU.
+template <int WAVES>
+__device__ __forceinline__ bool block_or(bool p, uint32_t *flag) {
+    const bool any = __ballot(p) != 0;
+    if ((threadIdx.x & 63) == 0) flag[threadIdx.x >> 6] = any;
+    __syncthreads();
+    uint32_t r = 0;
+#pragma unroll
+    for (int i = 0; i < WAVES; ++i) r |= flag[i];
+    return r != 0;
+}
 
 // Bin of key offset `off` (key - min): the top 32 bits of the offset times a 32-bit reciprocal
 // of the range, so all NB bins are used (monotone in the key, < NB).
@@ -559,7 +573,7 @@ template <typename T>
 struct BinMap {
     using U = typename sb::KeyU<T>::U;
     uint32_t pre;    // offsets are shifted right by pre first (int64 ranges above 2^32)
-    uint32_t scale;  // floor(NB * 2^32 / ((range >> pre) + 1)), capped
+    uint32_t scale;  // <= NB * 2^32 / ((range >> pre) + 1), capped at 2^32 - 1
     __device__ __forceinline__ uint32_t operator()(U off) const {
         return __umulhi((uint32_t)(off >> pre), scale);
     }
@@ -609,37 +623,93 @@ __device__ __forceinline__ void bin_put(T xv, T mn, const BinMap<T> &bm, uint32_
     }
 }
 
+// Batcher's odd-even merge of two sorted halves of K keys (the last stage of sort_net<K>).
+template <int K, typename T>
+__device__ __forceinline__ void merge_halves(T (&v)[K]) {
+    constexpr int P = K / 2;
+#pragma unroll
+    for (int k = P; k >= 1; k >>= 1) {
+#pragma unroll
+        for (int j = k % P; j + k < K; j += 2 * k) {
+#pragma unroll
+            for (int i = 0; i < k; ++i)
+                if (i + j + k < K) cex(v[i + j], v[i + j + k]);
+        }
+    }
+}
+
+// One window pass over s[0, M) (M <= TILE): thread t sorts (MERGE: merges the sorted halves of)
+// the 16 keys at 16 t + OFF.  Windows of one pass are disjoint, so each is read and written in
+// place.  A window is always moved as 16-byte vectors: slots past M read as key_max, sort to the
+// window's end and are written back past M, where nothing reads them.  (Guarding the vector path
+// with `ws + 16 <= M` let the compiler fold it into the scalar path: 16 ds_read2_b32 per window
+// at a 64-byte lane stride, 16-way bank conflicts.)  The last window at offset 8 would reach past
+// the tile; its second half is empty, so the merge is a no-op and it is skipped.
+template <int OFF, bool MERGE, typename T>
+__device__ __forceinline__ void window_pass(T *s, int M, int tid) {
+    using V = typename V16<T>::type;
+    constexpr int N = KPC<T>;
+    const int ws = 16 * tid + OFF;
+    if (ws >= M || ws + 16 > TILE_OF<T>) return;
+    T v[16];
+    V *p = reinterpret_cast<V *>(s + ws);  // 16-byte aligned: OFF * sizeof(T) is
+#pragma unroll
+    for (int q = 0; q < 16 / N; ++q) V16<T>::get(p[q], v + N * q);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = ws + k < M ? v[k] : key_max<T>();
+    if constexpr (MERGE) merge_halves<16>(v);
+    else sort_net<16>(v);
+#pragma unroll
+    for (int q = 0; q < 16 / N; ++q) p[q] = V16<T>::make(v + N * q);
+}
+
+// Bin sort of one tile held in x (slots past `valid` are key_max) into out[0, valid).
+//   1. range [mn, mx] of the keys below key_max (they and the padding are not binned: the output
+//      ends with valid - M of them, M = the binned keys);
+//   2. NB = TILE / 2 bins over the range, counted by LDS atomics on 16-bit counters (a duplicate
+//      run -- HOT -- with aggregated atomics);
+//   3. bin starts: thread t scans its own NB / THREADS consecutive bins (one 16-byte word), then
+//      the threads' totals;
+//   4. keys to their bins (the starts are cursors now);
+//   5. 16-key windows: sorted at 16 t, their halves merged at 16 t + 8.  That sorts every bin of
+//      at most 9 keys (a bin crossing 16 t + 8 lies inside [16 t, 16 t + 16)); a descent left at
+//      a boundary 16 t + 8 means a bigger bin: one more merge at 16 t sorts bins of <= 16 keys
+//      (the three passes are an odd-even transposition of 8-key blocks).  A tile still unsorted
+//      returns false (out untouched) and the caller runs the bitonic sort.
+// About 30 operations per key on the window networks, against ~180 for the bitonic tile sort.
+// cw holds the counters (NB / 2 words); the caller has passed a barrier since its last use.
 template <typename T>
-__device__ __forceinline__ bool bin_sort_tile(const T (&x)[R], int valid, T *s, BinLds<T> &L, T *out,
+__device__ __forceinline__ bool bin_sort_tile(const T (&x)[R], int valid, T *s, uint32_t *cw, T *out,
                                               bool hot_hint) {
     using U = typename sb::KeyU<T>::U;
-    constexpr int TILE = TILE_OF<T>, WAVES = WG<T>::WAVES, THREADS = 64 * WAVES, NB = TILE / 4;
+    constexpr int WAVES = WG<T>::WAVES, THREADS = 64 * WAVES, NB = BIN_NB<T>;
     constexpr int BPT = NB / THREADS;
-    static_assert(BPT == 4, "four bins per thread");
+    static_assert(BPT == 8, "one 16-byte word of counters per thread");
+    BinSm<T> &sm = *reinterpret_cast<BinSm<T> *>(s);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    // 1. range of the keys below key_max
+    // 1. range
     T mn = key_max<T>(), mx = key_min<T>();
 #pragma unroll
     for (int i = 0; i < R; ++i) {
-        if (x[i] != key_max<T>()) {
-            mn = x[i] < mn ? x[i] : mn;
-            mx = x[i] > mx ? x[i] : mx;
-        }
+        mn = x[i] < mn ? x[i] : mn;
+        const T xm = x[i] == key_max<T>() ? key_min<T>() : x[i];
+        mx = xm > mx ? xm : mx;
     }
     mn = wave_min(mn);
     mx = wave_max(mx);
     if (lane == 0) {
-        L.mn[w] = mn;
-        L.mx[w] = mx;
+        sm.mn[w] = mn;
+        sm.mx[w] = mx;
     }
-    for (int q = tid; q < NB / 2; q += THREADS) L.hw[q] = 0;
-    __syncthreads();
+    __syncthreads();  // (also: every lane's gather is done with the piece table in cw)
+    uint4 *c4 = reinterpret_cast<uint4 *>(cw) + tid;  // this thread's bins [8 tid, 8 tid + 8)
+    *c4 = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
     for (int i = 0; i < WAVES; ++i) {
-        mn = L.mn[i] < mn ? L.mn[i] : mn;
-        mx = L.mx[i] > mx ? L.mx[i] : mx;
+        mn = sm.mn[i] < mn ? sm.mn[i] : mn;
+        mx = sm.mx[i] > mx ? sm.mx[i] : mx;
     }
-    if (mx < mn) {  // every key is key_max
+    if (mx < mn || (mn == key_max<T>())) {  // every key is key_max
         for (int i = tid; i < valid; i += THREADS) out[i] = key_max<T>();
         return true;
     }
@@ -647,105 +717,77 @@ __device__ __forceinline__ bool bin_sort_tile(const T (&x)[R], int valid, T *s, 
     BinMap<T> bm;
     bm.pre = 0;
     while ((range >> bm.pre) > (U)0xFFFFFFFFu) ++bm.pre;
-    const uint64_t den = (uint64_t)(uint32_t)(range >> bm.pre) + 1;
-    const uint64_t sc = ((uint64_t)NB << 32) / den;
-    bm.scale = sc > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)sc;
-    // a hot tile (some wave's first keys share a bin: a duplicate run) counts with aggregated
-    // atomics
+    {
+        // NB * 2^32 / (range' + 1) through a float reciprocal, shaded down by 2^-20 (more than its
+        // error) so that the largest offset still maps below NB
+        const float den = (float)(uint32_t)(range >> bm.pre) + 1.0f;
+        const float f = (float)NB * 4294967296.0f * (1.0f - 0x1p-20f) * __builtin_amdgcn_rcpf(den);
+        bm.scale = f >= 4294967040.0f ? 0xFFFFFFFFu : (uint32_t)f;
+    }
     const bool act0 = x[0] != key_max<T>();
     const uint32_t bx = bm((U)x[0] - (U)mn);
     const uint32_t bf = (uint32_t)__builtin_amdgcn_readfirstlane((int)bx);
-    const bool hot = __syncthreads_or(hot_hint || (lane == 0 && __popcll(__ballot(act0 && bx == bf)) >= 8));
-    // 2. counting (16-bit counters, two bins per word)
+    const bool hot = block_or<WAVES>(hot_hint || (lane == 0 && __popcll(__ballot(act0 && bx == bf)) >= 8), sm.flag);
+    // 2. counting
     if (hot) {
 #pragma unroll
-        for (int i = 0; i < R; ++i) bin_put<true, false>(x[i], mn, bm, L.hw, s, lane);
+        for (int i = 0; i < R; ++i) bin_put<true, false>(x[i], mn, bm, cw, s, lane);
     } else {
 #pragma unroll
-        for (int i = 0; i < R; ++i) bin_put<false, false>(x[i], mn, bm, L.hw, s, lane);
+        for (int i = 0; i < R; ++i) bin_put<false, false>(x[i], mn, bm, cw, s, lane);
     }
     __syncthreads();
-    // 3. my bins are tid + k * THREADS; bins in order = k-major, so one scan of the four 16-bit
-    // counts packed in a 64-bit word gives every bin's start
-    uint32_t cnt[BPT];
+    // 3. starts
+    uint4 cv = *c4;
+    uint32_t wd[4] = {cv.x, cv.y, cv.z, cv.w};
+    uint32_t tot = 0;
 #pragma unroll
-    for (int k = 0; k < BPT; ++k) {
-        const uint32_t b = (uint32_t)(tid + k * THREADS), wd = L.hw[b >> 1];
-        cnt[k] = (b & 1) ? wd >> 16 : wd & 0xFFFFu;
-    }
-    const uint64_t pv = (uint64_t)cnt[0] | (uint64_t)cnt[1] << 16 | (uint64_t)cnt[2] << 32 | (uint64_t)cnt[3] << 48;
-    uint64_t incl = pv;
+    for (int k = 0; k < 4; ++k) tot += (wd[k] & 0xFFFFu) + (wd[k] >> 16);
+    uint32_t incl = tot;
+#pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        const uint64_t y = __shfl_up(incl, o);
+        const uint32_t y = __shfl_up(incl, o);
         if (lane >= o) incl += y;
     }
-    if (lane == 63) L.wsum[w] = incl;
+    if (lane == 63) sm.wsum[w] = incl;
     __syncthreads();
-    uint64_t ex = incl - pv, tot = 0;
+    uint32_t run = incl - tot, M = 0;
 #pragma unroll
     for (int i = 0; i < WAVES; ++i) {
-        ex += i < w ? L.wsum[i] : 0;
-        tot += L.wsum[i];
+        const uint32_t v = sm.wsum[i];
+        run += i < w ? v : 0;
+        M += v;
     }
-    uint32_t st[BPT];
-    uint32_t before = 0;  // keys in the bins of lower k
 #pragma unroll
-    for (int k = 0; k < BPT; ++k) {
-        st[k] = before + (uint32_t)((ex >> (16 * k)) & 0xFFFFu);
-        before += (uint32_t)((tot >> (16 * k)) & 0xFFFFu);
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t c0 = wd[k] & 0xFFFFu, c1 = wd[k] >> 16;
+        wd[k] = run | (run + c0) << 16;
+        run += c0 + c1;
     }
-    const uint32_t M = before;  // binned keys
-    __syncthreads();            // every count read before the starts overwrite them
-#pragma unroll
-    for (int k = 0; k < BPT; ++k) {  // bin b (even) and b + 1 sit in adjacent lanes: one word
-        const uint32_t nb = __shfl_down(st[k], 1);
-        if (!(tid & 1)) L.hw[(tid + k * THREADS) >> 1] = st[k] | nb << 16;
-    }
-    __syncthreads();
-    // 4. keys to their bins: the starts are cursors now
+    *c4 = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+    __syncthreads();  // (also: sm, in s, is dead from here)
+    // 4. keys to their places
     if (hot) {
 #pragma unroll
-        for (int i = 0; i < R; ++i) bin_put<true, true>(x[i], mn, bm, L.hw, s, lane);
+        for (int i = 0; i < R; ++i) bin_put<true, true>(x[i], mn, bm, cw, s, lane);
     } else {
 #pragma unroll
-        for (int i = 0; i < R; ++i) bin_put<false, true>(x[i], mn, bm, L.hw, s, lane);
+        for (int i = 0; i < R; ++i) bin_put<false, true>(x[i], mn, bm, cw, s, lane);
     }
     __syncthreads();
-    // 5. three passes of 16-key windows, one per thread (offsets 0, 8, 0): within a bin of at most
-    // 16 keys (at most three 8-key blocks) this is an odd-even transposition of blocks, so every
-    // bin ends sorted.  Slots past the binned keys read as key_max and are not written back.
-#pragma unroll 1
-    for (int p = 0; p < 3; ++p) {
-        const int ws = 16 * tid + (p == 1 ? 8 : 0);
-        T v[16];
-        if (ws + 16 <= (int)M && !(ws & (KPC<T> - 1))) {
-            using V = typename V16<T>::type;
-            const V *src = reinterpret_cast<const V *>(s + ws);
-#pragma unroll
-            for (int q = 0; q < 16 / KPC<T>; ++q) V16<T>::get(src[q], v + KPC<T> * q);
-        } else {
-#pragma unroll
-            for (int k = 0; k < 16; ++k) v[k] = ws + k < (int)M ? s[ws + k] : key_max<T>();
-        }
-        sort_net<16>(v);
-        __syncthreads();  // every window read before any is written (offset windows overlap)
-        if (ws + 16 <= (int)M && !(ws & (KPC<T> - 1))) {
-            using V = typename V16<T>::type;
-            V *dst = reinterpret_cast<V *>(s + ws);
-#pragma unroll
-            for (int q = 0; q < 16 / KPC<T>; ++q) dst[q] = V16<T>::make(v + KPC<T> * q);
-        } else {
-#pragma unroll
-            for (int k = 0; k < 16; ++k)
-                if (ws + k < (int)M) s[ws + k] = v[k];
-        }
+    // 5. window passes; a descent can only be left at a boundary of the last pass's windows
+    window_pass<0, false>(s, (int)M, tid);
+    __syncthreads();
+    window_pass<8, true>(s, (int)M, tid);
+    __syncthreads();
+    const int e8 = 16 * tid + 8;
+    if (block_or<WAVES>(e8 < (int)M && s[e8 - 1] > s[e8], cw)) {  // (cw is dead from step 5)
+        window_pass<0, true>(s, (int)M, tid);
         __syncthreads();
+        const int e16 = 16 * tid + 16;
+        if (block_or<WAVES>(e16 < (int)M && s[e16 - 1] > s[e16], cw + WAVES)) return false;
     }
-    // 6. every window is sorted now; a bin of more than 16 keys holding more than one key value
-    // (rare: not a duplicate run) may still leave a descent at a window boundary
-    const bool bad = 16 * tid + 16 < (int)M && s[16 * tid + 15] > s[16 * tid + 16];
-    if (__syncthreads_or(bad)) return false;
-    // 7. out: the binned keys in order, then key_max
+    // 6. out: the binned keys in order, then key_max
     for (int i = tid; i < valid; i += THREADS) out[i] = (uint32_t)i < M ? s[i] : key_max<T>();
     return true;
 }
@@ -763,17 +805,16 @@ template <typename T> constexpr int kMaxPieces = WK * (int)sizeof(T) / 8 - 2;
 // loads tile slots w * 1024 + 64 i + t straight into x[i] (the order before the sort does not
 // matter), walking the pieces upwards as i grows: consecutive lanes read consecutive keys of a
 // piece, and all R loads of a lane are in flight together.
+// poff: 2 kMaxPieces + 1 words of LDS for the piece table; wsum: one word per wave.
 template <typename T>
-__device__ __forceinline__ void gather_tile(const sb::Gather &ga, const sb::GTile &gt, const T *in, T *s,
-                                            T (&x)[R]) {
-    constexpr int TILE = TILE_OF<T>, WAVES = WG<T>::WAVES, THREADS = 64 * WAVES;
+__device__ __forceinline__ void gather_tile(const sb::Gather &ga, const sb::GTile &gt, const T *in, uint32_t *poff,
+                                            uint32_t *wsum, T (&x)[R], const int tid = threadIdx.x) {
+    constexpr int WAVES = WG<T>::WAVES, THREADS = 64 * WAVES;
     static_assert(2 * THREADS >= kMaxPieces<T> + 1, "two pieces per thread");
-    uint32_t *poff = reinterpret_cast<uint32_t *>(s + TILE);  // kMaxPieces + 1 offsets
-    uint32_t *psrc = poff + kMaxPieces<T> + 1;                 // kMaxPieces sources
-    uint32_t *wsum = reinterpret_cast<uint32_t *>(s);          // per-wave sums
+    uint32_t *psrc = poff + kMaxPieces<T> + 1;  // kMaxPieces sources after kMaxPieces + 1 offsets
     const sb::BInfo b = ga.bi[gt.b];
     const int np = (int)(b.c1 - b.c0);
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int lane = tid & 63, w = tid >> 6;
     uint32_t len[2], src[2];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -839,18 +880,18 @@ __device__ __forceinline__ void gather_tile(const sb::Gather &ga, const sb::GTil
 // past the tile count (the grid is an upper bound).
 template <typename T, bool GATHER>
 __device__ __forceinline__ bool load_tile(const T *in, uint64_t n, const uint4 *tiles, const uint32_t *ntiles,
-                                          const sb::Gather &ga, uint32_t j, T *s, T (&x)[R], uint64_t &base,
-                                          int &valid) {
+                                          const sb::Gather &ga, uint32_t j, uint32_t *poff, uint32_t *wsum,
+                                          T (&x)[R], uint64_t &base, int &valid, const int tid = threadIdx.x) {
     constexpr int TILE = TILE_OF<T>, N = KPC<T>;
     using V = typename V16<T>::type;
-    const int t = lane_id();
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
+    const int t = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform
     if constexpr (GATHER) {
         if (j >= *ntiles) return false;
         const sb::GTile gt = ga.tiles[j];
         base = gt.base;
         valid = (int)gt.valid;
-        gather_tile<T>(ga, gt, in, s, x);  // (the piece table sits in the slack, not in the runs)
+        gather_tile<T>(ga, gt, in, poff, wsum, x, tid);
         return true;
     } else if (tiles) {
         if (j >= *ntiles) return false;
@@ -905,12 +946,15 @@ __global__ void __launch_bounds__(64 * WG<T>::WAVES, DSORT_BIN_OCC) bin_sort_ker
                                                                      const uint4 *tiles, const uint32_t *ntiles,
                                                                      sb::Gather ga, uint32_t *fb, uint32_t *nfb) {
     constexpr int TILE = TILE_OF<T>;
-    __shared__ __attribute__((aligned(16))) T s[TILE + WK];
-    __shared__ BinLds<T> bl;
+    static_assert(BIN_NB<T> / 2 >= 2 * kMaxPieces<T> + 1, "the piece table fits in the counters");
+    __shared__ __attribute__((aligned(16))) T s[TILE];
+    __shared__ __attribute__((aligned(16))) uint32_t cw[BIN_NB<T> / 2];
     T x[R];
     uint64_t base;
     int valid;
-    if (!load_tile<T, GATHER>(in, n, tiles, ntiles, ga, blockIdx.x, s, x, base, valid)) return;
+    if (!load_tile<T, GATHER>(in, n, tiles, ntiles, ga, blockIdx.x, cw, reinterpret_cast<uint32_t *>(s), x, base,
+                              valid))
+        return;
     if (valid == 0) return;
     // a duplicate run inside a gathered tile shows as two equal neighbouring splitters
     bool hint = false;
@@ -923,7 +967,7 @@ __global__ void __launch_bounds__(64 * WG<T>::WAVES, DSORT_BIN_OCC) bin_sort_ker
         if (j < jh && j + 1 < nspl) hint = sp[j].k == sp[j + 1].k;
         hint = __ballot(hint) != 0;
     }
-    if (!bin_sort_tile<T>(x, valid, s, bl, out + base, hint) && threadIdx.x == 0) fb[atomicAdd(nfb, 1u)] = blockIdx.x;
+    if (!bin_sort_tile<T>(x, valid, s, cw, out + base, hint) && threadIdx.x == 0) fb[atomicAdd(nfb, 1u)] = blockIdx.x;
 }
 
 // The bitonic tile sort: tile fb[blockIdx.x] (fb = the bin sort's declined tiles) or tile
@@ -944,7 +988,10 @@ __global__ void __launch_bounds__(64 * WG<T>::WAVES, WG<T>::OCC) block_sort_w_ke
     uint64_t base;
     int valid;
     const uint32_t j = fb ? fb[blockIdx.x] : blockIdx.x;
-    if (!load_tile<T, GATHER>(in, n, tiles, ntiles, ga, j, s, x, base, valid)) return;
+    // (the piece table of a gathered tile sits in the slack, not in the runs)
+    if (!load_tile<T, GATHER>(in, n, tiles, ntiles, ga, j, reinterpret_cast<uint32_t *>(s + TILE),
+                              reinterpret_cast<uint32_t *>(s), x, base, valid))
+        return;
     sort_wave(x, c);
     // lane-major run of the wave -> LDS; odd waves' runs (the B runs of the first level) are
     // stored descending
