@@ -132,9 +132,10 @@ def launch_ranks(n, argv, check_devices=True, timeout_s=1800):
 
 def launcher_selftest():
     """--launcher-selftest: one line per rank with the plumbing it received (CPU test)."""
-    print(json.dumps({"rank": int(os.environ["RANK"]), "world": int(os.environ["WORLD_SIZE"]),
-                      "local_rank": int(os.environ["LOCAL_RANK"]), "master": os.environ["MASTER_ADDR"],
-                      "port": int(os.environ["MASTER_PORT"])}), flush=True)
+    line = json.dumps({"rank": int(os.environ["RANK"]), "world": int(os.environ["WORLD_SIZE"]),
+                       "local_rank": int(os.environ["LOCAL_RANK"]), "master": os.environ["MASTER_ADDR"],
+                       "port": int(os.environ["MASTER_PORT"])}) + "\n"
+    os.write(1, line.encode())  # one write per line: the ranks share the parent's stdout
 
 
 # ------------------------------------------------------------------------- CPU baseline

@@ -111,15 +111,12 @@ __device__ __forceinline__ bool below(const Spl<T> &s, T key, uint32_t pos) {
 // sub-bucket of (key, pos): the number of splitters below it.  Splitters outside the key's
 // slot are below it iff their slot is lower (slot_of is monotone), so only the slot's own
 // splitters are searched -- usually none or one.
+// The part after the reads: r = the key's slot entry, a and b = the slot's first two splitters.
 template <typename T>
-__device__ __forceinline__ int sub_of(const Spl<T> *spl, const uint32_t *rng, T klo, uint32_t sh, T key,
-                                      uint32_t pos) {
-    const uint32_t r = rng[slot_of<T>(key, klo, sh)];
+__device__ __forceinline__ int sub_pick(const Spl<T> *spl, uint32_t r, const Spl<T> &a, const Spl<T> &b, T key,
+                                        uint32_t pos) {
     int lo = (int)(r & 0xFFFF);
     const int hi = (int)(r >> 16);
-    // the first two splitters of the slot without a branch (the table holds SB_MAXS entries, so
-    // the reads stay inside it), then the rare crowded slot
-    const Spl<T> a = spl[lo], b = spl[lo + 1];
     const int j = lo + (lo < hi && below<T>(a, key, pos) ? 1 + (lo + 1 < hi && below<T>(b, key, pos)) : 0);
     if (j < lo + 2 || j >= hi) return j;
     lo = j;
@@ -130,6 +127,15 @@ __device__ __forceinline__ int sub_of(const Spl<T> *spl, const uint32_t *rng, T 
         else h = mid;
     }
     return lo;
+}
+template <typename T>
+__device__ __forceinline__ int sub_of(const Spl<T> *spl, const uint32_t *rng, T klo, uint32_t sh, T key,
+                                      uint32_t pos) {
+    // the first two splitters of the slot without a branch (the table holds SB_MAXS + 1 entries,
+    // so the reads stay inside it), then the rare crowded slot
+    const uint32_t r = rng[slot_of<T>(key, klo, sh)];
+    const int lo = (int)(r & 0xFFFF);
+    return sub_pick<T>(spl, r, spl[lo], spl[lo + 1], key, pos);
 }
 
 // Sample g (global index, bucket b's samples at [soff, soff + ns)) = the key at position
@@ -452,6 +458,7 @@ __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restric
 constexpr int SB_LT = DSORT_SB_LT;
 // keys per thread: the chunk (int32 62 KiB, int64 52 KiB) + tables fit two workgroups per CU
 template <typename T> constexpr int SB_LKPT = sizeof(T) == 4 ? 31 : 13;
+
 template <typename T> constexpr int SB_LCH = SB_LT * SB_LKPT<T>;
 
 template <typename T>
@@ -493,13 +500,42 @@ __global__ void __launch_bounds__(SB_LT, 4) sb_local_kernel(T *__restrict__ buf,
     const SlotFn<T> f = sfn[c.b];
     __syncthreads();
     uint32_t pk[KPT];  // sub-bucket | rank << 10
+    // In groups of G keys: the slot-table reads, then the splitter reads, then the atomics, so a
+    // key's LDS round trips do not wait for the previous key's.  A key past the chunk adds 0.
+    // (int32: 31 keys and their ranks are already live; batching spills and measured slower)
+    constexpr int G = sizeof(T) == 4 ? 1 : 8;
+    if constexpr (G == 1) {
 #pragma unroll
-    for (int k = 0; k < KPT; ++k) {
-        const uint32_t i = tid + k * SB_LT;
-        if (i < c.len) {
-            const int j = sub_of<T>(spl, rng, f.klo, f.sh, key[k], (uint32_t)(c.start + i));
-            pk[k] = (uint32_t)j | atomicAdd(&hist[j], 1u) << 10;
+        for (int k = 0; k < KPT; ++k) {
+            const uint32_t i = tid + k * SB_LT;
+            if (i < c.len) {
+                const int j = sub_of<T>(spl, rng, f.klo, f.sh, key[k], (uint32_t)(c.start + i));
+                pk[k] = (uint32_t)j | atomicAdd(&hist[j], 1u) << 10;
+            }
         }
+    } else {
+#pragma unroll
+    for (int g0 = 0; g0 < KPT; g0 += G) {
+        uint32_t r[G];
+        Spl<T> sa[G], sb[G];
+#pragma unroll
+        for (int u = 0; u < G; ++u)
+            if (g0 + u < KPT) r[u] = rng[slot_of<T>(key[g0 + u], f.klo, f.sh)];
+#pragma unroll
+        for (int u = 0; u < G; ++u)
+            if (g0 + u < KPT) {
+                sa[u] = spl[r[u] & 0xFFFF];
+                sb[u] = spl[(r[u] & 0xFFFF) + 1];
+            }
+#pragma unroll
+        for (int u = 0; u < G; ++u)
+            if (g0 + u < KPT) {
+                const uint32_t i = tid + (g0 + u) * SB_LT;
+                const int j = sub_pick<T>(spl, r[u], sa[u], sb[u], key[g0 + u], (uint32_t)(c.start + i));
+                // (a key past the chunk adds 0 to a lane-spread counter, not all to one)
+                pk[g0 + u] = (uint32_t)j | atomicAdd(&hist[i < c.len ? j : lane], i < c.len ? 1u : 0u) << 10;
+            }
+    }
     }
     __syncthreads();
     uint32_t h[PER], sum = 0;

@@ -582,13 +582,17 @@ struct BinMap {
 // The keys of one register slot into the bins.  HOT: the lanes whose bin is the first active
 // lane's add with one atomic (a duplicate run puts a whole wave into one bin).  SCATTER: the
 // atomic returns the bin's cursor and the key goes to s there; else it only counts.
-template <bool HOT, bool SCATTER, typename T>
-__device__ __forceinline__ void bin_put(T xv, T mn, const BinMap<T> &bm, uint32_t *hw, T *s, int lane) {
+// Counting (SCATTER = false) or placing (the atomic returns the bin's cursor and the key goes to
+// s there) of one key.  hot (a duplicate run): the lanes whose bin is the first active lane's add
+// with one aggregated atomic.  (The batched int64 plain path is bin_count / bin_place.)
+template <bool SCATTER, typename T>
+__device__ __forceinline__ void bin_put(T xv, T mn, const BinMap<T> &bm, uint32_t *hw, T *s, int lane,
+                                            bool hot) {
     using U = typename sb::KeyU<T>::U;
     const bool act = xv != key_max<T>();
     const uint32_t b = bm((U)xv - (U)mn);
     const uint32_t inc = (b & 1) ? 0x10000u : 1u;
-    if constexpr (!HOT) {
+    if (!hot) {  // (the plain path one key at a time: int32)
         if (act) {
             if constexpr (SCATTER) {
                 const uint32_t old = atomicAdd(&hw[b >> 1], inc);
@@ -597,28 +601,74 @@ __device__ __forceinline__ void bin_put(T xv, T mn, const BinMap<T> &bm, uint32_
                 atomicAdd(&hw[b >> 1], inc);
             }
         }
+        return;
+    }
+    const uint64_t am = __ballot(act);
+    if (!am) return;
+    const int first = (int)__ffsll((long long)am) - 1;
+    const uint32_t b0 = (uint32_t)__shfl((int)b, first);
+    const uint64_t same = __ballot(act && b == b0);
+    const uint32_t inc0 = ((b0 & 1) ? 0x10000u : 1u) * (uint32_t)__popcll(same);
+    if constexpr (SCATTER) {
+        uint32_t pos = 0;
+        if (act && b != b0) {
+            const uint32_t old = atomicAdd(&hw[b >> 1], inc);
+            pos = (b & 1) ? old >> 16 : old & 0xFFFFu;
+        }
+        uint32_t old0 = 0;
+        if (lane == first) old0 = atomicAdd(&hw[b0 >> 1], inc0);
+        old0 = (uint32_t)__shfl((int)old0, first);
+        if (act && b == b0)
+            pos = ((b0 & 1) ? old0 >> 16 : old0 & 0xFFFFu) + (uint32_t)__popcll(same & ((1ull << lane) - 1));
+        if (act) s[pos] = xv;
     } else {
-        const uint64_t am = __ballot(act);
-        if (!am) return;
-        const int first = (int)__ffsll((long long)am) - 1;
-        const uint32_t b0 = (uint32_t)__shfl((int)b, first);
-        const uint64_t same = __ballot(act && b == b0);
-        const uint32_t inc0 = ((b0 & 1) ? 0x10000u : 1u) * (uint32_t)__popcll(same);
-        if constexpr (SCATTER) {
-            uint32_t pos = 0;
-            if (act && b != b0) {
-                const uint32_t old = atomicAdd(&hw[b >> 1], inc);
-                pos = (b & 1) ? old >> 16 : old & 0xFFFFu;
-            }
-            uint32_t old0 = 0;
-            if (lane == first) old0 = atomicAdd(&hw[b0 >> 1], inc0);
-            old0 = (uint32_t)__shfl((int)old0, first);
-            if (act && b == b0)
-                pos = ((b0 & 1) ? old0 >> 16 : old0 & 0xFFFFu) + (uint32_t)__popcll(same & ((1ull << lane) - 1));
-            if (act) s[pos] = xv;
-        } else {
-            if (act && b != b0) atomicAdd(&hw[b >> 1], inc);
-            if (lane == first) atomicAdd(&hw[b0 >> 1], inc0);
+        if (act && b != b0) atomicAdd(&hw[b >> 1], inc);
+        if (lane == first) atomicAdd(&hw[b0 >> 1], inc0);
+    }
+}
+
+// Batched plain path (int64): bin, counter word and half of every key, with no branch in the
+// atomics -- a key that is not binned (key_max, the padding) adds 0 to the lane's own counter
+// word (spread: a whole padding wave on one word would serialise) and is not stored -- and all
+// of a thread's atomics issued (in batches of 8) before any result is used.  That pays at the
+// int64 tile's 4 waves per SIMD (bin sort 8.46 -> 8.18 ms at 2^30 Zipf); at int32's 8 waves per
+// SIMD the other waves already hide the latency and one key at a time is faster (3.26 vs 3.61 ms).
+template <typename T> constexpr bool BIN_BATCH = sizeof(T) == 8;
+template <typename T>
+struct BinAt {
+    uint32_t word, sh, inc;
+    __device__ __forceinline__ BinAt(T xv, T mn, const BinMap<T> &bm) {
+        using U = typename sb::KeyU<T>::U;
+        const bool act = xv != key_max<T>();
+        const uint32_t b = bm((U)xv - (U)mn);
+        word = act ? b >> 1 : (uint32_t)(threadIdx.x & 63);
+        sh = (b & 1) << 4;
+        inc = act ? 1u << sh : 0u;
+    }
+};
+template <typename T>
+__device__ __forceinline__ void bin_count(const T (&x)[R], T mn, const BinMap<T> &bm, uint32_t *cw) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        const BinAt<T> a(x[i], mn, bm);
+        atomicAdd(&cw[a.word], a.inc);
+    }
+}
+template <typename T>
+__device__ __forceinline__ void bin_place(const T (&x)[R], T mn, const BinMap<T> &bm, uint32_t *cw, T *s) {
+    constexpr int G = 8;  // atomics in flight per thread (more spill at 64 registers)
+#pragma unroll
+    for (int g = 0; g < R; g += G) {
+        uint32_t old[G];
+#pragma unroll
+        for (int i = 0; i < G; ++i) {
+            const BinAt<T> a(x[g + i], mn, bm);
+            old[i] = atomicAdd(&cw[a.word], a.inc);
+        }
+#pragma unroll
+        for (int i = 0; i < G; ++i) {
+            const BinAt<T> a(x[g + i], mn, bm);
+            if (a.inc) s[(old[i] >> a.sh) & 0xFFFFu] = x[g + i];
         }
     }
 }
@@ -729,12 +779,11 @@ __device__ __forceinline__ bool bin_sort_tile(const T (&x)[R], int valid, T *s, 
     const uint32_t bf = (uint32_t)__builtin_amdgcn_readfirstlane((int)bx);
     const bool hot = block_or<WAVES>(hot_hint || (lane == 0 && __popcll(__ballot(act0 && bx == bf)) >= 8), sm.flag);
     // 2. counting
-    if (hot) {
+    if (hot || !BIN_BATCH<T>) {
 #pragma unroll
-        for (int i = 0; i < R; ++i) bin_put<true, false>(x[i], mn, bm, cw, s, lane);
+        for (int i = 0; i < R; ++i) bin_put<false>(x[i], mn, bm, cw, s, lane, hot);
     } else {
-#pragma unroll
-        for (int i = 0; i < R; ++i) bin_put<false, false>(x[i], mn, bm, cw, s, lane);
+        bin_count(x, mn, bm, cw);
     }
     __syncthreads();
     // 3. starts
@@ -767,12 +816,14 @@ __device__ __forceinline__ bool bin_sort_tile(const T (&x)[R], int valid, T *s, 
     *c4 = make_uint4(wd[0], wd[1], wd[2], wd[3]);
     __syncthreads();  // (also: sm, in s, is dead from here)
     // 4. keys to their places
-    if (hot) {
+    // (mn through an opaque copy: the bins are recomputed here, not kept in registers across
+    // the scan, where they would spill)
+    asm volatile("" : "+v"(mn));
+    if (hot || !BIN_BATCH<T>) {
 #pragma unroll
-        for (int i = 0; i < R; ++i) bin_put<true, true>(x[i], mn, bm, cw, s, lane);
+        for (int i = 0; i < R; ++i) bin_put<true>(x[i], mn, bm, cw, s, lane, hot);
     } else {
-#pragma unroll
-        for (int i = 0; i < R; ++i) bin_put<false, true>(x[i], mn, bm, cw, s, lane);
+        bin_place(x, mn, bm, cw, s);
     }
     __syncthreads();
     // 5. window passes; a descent can only be left at a boundary of the last pass's windows

@@ -6,8 +6,8 @@ REPO="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}"
 cd /tmp; export TMPDIR=/tmp; cd "$REPO"
 for spec in "$@"; do
   tag=${spec%%:*}; envs=${spec#*:}
-  mkdir -p "$REPO/gpurun_out/pv_$tag"
-  env $envs timeout -k 10 120 rocprofv3 --kernel-trace -d "$REPO/gpurun_out/pv_$tag" -o run -- \
-    python3 -u "$REPO/scripts/dev/ktime.py" --reps ${REPS:-3} $KTIME_ARGS > "$REPO/gpurun_out/pv_$tag/ktime.log" 2>&1
-  grep total "$REPO/gpurun_out/pv_$tag/ktime.log" | grep -v SQLite
+  P=${PREFIX:-pv}; mkdir -p "$REPO/gpurun_out/${P}_$tag"
+  env $envs timeout -k 10 120 rocprofv3 --kernel-trace -d "$REPO/gpurun_out/${P}_$tag" -o run -- \
+    python3 -u "$REPO/scripts/dev/ktime.py" --reps ${REPS:-3} $KTIME_ARGS > "$REPO/gpurun_out/${P}_$tag/ktime.log" 2>&1
+  grep total "$REPO/gpurun_out/${P}_$tag/ktime.log" | grep -v SQLite
 done

@@ -1,6 +1,7 @@
 """Per-kernel average times from the rocprofv3 databases written by prof_variants.sh."""
 import glob, sqlite3, sys
-for d in sorted(glob.glob("gpurun_out/pv_*")):
+import os
+for d in sorted(glob.glob("gpurun_out/" + os.environ.get("PREFIX", "pv") + "_*")):
     if len(sys.argv) > 1 and not any(a in d for a in sys.argv[1:]):
         continue
     dbs = glob.glob(d + "/**/*.db", recursive=True)
