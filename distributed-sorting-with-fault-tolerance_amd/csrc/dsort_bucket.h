@@ -548,6 +548,11 @@ __device__ __forceinline__ uint32_t wg_order(uint32_t bid, uint32_t G) {
 #endif
 }
 
+#ifdef DSORT_STAMPS
+// Diagnostic build only: per-workgroup phase cycle sums of the line scatter (wave 0), read back
+// by dsort_debug_bkstamps().
+__device__ unsigned long long g_bkstamps[8192 * 16];
+#endif
 constexpr int BK_LK = 16;      // int32 keys per 64-byte line
 constexpr int BK_MAXC = 3072;  // lines per sub-tile at most: (SUB + 30 * BK_MAXB) / 16
 static __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const int32_t *__restrict__ in, uint64_t n,
@@ -572,6 +577,19 @@ static __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const
     const int tb = threadIdx.x, lane = tb & 63, w = tb >> 6;
     const uint32_t g = wg_order(blockIdx.x, gridDim.x);
     const bool owner = tb < B;  // thread b owns bucket b's line stream
+#ifdef DSORT_STAMPS
+    uint64_t st_acc[10] = {}, st_t0 = __builtin_amdgcn_s_memtime();
+#define BKST(k)                                                   \
+    do {                                                          \
+        const uint64_t t1_ = __builtin_amdgcn_s_memtime();        \
+        st_acc[k] += t1_ - st_t0;                                 \
+        st_t0 = t1_;                                              \
+    } while (0)
+#else
+#define BKST(k) \
+    do {        \
+    } while (0)
+#endif
     uint32_t vc = 0, ph = 0, gb = 0;
     if (owner) {
         const uint32_t o = (uint32_t)offs[(uint64_t)g * B + tb];
@@ -618,6 +636,7 @@ static __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const
             }
         }
         __syncthreads();
+        BKST(0);
         // one scan of (new keys, lines to write) per bucket, packed in 16-bit halves
         const uint32_t hv = owner ? hm.hist[tb] : 0;
         const uint32_t L = vc + hv;  // entries of the stream not yet written
@@ -630,6 +649,7 @@ static __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const
         }
         if (lane == 63) wsum[w] = incl;
         __syncthreads();
+        BKST(1);
         uint32_t woff = 0, all = 0;
 #pragma unroll
         for (int i = 0; i < BK_T / 64; ++i) {
@@ -642,11 +662,13 @@ static __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const
         if (owner) st[tb] = make_uint4(lks, vc | ph << 5 | hv << 10, p0, gb);
         for (uint32_t i = tb; i < C; i += BK_T) hm.map[i] = 0;  // the histogram is dead
         __syncthreads();
+        BKST(2);
 #pragma unroll
         for (int k = 0; k < KPT; ++k)
             if (bk[k] >= 0) lk[st[bk[k]].x + slot[k]] = key[k];
         if (nl) hm.map[p0] = (uint16_t)(tb + 1);
         __syncthreads();
+        BKST(3);
         // max-scan of the map: every line gets the bucket of the last first-line at or before it
         uint32_t m[3];
 #pragma unroll
@@ -663,6 +685,7 @@ static __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const
         const uint32_t below = __shfl_up(mx, 1);
         if (lane == 63) wsum[w] = mx;
         __syncthreads();
+        BKST(4);
         uint32_t pre = lane ? below : 0;
         for (int i = 0; i < w; ++i) pre = wsum[i] > pre ? wsum[i] : pre;
 #pragma unroll
@@ -671,6 +694,7 @@ static __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const
             if (i < C) hm.map[i] = (uint16_t)(m[t] > pre ? m[t] : pre);
         }
         __syncthreads();
+        BKST(5);
         // whole lines: 4 lanes per line, 4 keys (16 bytes) per lane
         for (uint32_t it = tb; it < 4 * C; it += BK_T) {
             const uint32_t j = it >> 2, q = it & 3;
@@ -697,8 +721,10 @@ static __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const
                     if (ok[t]) out[(uint32_t)(gi + t)] = v[t];
             }
         }
+        BKST(6);
         if (last) break;
         __syncthreads();
+        BKST(7);
         // carry the tail of every stream: entries [16 nl, L) -> carry[0, L - 16 nl)
         if (owner) {
             const uint32_t nv = L - nl * BK_LK;
@@ -708,7 +734,13 @@ static __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const
             gb += nl * BK_LK;
             vc = nv;
         }
+        BKST(8);
     }
+#ifdef DSORT_STAMPS
+    if (tb == 0 && blockIdx.x < 8192)
+        for (int k = 0; k < 10; ++k) g_bkstamps[blockIdx.x * 16 + k] = st_acc[k];
+#endif
+#undef BKST
 }
 
 }  // namespace bk

@@ -582,6 +582,19 @@ struct BinMap {
 // The keys of one register slot into the bins.  HOT: the lanes whose bin is the first active
 // lane's add with one atomic (a duplicate run puts a whole wave into one bin).  SCATTER: the
 // atomic returns the bin's cursor and the key goes to s there; else it only counts.
+// Physical LDS slot of tile position p in the bin sort.  A window of 16 keys (one thread's) is
+// sizeof(T) 16-byte chunks; unswizzled, the lanes of one ds_read_b128 / ds_write_b128 group read
+// windows 64 (int32) or 128 (int64) bytes apart, i.e. the same banks 4 or 8 times over.  The
+// chunks of a window are XOR-rotated by the window's index above its bank row, so those lanes hit
+// distinct banks; the rotation stays inside the window (a bijection on [0, TILE)).
+template <typename T>
+__device__ __forceinline__ uint32_t bsw(uint32_t p) {
+    constexpr int CW = (int)sizeof(T);          // chunks per window: 4 (int32), 8 (int64)
+    constexpr int LK = sizeof(T) == 4 ? 2 : 1;  // log2 keys per chunk
+    constexpr int A = sizeof(T) == 4 ? 6 : 5;   // log2 keys per bank row of windows (256 B) + 4
+    return p ^ (((p >> A) & (CW - 1)) << LK);
+}
+
 // Counting (SCATTER = false) or placing (the atomic returns the bin's cursor and the key goes to
 // s there) of one key.  hot (a duplicate run): the lanes whose bin is the first active lane's add
 // with one aggregated atomic.  (The batched int64 plain path is bin_count / bin_place.)
@@ -596,7 +609,7 @@ __device__ __forceinline__ void bin_put(T xv, T mn, const BinMap<T> &bm, uint32_
         if (act) {
             if constexpr (SCATTER) {
                 const uint32_t old = atomicAdd(&hw[b >> 1], inc);
-                s[(b & 1) ? old >> 16 : old & 0xFFFFu] = xv;
+                s[bsw<T>((b & 1) ? old >> 16 : old & 0xFFFFu)] = xv;
             } else {
                 atomicAdd(&hw[b >> 1], inc);
             }
@@ -620,7 +633,7 @@ __device__ __forceinline__ void bin_put(T xv, T mn, const BinMap<T> &bm, uint32_
         old0 = (uint32_t)__shfl((int)old0, first);
         if (act && b == b0)
             pos = ((b0 & 1) ? old0 >> 16 : old0 & 0xFFFFu) + (uint32_t)__popcll(same & ((1ull << lane) - 1));
-        if (act) s[pos] = xv;
+        if (act) s[bsw<T>(pos)] = xv;
     } else {
         if (act && b != b0) atomicAdd(&hw[b >> 1], inc);
         if (lane == first) atomicAdd(&hw[b0 >> 1], inc0);
@@ -668,7 +681,7 @@ __device__ __forceinline__ void bin_place(const T (&x)[R], T mn, const BinMap<T>
 #pragma unroll
         for (int i = 0; i < G; ++i) {
             const BinAt<T> a(x[g + i], mn, bm);
-            if (a.inc) s[(old[i] >> a.sh) & 0xFFFFu] = x[g + i];
+            if (a.inc) s[bsw<T>((old[i] >> a.sh) & 0xFFFFu)] = x[g + i];
         }
     }
 }
@@ -702,15 +715,17 @@ __device__ __forceinline__ void window_pass(T *s, int M, int tid) {
     const int ws = 16 * tid + OFF;
     if (ws >= M || ws + 16 > TILE_OF<T>) return;
     T v[16];
-    V *p = reinterpret_cast<V *>(s + ws);  // 16-byte aligned: OFF * sizeof(T) is
+    V *p[16 / N];  // the window's 16-byte chunks (their physical slots: bsw)
 #pragma unroll
-    for (int q = 0; q < 16 / N; ++q) V16<T>::get(p[q], v + N * q);
+    for (int q = 0; q < 16 / N; ++q) p[q] = reinterpret_cast<V *>(s + bsw<T>((uint32_t)(ws + N * q)));
+#pragma unroll
+    for (int q = 0; q < 16 / N; ++q) V16<T>::get(*p[q], v + N * q);
 #pragma unroll
     for (int k = 0; k < 16; ++k) v[k] = ws + k < M ? v[k] : key_max<T>();
     if constexpr (MERGE) merge_halves<16>(v);
     else sort_net<16>(v);
 #pragma unroll
-    for (int q = 0; q < 16 / N; ++q) p[q] = V16<T>::make(v + N * q);
+    for (int q = 0; q < 16 / N; ++q) *p[q] = V16<T>::make(v + N * q);
 }
 
 // Bin sort of one tile held in x (slots past `valid` are key_max) into out[0, valid).
@@ -832,14 +847,14 @@ __device__ __forceinline__ bool bin_sort_tile(const T (&x)[R], int valid, T *s, 
     window_pass<8, true>(s, (int)M, tid);
     __syncthreads();
     const int e8 = 16 * tid + 8;
-    if (block_or<WAVES>(e8 < (int)M && s[e8 - 1] > s[e8], cw)) {  // (cw is dead from step 5)
+    if (block_or<WAVES>(e8 < (int)M && s[bsw<T>(e8 - 1)] > s[bsw<T>(e8)], cw)) {  // (cw is dead from step 5)
         window_pass<0, true>(s, (int)M, tid);
         __syncthreads();
         const int e16 = 16 * tid + 16;
-        if (block_or<WAVES>(e16 < (int)M && s[e16 - 1] > s[e16], cw + WAVES)) return false;
+        if (block_or<WAVES>(e16 < (int)M && s[bsw<T>(e16 - 1)] > s[bsw<T>(e16)], cw + WAVES)) return false;
     }
     // 6. out: the binned keys in order, then key_max
-    for (int i = tid; i < valid; i += THREADS) out[i] = (uint32_t)i < M ? s[i] : key_max<T>();
+    for (int i = tid; i < valid; i += THREADS) out[i] = (uint32_t)i < M ? s[bsw<T>(i)] : key_max<T>();
     return true;
 }
 
@@ -2054,6 +2069,9 @@ static int wave_merge(dsort_ctx *ctx, const T *d_in, const size_t *lens, int k, 
 #ifdef DSORT_STAMPS
 extern "C" int dsort_debug_stamps(void *host, size_t bytes) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(wv::g_stamps), bytes) == hipSuccess ? 0 : -1;
+}
+extern "C" int dsort_debug_bkstamps(void *host, size_t bytes) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(bk::g_bkstamps), bytes) == hipSuccess ? 0 : -1;
 }
 #endif
 

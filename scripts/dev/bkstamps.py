@@ -1,0 +1,34 @@
+#!/usr/bin/env python3
+"""Phase cycle sums of the int32 line scatter from a DSORT_STAMPS build (DSORT_LIB=...): per
+workgroup (wave 0's view), averaged over workgroups; dev tool."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(REPO, "distributed-sorting-with-fault-tolerance_amd"))
+import torch  # noqa: E402
+import dsort  # noqa: E402
+
+n = 1 << 30
+ctx = dsort.Context(0)
+t = torch.empty(n, dtype=torch.int32, device="cuda")
+ctx.gen_uniform(t, 0x5EED2026)
+o = torch.empty_like(t)
+ctx.sort_dev(t, o)
+ctx.sort_dev(t, o)
+torch.cuda.synchronize()
+buf = np.zeros(8192 * 16, dtype=np.uint64)
+fn = ctx.lib.dsort_debug_bkstamps
+fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+assert fn(buf.ctypes.data, buf.nbytes) == 0
+S = buf.reshape(-1, 16).astype(np.float64)
+S = S[S[:, :9].sum(axis=1) > 0]
+names = ["zero+loads+lookup+atomics", "scan", "st+map clear", "lk writes", "max-scan", "map write",
+         "lines", "barrier", "carry"]
+tot = S[:, :9].sum(axis=1)
+print(f"workgroups {len(S)}  cycles per workgroup: mean {tot.mean():.0f}")
+for k, nm in enumerate(names):
+    print(f"  {nm:28s} {S[:, k].mean():12.0f}  {100 * S[:, k].mean() / tot.mean():5.1f} %")
