@@ -854,7 +854,13 @@ __device__ __forceinline__ bool bin_sort_tile(const T (&x)[R], int valid, T *s, 
         if (block_or<WAVES>(e16 < (int)M && s[bsw<T>(e16 - 1)] > s[bsw<T>(e16)], cw + WAVES)) return false;
     }
     // 6. out: the binned keys in order, then key_max
-    for (int i = tid; i < valid; i += THREADS) out[i] = (uint32_t)i < M ? s[bsw<T>(i)] : key_max<T>();
+    // (indices start m keys below the tile, at the 128-byte line below out, so every wave's store
+    // covers whole lines: tiles start anywhere, and lines shared by two waves' stores came out as
+    // partial writes, 14 % of the written bytes)
+    constexpr int LK = 128 / (int)sizeof(T);
+    const int m = (int)((reinterpret_cast<uintptr_t>(out) / sizeof(T)) & (LK - 1));
+    for (int i = tid - m; i < valid; i += THREADS)
+        if (i >= 0) out[i] = (uint32_t)i < M ? s[bsw<T>(i)] : key_max<T>();
     return true;
 }
 
