@@ -79,6 +79,7 @@ template <> struct Comp<int32_t> {
     __host__ __device__ static uint32_t slot_of(int32_t key, int bits) {
         return ((uint32_t)key ^ 0x80000000u) >> (32 - bits);
     }
+    __host__ __device__ static int32_t key_of(C c) { return (int32_t)(c >> 32); }
     static constexpr int KB = 32;  // key bits
 };
 template <> struct Comp<int64_t> {
@@ -94,6 +95,7 @@ template <> struct Comp<int64_t> {
     __host__ __device__ static uint32_t slot_of(int64_t key, int bits) {
         return (uint32_t)(((uint64_t)key ^ 0x8000000000000000ull) >> (64 - bits));
     }
+    __host__ __device__ static int64_t key_of(const C &c) { return c.k; }
     static constexpr int KB = 64;
 };
 

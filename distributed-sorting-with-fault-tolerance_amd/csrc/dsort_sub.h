@@ -452,6 +452,11 @@ __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restric
 // [j0, j1) of a bucket) is then one contiguous piece of every chunk of the bucket,
 // [pref[c][j0], pref[c][j1]), gathered by the tile sort (about 1 KiB per piece) -- no
 // element-granular scatter to HBM.
+#ifdef DSORT_STAMPS
+// Diagnostic build only: per-workgroup phase cycles of sb_local_kernel, read back by
+// dsort_debug_sbstamps().
+__device__ unsigned long long g_sbstamps[(1u << 18) * 8];
+#endif
 #ifndef DSORT_SB_LT
 #define DSORT_SB_LT 512
 #endif
@@ -475,6 +480,19 @@ __global__ void __launch_bounds__(SB_LT, 4) sb_local_kernel(T *__restrict__ buf,
     __shared__ uint32_t hist[SB_MAXS];   // chunk histogram, then the LDS starts
     __shared__ uint32_t wsum[SB_LT / 64];
     __shared__ T lk[CHL];
+#ifdef DSORT_STAMPS
+    uint64_t st_acc[6] = {}, st_t0 = __builtin_amdgcn_s_memtime();
+#define SBST(k)                                            \
+    do {                                                   \
+        const uint64_t t1_ = __builtin_amdgcn_s_memtime(); \
+        st_acc[k] = t1_ - st_t0;                           \
+        st_t0 = t1_;                                       \
+    } while (0)
+#else
+#define SBST(k) \
+    do {        \
+    } while (0)
+#endif
     const Chunk c = ch[blockIdx.x];
     const BInfo b = bi[c.b];
     uint32_t *pc = pref + (uint64_t)blockIdx.x * (SS + 1);
@@ -499,6 +517,7 @@ __global__ void __launch_bounds__(SB_LT, 4) sb_local_kernel(T *__restrict__ buf,
     for (int q = 0; q < PER; ++q) hist[PER * tid + q] = 0;
     const SlotFn<T> f = sfn[c.b];
     __syncthreads();
+    SBST(0);
     uint32_t pk[KPT];  // sub-bucket | rank << 10
     // In groups of G keys: the slot-table reads, then the splitter reads, then the atomics, so a
     // key's LDS round trips do not wait for the previous key's.  A key past the chunk adds 0.
@@ -538,6 +557,7 @@ __global__ void __launch_bounds__(SB_LT, 4) sb_local_kernel(T *__restrict__ buf,
     }
     }
     __syncthreads();
+    SBST(1);
     uint32_t h[PER], sum = 0;
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
@@ -551,6 +571,7 @@ __global__ void __launch_bounds__(SB_LT, 4) sb_local_kernel(T *__restrict__ buf,
     }
     if (lane == 63) wsum[w] = incl;
     __syncthreads();
+    SBST(2);
     uint32_t ex = incl - sum;
 #pragma unroll
     for (int i = 0; i < SB_LT / 64; ++i) ex += i < w ? wsum[i] : 0u;
@@ -563,17 +584,25 @@ __global__ void __launch_bounds__(SB_LT, 4) sb_local_kernel(T *__restrict__ buf,
         ex += h[q];
     }
     __syncthreads();
+    SBST(3);
 #pragma unroll
     for (int k = 0; k < KPT; ++k) {
         const uint32_t i = tid + k * SB_LT;
         if (i < c.len) lk[hist[pk[k] & 1023] + (pk[k] >> 10)] = key[k];
     }
     __syncthreads();
+    SBST(4);
 #pragma unroll
     for (int k = 0; k < KPT; ++k) {
         const uint32_t i = tid + k * SB_LT;
         if (i < c.len) src[i] = lk[i];
     }
+#ifdef DSORT_STAMPS
+    SBST(5);
+    if (tid == 0 && blockIdx.x < (1u << 18))
+        for (int k = 0; k < 6; ++k) g_sbstamps[blockIdx.x * 8 + k] = st_acc[k];
+#endif
+#undef SBST
 }
 
 // Workgroup -> chunk: every XCD takes a contiguous block of chunks, i.e. of buckets, so the

@@ -745,13 +745,13 @@ __device__ __forceinline__ void window_pass(T *s, int M, int tid) {
 // cw holds the counters (NB / 2 words); the caller has passed a barrier since its last use.
 template <typename T>
 __device__ __forceinline__ bool bin_sort_tile(const T (&x)[R], int valid, T *s, uint32_t *cw, T *out,
-                                              bool hot_hint) {
+                                              bool hot_hint, const int tid) {
     using U = typename sb::KeyU<T>::U;
     constexpr int WAVES = WG<T>::WAVES, THREADS = 64 * WAVES, NB = BIN_NB<T>;
     constexpr int BPT = NB / THREADS;
     static_assert(BPT == 8, "one 16-byte word of counters per thread");
     BinSm<T> &sm = *reinterpret_cast<BinSm<T> *>(s);
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int lane = tid & 63, w = tid >> 6;
     // 1. range
     T mn = key_max<T>(), mx = key_min<T>();
 #pragma unroll
@@ -1039,7 +1039,8 @@ __global__ void __launch_bounds__(64 * WG<T>::WAVES, DSORT_BIN_OCC) bin_sort_ker
         if (j < jh && j + 1 < nspl) hint = sp[j].k == sp[j + 1].k;
         hint = __ballot(hint) != 0;
     }
-    if (!bin_sort_tile<T>(x, valid, s, cw, out + base, hint) && threadIdx.x == 0) fb[atomicAdd(nfb, 1u)] = blockIdx.x;
+    if (!bin_sort_tile<T>(x, valid, s, cw, out + base, hint, threadIdx.x) && threadIdx.x == 0)
+        fb[atomicAdd(nfb, 1u)] = blockIdx.x;
 }
 
 // The bitonic tile sort: tile fb[blockIdx.x] (fb = the bin sort's declined tiles) or tile
@@ -1344,7 +1345,9 @@ static int tile_sort(dsort_ctx *ctx, const T *in, T *out, uint64_t n, const uint
     const dim3 blk(64 * WG<T>::WAVES);
     int rc = tile_sort_event(ctx, s, timed, 0);
     if (rc) return rc;
-    if (DSORT_BIN_SORT && grid) {
+    // The library's own small sorts (timed = false: the splitter samples) take the bitonic sort
+    // alone: it needs no read-back, so the host never waits in the middle of a sort for them.
+    if (DSORT_BIN_SORT && grid && timed) {
         rc = ensure(ctx, &ctx->tfb, &ctx->tfb_bytes, ((size_t)grid + 1) * 4, "tile fallback list");
         if (rc) return rc;
         if (!ctx->tfb_host) DSORT_HIP(ctx, hipHostMalloc((void **)&ctx->tfb_host, 64, hipHostMallocDefault));
@@ -1475,12 +1478,12 @@ static std::vector<size_t> sub_tile_runs(uint64_t p, uint64_t len, uint64_t tile
 // locally partitioned keys, if the local pass already ran: still the same buckets).
 template <typename T>
 static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_t *hb, int B, uint64_t m,
-                    hipStream_t s, bool timed, bool local) {
+                    hipStream_t s, bool timed, bool local, const uint8_t *pure) {
     using namespace sb;
     constexpr int TILE = TILE_OF<T>;
     constexpr uint64_t ALIGN = KPC<T>;
     for (int b = 0; b < B && local; ++b)
-        if (ceil_div(hb[b + 1] - hb[b], (uint64_t)SB_LCH<T>) > (uint64_t)kMaxPieces<T>) local = false;
+        if (!pure[b] && ceil_div(hb[b + 1] - hb[b], (uint64_t)SB_LCH<T>) > (uint64_t)kMaxPieces<T>) local = false;
     const uint64_t CH = local ? SB_LCH<T> : SB_CH<T>;
     // samples per sub-bucket; a bucket's samples (<= SB_MAXS * 8) fit one int64 tile
     constexpr int kMaxOs = TILE_OF<int64_t> / SB_MAXS;
@@ -1489,13 +1492,13 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
     // maximum rate, so the size spread (about 1/sqrt(os)) keeps every sub-bucket below a tile
     if (ctx->opt.sub_os <= 0)
         for (int b = 0; b < B; ++b)
-            if (hb[b + 1] - hb[b] > (uint64_t)SB_MAXS * TILE / 4) os = kMaxOs;
+            if (!pure[b] && hb[b + 1] - hb[b] > (uint64_t)SB_MAXS * TILE / 4) os = kMaxOs;
     // bucket and chunk tables
     std::vector<BInfo> bi((size_t)B);
     uint64_t nsmp = 0, nch = 0, nsubs = 0;
     int SS = 1;
     for (int b = 0; b < B; ++b) {
-        const uint64_t len = hb[b + 1] - hb[b];
+        const uint64_t len = pure[b] ? 0 : hb[b + 1] - hb[b];  // (a pure bucket: no chunks, no tiles)
         uint64_t ns = len <= (uint64_t)TILE ? 1 : ceil_div(len, m);
         ns = ns > (uint64_t)SB_MAXS ? SB_MAXS : ns;
         const uint64_t nc = ceil_div(len, CH);
@@ -1561,6 +1564,19 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
     if (nch) DSORT_HIP(ctx, hipMemcpyAsync(dch, h + h_ch, nch * sizeof(Chunk), hipMemcpyHostToDevice, s));
     DSORT_HIP(ctx, hipMemcpyAsync(stl, hst, B * sizeof(bk::TileRef) + 16, hipMemcpyHostToDevice, s));
     DSORT_HIP(ctx, hipMemsetAsync(num, 0, 8, s));
+    // pure buckets (one key) to the output as they lie, runs of them in one copy
+    for (int b = 0; b < B;) {
+        if (!pure[b]) {
+            ++b;
+            continue;
+        }
+        int e = b;
+        while (e < B && pure[e]) ++e;
+        if (hb[e] > hb[b])
+            DSORT_HIP(ctx, hipMemcpyAsync(d_keys + hb[b], src + hb[b], (hb[e] - hb[b]) * sizeof(T),
+                                          hipMemcpyDeviceToDevice, s));
+        b = e;
+    }
     // 1. splitters of every bucket from a regular sample.  A bucket's samples fit one int64 tile,
     // so the tile sort alone sorts them, one workgroup per bucket.
     if (nsmp) {
@@ -1593,9 +1609,11 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         DSORT_HIP(ctx, hipGetLastError());
         DSORT_HIP(ctx, hipMemcpyAsync(hn, num, 8, hipMemcpyDeviceToHost, s));
         DSORT_HIP(ctx, hipEventRecord(ctx->sub_ev, s));
+        // (the tile count sizes the grid: a grid at its bound, 9x the tiles at 2^30 int32, cost
+        // more in empty workgroups than this wait -- measured 10.6 vs 10.1 ms)
         DSORT_HIP(ctx, hipEventSynchronize(ctx->sub_ev));
         const uint32_t ntiles = hn[0], novf = hn[1];
-        if (novf) return sub_sort<T>(ctx, src, d_keys, n, hb, B, m, s, timed, false);
+        if (novf) return sub_sort<T>(ctx, src, d_keys, n, hb, B, m, s, timed, false, pure);
         if (ntiles > tmax) return set_err(ctx, DSORT_EHIP, "sub-bucket packing overflow");
         ctx->stats.merge_passes = 0;
         // 3. tile sort: gathered from the chunks into d_keys
@@ -1704,7 +1722,7 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
     rc = ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, n * sizeof(T), "sort scratch");
     if (rc) return rc;
     T *scratch = static_cast<T *>(ctx->scratch);
-    const size_t hbytes = (size_t)(BK_MAXB + 1) * 8;
+    const size_t hbytes = (size_t)(BK_MAXB + 1) * 8 + (size_t)BK_MAXB * 16;  // starts, then the splitters
     if (ctx->bucket_host_bytes < hbytes) {
         if (ctx->bucket_host) (void)hipHostFree(ctx->bucket_host);
         ctx->bucket_host = nullptr;
@@ -1764,6 +1782,8 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
     // input: the context owns it); the tile sort then writes whichever buffer makes the last
     // pass land in d_keys.
     DSORT_HIP(ctx, hipMemcpyAsync(hb, bst, (size_t)(B + 1) * 8, hipMemcpyDeviceToHost, s));
+    C *hspl = reinterpret_cast<C *>(hb + BK_MAXB + 1);
+    DSORT_HIP(ctx, hipMemcpyAsync(hspl, spl, (size_t)(B - 1) * sizeof(C), hipMemcpyDeviceToHost, s));
     DSORT_HIP(ctx, hipEventRecord(ctx->bucket_ev, s));
     T *part_out = scratch;
     if constexpr (std::is_same<T, int32_t>::value && DSORT_BK_LINES) {
@@ -1776,8 +1796,14 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
     DSORT_HIP(ctx, hipGetLastError());
     DSORT_HIP(ctx, hipEventSynchronize(ctx->bucket_ev));
     if (hb[B] != n) return set_err(ctx, DSORT_EHIP, "bucket partition lost keys");
-    if (const uint64_t m = sub_keys<T>(ctx))
-        return sub_sort<T>(ctx, part_out, d_keys, n, hb, B, m, s, timed, ctx->opt.sub_gather != 0);
+    if (const uint64_t m = sub_keys<T>(ctx)) {
+        // A bucket between two splitters of the same key holds only that key: it is sorted as it
+        // lies (a heavy duplicate -- Zipf's top keys fill whole buckets).  The second level skips
+        // it and copies it to the output.
+        std::vector<uint8_t> pure((size_t)B, 0);
+        for (int b = 1; b + 1 < B; ++b) pure[b] = Comp<T>::key_of(hspl[b - 1]) == Comp<T>::key_of(hspl[b]);
+        return sub_sort<T>(ctx, part_out, d_keys, n, hb, B, m, s, timed, ctx->opt.sub_gather != 0, pure.data());
+    }
     // pass plan: the runs of every bucket; the largest bucket's run count R sets the merge
     // levels L = ceil(log2 R), split into the fewest passes of <= max_logf levels (larger passes
     // first).
@@ -2075,6 +2101,9 @@ static int wave_merge(dsort_ctx *ctx, const T *d_in, const size_t *lens, int k, 
 #ifdef DSORT_STAMPS
 extern "C" int dsort_debug_stamps(void *host, size_t bytes) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(wv::g_stamps), bytes) == hipSuccess ? 0 : -1;
+}
+extern "C" int dsort_debug_sbstamps(void *host, size_t bytes) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(sb::g_sbstamps), bytes) == hipSuccess ? 0 : -1;
 }
 extern "C" int dsort_debug_bkstamps(void *host, size_t bytes) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(bk::g_bkstamps), bytes) == hipSuccess ? 0 : -1;

@@ -245,3 +245,24 @@ def test_bucketed_sort_unaligned_view_in_place(gpu_ctx, dtype, shift):
     d = buf.cpu().numpy()
     assert np.array_equal(d[shift:shift + n], np.sort(a))
     assert (d[:shift] == 5).all() and (d[shift + n:] == 5).all()
+
+
+@pytest.mark.parametrize("dtype", [np.int32, np.int64])
+@pytest.mark.parametrize("mode", ["local", "scatter"])
+@pytest.mark.parametrize("n", [1 << 22, (1 << 22) + 12345])
+def test_pure_buckets_heavy_keys(gpu_ctx, dtype, mode, n):
+    """Heavy keys filling whole buckets: a bucket between two splitters of the same key holds only
+    that key and is copied to the output as it lies (no sub-buckets, no tiles); the buckets around
+    it (the heavy key plus its neighbours) take the normal path.  Runs of pure buckets next to each
+    other and a pure bucket next to the first and the last bucket."""
+    rng = np.random.default_rng(n + (7 if dtype == np.int64 else 0))
+    info = np.iinfo(dtype)
+    a = rng.integers(info.min, info.max, n, endpoint=True, dtype=dtype)
+    r = rng.random(n)
+    a[r < 0.40] = dtype(7)
+    a[(r >= 0.40) & (r < 0.55)] = dtype(-3)
+    a[(r >= 0.55) & (r < 0.60)] = info.max
+    a[(r >= 0.60) & (r < 0.63)] = info.min
+    opts = {"local": dict(), "scatter": dict(sub_gather=0)}[mode]
+    with gpu_ctx.options(buckets=256, **opts):
+        assert np.array_equal(_sort(gpu_ctx, a, False), np.sort(a))
