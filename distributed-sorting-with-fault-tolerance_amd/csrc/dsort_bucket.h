@@ -401,10 +401,11 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_kernel(const T *__restric
                                                               const typename Comp<T>::C *__restrict__ spl_g,
                                                               int B, int BP, int subs,
                                                               const uint64_t *__restrict__ offs,
-                                                              T *__restrict__ out) {
+                                                              T *__restrict__ out, T *__restrict__ out2) {
     using CT = Comp<T>;
     constexpr int KPT = Geo<T>::KPT, SUB = BK_T * KPT;
     __shared__ typename CT::C spl[BK_MAXB];
+    __shared__ uint8_t bpure[BK_MAXB];  // bucket between two splitters of one key: written to out2
     __shared__ uint32_t rng[BK_SLOTS];
     __shared__ uint2 sgo[BK_MAXB];       // (sub-tile scan, next global position) per bucket; n < 2^32
     __shared__ uint32_t hist[BK_MAXB];   // sub-tile histogram
@@ -421,6 +422,8 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_kernel(const T *__restric
     load_splitters<T>(spl_g, BP, spl);
     __syncthreads();
     build_slots<T>(spl, BP, rng);
+    for (int b = threadIdx.x; b < B; b += BK_T)
+        bpure[b] = out2 && b > 0 && b + 1 < B && CT::key_of(spl[b - 1]) == CT::key_of(spl[b]);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t g0 = (uint64_t)blockIdx.x * subs * SUB;
     T nxt[KPT];
@@ -499,7 +502,8 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_kernel(const T *__restric
             if (bk[k] >= 0) {
                 const uint2 so = sgo[bk[k]];
                 lk[so.x + slot[k]] = key[k];
-                lg[so.x + slot[k]] = so.y + slot[k];
+                // (bit 31: a pure bucket, to out2; out2 is only given when n < 2^31)
+                lg[so.x + slot[k]] = (so.y + slot[k]) | (uint32_t)bpure[bk[k]] << 31;
             }
         }
         __syncthreads();
@@ -507,11 +511,10 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_kernel(const T *__restric
 #pragma unroll
         for (int k = 0; k < KPT; ++k) {
             const uint32_t p = threadIdx.x + k * BK_T;
-#if defined(DSORT_ABL_SEQSTORE)
-            if (p < cnt) out[s0 + p] = lk[p] + (T)(lg[p] & 1);  // ablation: coalesced stores
-#else
-            if (p < cnt) out[lg[p]] = lk[p];
-#endif
+            if (p < cnt) {
+                const uint32_t gp = lg[p];
+                (gp >> 31 ? out2 : out)[gp & 0x7FFFFFFFu] = lk[p];
+            }
         }
         // advance every bucket's global position by this sub-tile's keys (sgo.x is not read
         // again before the next scan, which follows two barriers)
@@ -561,9 +564,11 @@ static __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const
                                                                     const int64_t *__restrict__ spl_g,
                                                                     int B, int BP, int subs,
                                                                     const uint64_t *__restrict__ offs,
-                                                                    int32_t *__restrict__ out) {
+                                                                    int32_t *__restrict__ out,
+                                                                    int32_t *__restrict__ out2) {
     using CT = Comp<int32_t>;
     constexpr int KPT = Geo<int32_t>::KPT, SUB = BK_T * KPT;
+    __shared__ uint8_t bpure[BK_MAXB];  // bucket between two splitters of one key: written to out2
     static_assert((SUB + 30 * BK_MAXB) / BK_LK <= BK_MAXC, "line map too small");
     static_assert(SUB < (1 << 15), "packed scan fields");
     __shared__ int64_t spl[BK_MAXB];
@@ -595,7 +600,9 @@ static __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const
     uint32_t vc = 0, ph = 0, gb = 0;
     if (owner) {
         const uint32_t o = (uint32_t)offs[(uint64_t)g * B + tb];
-        ph = (uint32_t)(((uintptr_t)(out + o) >> 2) & (BK_LK - 1));
+        const bool pure = out2 && tb > 0 && tb + 1 < B && CT::key_of(spl_g[tb - 1]) == CT::key_of(spl_g[tb]);
+        bpure[tb] = pure;
+        ph = (uint32_t)(((uintptr_t)((pure ? out2 : out) + o) >> 2) & (BK_LK - 1));
         vc = ph;
         gb = o - ph;  // (mod 2^32) the first line of the stream starts ph entries before o
     }
@@ -715,12 +722,13 @@ static __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const
                 v[t] = !ok[t] ? 0 : e < cv ? carry[b * BK_LK + e] : lk[sb.x + e - cv];
             }
             const uint32_t gi = sb.w + e0;  // mod 2^32
+            int32_t *tgt = bpure[b] ? out2 : out;
             if (full) {
-                *reinterpret_cast<int4 *>(out + gi) = make_int4(v[0], v[1], v[2], v[3]);
+                *reinterpret_cast<int4 *>(tgt + gi) = make_int4(v[0], v[1], v[2], v[3]);
             } else {
 #pragma unroll
                 for (int t = 0; t < 4; ++t)
-                    if (ok[t]) out[(uint32_t)(gi + t)] = v[t];
+                    if (ok[t]) tgt[(uint32_t)(gi + t)] = v[t];
             }
         }
         BKST(6);

@@ -1478,7 +1478,7 @@ static std::vector<size_t> sub_tile_runs(uint64_t p, uint64_t len, uint64_t tile
 // locally partitioned keys, if the local pass already ran: still the same buckets).
 template <typename T>
 static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_t *hb, int B, uint64_t m,
-                    hipStream_t s, bool timed, bool local, const uint8_t *pure) {
+                    hipStream_t s, bool timed, bool local, const uint8_t *pure, bool pure_done) {
     using namespace sb;
     constexpr int TILE = TILE_OF<T>;
     constexpr uint64_t ALIGN = KPC<T>;
@@ -1564,8 +1564,9 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
     if (nch) DSORT_HIP(ctx, hipMemcpyAsync(dch, h + h_ch, nch * sizeof(Chunk), hipMemcpyHostToDevice, s));
     DSORT_HIP(ctx, hipMemcpyAsync(stl, hst, B * sizeof(bk::TileRef) + 16, hipMemcpyHostToDevice, s));
     DSORT_HIP(ctx, hipMemsetAsync(num, 0, 8, s));
-    // pure buckets (one key) to the output as they lie, runs of them in one copy
-    for (int b = 0; b < B;) {
+    // pure buckets (one key) to the output as they lie, runs of them in one copy (unless the
+    // scatter wrote them there)
+    for (int b = 0; b < B && !pure_done;) {
         if (!pure[b]) {
             ++b;
             continue;
@@ -1613,7 +1614,7 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         // more in empty workgroups than this wait -- measured 10.6 vs 10.1 ms)
         DSORT_HIP(ctx, hipEventSynchronize(ctx->sub_ev));
         const uint32_t ntiles = hn[0], novf = hn[1];
-        if (novf) return sub_sort<T>(ctx, src, d_keys, n, hb, B, m, s, timed, false, pure);
+        if (novf) return sub_sort<T>(ctx, src, d_keys, n, hb, B, m, s, timed, false, pure, pure_done);
         if (ntiles > tmax) return set_err(ctx, DSORT_EHIP, "sub-bucket packing overflow");
         ctx->stats.merge_passes = 0;
         // 3. tile sort: gathered from the chunks into d_keys
@@ -1786,12 +1787,15 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
     DSORT_HIP(ctx, hipMemcpyAsync(hspl, spl, (size_t)(B - 1) * sizeof(C), hipMemcpyDeviceToHost, s));
     DSORT_HIP(ctx, hipEventRecord(ctx->bucket_ev, s));
     T *part_out = scratch;
+    // Pure buckets (one key, see below) go straight to d_keys, in their final places, when the
+    // second level runs (it skips them) and d_keys is not the input the scatter still reads.
+    T *direct = sub_keys<T>(ctx) && (const void *)d_in != (const void *)d_keys && n < (1ull << 31) ? d_keys : nullptr;
     if constexpr (std::is_same<T, int32_t>::value && DSORT_BK_LINES) {
         hipLaunchKernelGGL(bucket_scatter_lines_kernel, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl,
-                           B, BP, subs, offs, part_out);
+                           B, BP, subs, offs, part_out, direct);
     } else {
         hipLaunchKernelGGL(bucket_scatter_kernel<T>, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, B,
-                           BP, subs, offs, part_out);
+                           BP, subs, offs, part_out, direct);
     }
     DSORT_HIP(ctx, hipGetLastError());
     DSORT_HIP(ctx, hipEventSynchronize(ctx->bucket_ev));
@@ -1802,7 +1806,8 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
         // it and copies it to the output.
         std::vector<uint8_t> pure((size_t)B, 0);
         for (int b = 1; b + 1 < B; ++b) pure[b] = Comp<T>::key_of(hspl[b - 1]) == Comp<T>::key_of(hspl[b]);
-        return sub_sort<T>(ctx, part_out, d_keys, n, hb, B, m, s, timed, ctx->opt.sub_gather != 0, pure.data());
+        return sub_sort<T>(ctx, part_out, d_keys, n, hb, B, m, s, timed, ctx->opt.sub_gather != 0, pure.data(),
+                           direct != nullptr);
     }
     // pass plan: the runs of every bucket; the largest bucket's run count R sets the merge
     // levels L = ceil(log2 R), split into the fewest passes of <= max_logf levels (larger passes
