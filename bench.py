@@ -430,7 +430,7 @@ def run_single(args):
     if not ok:
         raise SystemExit("bench: sorted output failed verification")
     torch.cuda.synchronize()
-    kms, klaunch, bms, tot, npass, tsk, pms = 0.0, 0, 0.0, 0.0, 0, 0.0, 0.0
+    kms, klaunch, bms, tot, npass, tsk, pms, tkeys = 0.0, 0, 0.0, 0.0, 0, 0.0, 0.0, 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         ctx.sort_dev(t_in, out)
@@ -442,13 +442,14 @@ def run_single(args):
         npass += st["merge_passes"]
         tsk += st["tile_sort_kernel_ms"]
         pms += st["partition_ms"]
+        tkeys += st["tile_sort_keys"]
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     stats = ctx.stats()
     ctx.close()
     return t1 - t0, {"kernel_ms": kms, "launches": klaunch, "block_ms": bms, "device_ms": tot,
                      "passes": stats["merge_passes"], "npass": npass, "tile": stats["tile_keys"], "w": w,
-                     "tile_sort_ms": tsk, "partition_ms": pms}
+                     "tile_sort_ms": tsk, "partition_ms": pms, "tile_sort_keys": tkeys // max(args.steps, 1)}
 
 
 def run_multi(args, rank, world):
@@ -555,7 +556,9 @@ def report_single(args, elapsed, k):
     # sub-bucket path gathers its tiles from the locally partitioned chunks); merge passes only
     # run for oversized sub-buckets or with DSORT_OPT_SUB_KEYS = 0
     tile_ms = k["tile_sort_ms"] / args.steps
-    bytes_tile = 2 * k["w"] * n
+    # the keys the tile sort sorted: all of them, less the buckets of a single key (heavy
+    # duplicates), which the second level skips
+    bytes_tile = 2 * k["w"] * k["tile_sort_keys"]
     achieved = bytes_tile / (tile_ms * 1e-3) / 1e9 if tile_ms > 0 else 0.0
     npass = k["npass"]
     cfg = "C2-style" if args.dtype == "i32" else "C4-style"
@@ -568,6 +571,7 @@ def report_single(args, elapsed, k):
         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(TILE_SORT_KERNEL[k["w"]], n, k["w"]),
         "avg_launch_ms": round(tile_ms, 4), "algorithmic_bytes_per_launch": bytes_tile,
+        "tile_sort_keys": k["tile_sort_keys"],
         "partition_ms": round(k["partition_ms"] / args.steps, 3),
         "merge_passes": npass // max(args.steps, 1),
         "merge_kernel_ms": round(k["kernel_ms"] / args.steps, 4),

@@ -1564,6 +1564,9 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
     if (nch) DSORT_HIP(ctx, hipMemcpyAsync(dch, h + h_ch, nch * sizeof(Chunk), hipMemcpyHostToDevice, s));
     DSORT_HIP(ctx, hipMemcpyAsync(stl, hst, B * sizeof(bk::TileRef) + 16, hipMemcpyHostToDevice, s));
     DSORT_HIP(ctx, hipMemsetAsync(num, 0, 8, s));
+    uint64_t npure = 0;
+    for (int b = 0; b < B; ++b) npure += pure[b] ? hb[b + 1] - hb[b] : 0;
+    ctx->stats.tile_sort_keys = n - npure;
     // pure buckets (one key) to the output as they lie, runs of them in one copy (unless the
     // scatter wrote them there)
     for (int b = 0; b < B && !pure_done;) {
@@ -1757,6 +1760,7 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
     // (the nested sort reset the statistics and events; this sort's start from here)
     ctx->stats = dsort_stats{};
     ctx->stats.keys_in = ctx->stats.keys_out = n;
+    ctx->stats.tile_sort_keys = n;
     ctx->stats.tile_keys = TILE;
     ctx->ev_mask = 0;
     ctx->kev_used = 0;
@@ -2028,6 +2032,7 @@ static int wave_merge(dsort_ctx *ctx, const T *d_in, const size_t *lens, int k, 
     for (int j = 0; j < k; ++j) n += lens[j];
     if (!keep_stats) {
         ctx->stats.keys_in = ctx->stats.keys_out = n;
+        ctx->stats.tile_sort_keys = n;
         ctx->stats.tile_keys = TILE_OF<T>;
     }
     if (n == 0) return DSORT_OK;

@@ -62,7 +62,7 @@ class Stats(ctypes.Structure):
                 ("tile_keys", ctypes.c_int), ("keys_in", ctypes.c_size_t),
                 ("keys_out", ctypes.c_size_t), ("alltoall_ms", ctypes.c_double),
                 ("keys_sent", ctypes.c_size_t), ("tile_sort_kernel_ms", ctypes.c_double),
-                ("partition_ms", ctypes.c_double)]
+                ("partition_ms", ctypes.c_double), ("tile_sort_keys", ctypes.c_size_t)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -67,6 +67,8 @@ typedef struct dsort_stats {
     size_t keys_sent;       /* multi-GPU: keys this rank shipped to other ranks           */
     double tile_sort_kernel_ms; /* the tile sort kernel alone (HIP events around its launch) */
     double partition_ms;    /* bucketed sort: the partition passes before the tile sort   */
+    size_t tile_sort_keys;  /* keys the tile sort sorted (bucketed sort: a bucket of one key
+                               value -- a heavy duplicate -- is not tile-sorted)             */
 } dsort_stats;
 
 /* ---------------------------------------------------------------- lifecycle ---------- */
