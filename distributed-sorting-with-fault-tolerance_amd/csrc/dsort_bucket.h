@@ -80,7 +80,11 @@ template <> struct Comp<int32_t> {
         return ((uint32_t)key ^ 0x80000000u) >> (32 - bits);
     }
     __host__ __device__ static int32_t key_of(C c) { return (int32_t)(c >> 32); }
+    __host__ __device__ static uint32_t idx_of(C c) { return (uint32_t)c; }
+    using U = uint32_t;
+    __host__ __device__ static U flip(int32_t key) { return (uint32_t)key ^ 0x80000000u; }
     static constexpr int KB = 32;  // key bits
+    static constexpr bool ADAPT = false;  // fixed top-bit slots, no one-key slots (see BkMap)
 };
 template <> struct Comp<int64_t> {
     using C = Pair;
@@ -96,7 +100,11 @@ template <> struct Comp<int64_t> {
         return (uint32_t)(((uint64_t)key ^ 0x8000000000000000ull) >> (64 - bits));
     }
     __host__ __device__ static int64_t key_of(const C &c) { return c.k; }
+    __host__ __device__ static uint32_t idx_of(const C &c) { return c.i; }
+    using U = uint64_t;
+    __host__ __device__ static U flip(int64_t key) { return (uint64_t)key ^ 0x8000000000000000ull; }
     static constexpr int KB = 64;
+    static constexpr bool ADAPT = true;
 };
 
 // bucket of composite c: the number of splitters below c (spl holds BP entries, +inf padded)
@@ -108,44 +116,197 @@ __device__ __forceinline__ int bucket_of(const typename Comp<T>::C *spl, int BP,
     return lo;
 }
 
-// Radix-assisted lookup: slot = top BK_SLOTB bits of the (sign-flipped) key; rng[slot] packs
-// the number of splitters whose key lies below the slot (low 16 bits) and below the next slot
-// (high 16 bits).  Only splitters inside the key's slot need a comparison -- usually none or
-// one -- instead of a log2(B)-step search with bank conflicts on every step.
+// Radix-assisted lookup: rng[slot(key)] packs the number of splitters whose key lies below the
+// slot (bits 0-14), a "one-key slot" flag (bit 15) and the number below the next slot (bits
+// 16-31).  Only splitters inside the key's slot need a comparison -- usually none or one --
+// instead of a log2(B)-step search with bank conflicts on every step.
+//
+// The slot of a key is a monotone function of its sign-flipped value u above the first
+// splitter's, d = max(u - ulo, 0) (BkMap, chosen once per sort by bucket_slotmap_kernel):
+//   linear (mode 0): d >> sh, sh the smallest shift that maps the last splitter into the table:
+//                    uniform keys put ~B/SLOTS splitters in every slot;
+//   log    (mode 1): d itself below 2^M, else (bit length, the M bits after the leading one):
+//                    skewed keys (Zipf's small heavy integers) get a slot per heavy key and the
+//                    sparse tail shares wide slots.  Under the linear map they all fall in one
+//                    slot and every key binary-searches hundreds of splitters.
+// int32 keeps the fixed map (the top SLOTB bits, ulo = 0) and no one-key slots: its histogram
+// runs at the HBM rate and the extra lookup work measured +0.5 ms there at 2^30 uniform keys.
 #ifndef DSORT_BK_SLOTB
 #define DSORT_BK_SLOTB 11
 #endif
 constexpr int BK_SLOTB = DSORT_BK_SLOTB;
 constexpr int BK_SLOTS = 1 << BK_SLOTB;
 
+struct BkMap {
+    uint64_t ulo;   // flipped key of the first splitter
+    uint32_t sh;    // linear shift
+    uint32_t mode;  // 0 linear, 1 log
+    uint64_t invn;  // 2^48 / n: index -> 16-bit fraction of the input
+};
+#ifndef DSORT_BK_ONEKEY
+#define DSORT_BK_ONEKEY 1
+#endif
+// log mode: mantissa bits M, the largest with (KB - M + 1) * 2^M slots in the table
+template <typename T, int SB>
+__host__ __device__ constexpr int log_m() {
+    int m = 0;
+    while (m < 16 && (Comp<T>::KB - (m + 1) + 1) * (1 << (m + 1)) <= (1 << SB)) ++m;
+    return m;
+}
+
+template <typename T, int SB, int MODE>
+__host__ __device__ __forceinline__ uint32_t slot_mode(const BkMap &m, T key) {
+    using U = typename Comp<T>::U;
+    constexpr uint32_t NS = 1u << SB;
+    constexpr int M = log_m<T, SB>();
+    if (!Comp<T>::ADAPT) return Comp<T>::slot_of(key, SB);
+    const U u = Comp<T>::flip(key);
+    const U d = u < (U)m.ulo ? (U)0 : (U)(u - (U)m.ulo);
+    if (MODE == 0) {
+        const U q = d >> m.sh;
+        return q > (U)(NS - 1) ? NS - 1 : (uint32_t)q;
+    }
+    if (d < ((U)1 << M)) return (uint32_t)d;
+    const int e = (int)(sizeof(U) * 8) - (sizeof(U) == 8 ? __builtin_clzll((uint64_t)d) : __builtin_clz((uint32_t)d));
+    return (uint32_t)(e - M) << M | ((uint32_t)(d >> (e - 1 - M)) & ((1u << M) - 1));
+}
 template <typename T, int SB = BK_SLOTB>
-__device__ __forceinline__ void build_slots(const typename Comp<T>::C *spl, int BP, uint32_t *rng) {
-    using CT = Comp<T>;
-    constexpr int BK_SLOTB = SB, BK_SLOTS = 1 << SB;
-    for (int i = threadIdx.x; i < BK_SLOTS; i += blockDim.x) {
-        uint32_t cnt[2];
+__host__ __device__ __forceinline__ uint32_t slot_at(const BkMap &m, T key) {
+    return m.mode == 0 ? slot_mode<T, SB, 0>(m, key) : slot_mode<T, SB, 1>(m, key);
+}
+// the slots of K keys, the (workgroup-uniform) mode branch taken once
+template <typename T, int K>
+__device__ __forceinline__ void slots_at(const BkMap &m, const T (&key)[K], uint32_t (&sl)[K]) {
+    if (!Comp<T>::ADAPT || m.mode == 0) {
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            // splitters whose key lies below the start of slot i + e
-            const uint64_t su = (uint64_t)(i + e) << (CT::KB - BK_SLOTB);  // sign-flipped key
-            const typename CT::C c = i + e == BK_SLOTS ? CT::inf() : CT::slot_start(su);
-            cnt[e] = (uint32_t)bucket_of<T>(spl, BP, c);
-        }
-        rng[i] = cnt[0] | (cnt[1] << 16);
+        for (int k = 0; k < K; ++k) sl[k] = slot_mode<T, BK_SLOTB, 0>(m, key[k]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < K; ++k) sl[k] = slot_mode<T, BK_SLOTB, 1>(m, key[k]);
     }
 }
 
+// the smallest flipped key of slot i (i >= 1), or false when no key maps there or beyond
 template <typename T, int SB = BK_SLOTB>
-__device__ __forceinline__ int bucket_fast(const typename Comp<T>::C *spl, const uint32_t *rng,
+__host__ __device__ __forceinline__ bool slot_first(const BkMap &m, uint32_t i, uint64_t &u0) {
+    using U = typename Comp<T>::U;
+    constexpr int M = log_m<T, SB>();
+    constexpr int KB = Comp<T>::KB;
+    U d;
+    if (m.mode == 0) {
+        if (m.sh + SB > KB && (i >> (KB - m.sh)) != 0) return false;
+        d = (U)i << m.sh;
+    } else if (i < (1u << M)) {
+        d = (U)i;
+    } else {
+        const int e = (int)(i >> M) + M;
+        if (e > KB) return false;
+        d = (U)((1u << M) | (i & ((1u << M) - 1))) << (e - 1 - M);
+    }
+    const U umax = (U)~(U)0;
+    if (d > (U)(umax - (U)m.ulo)) return false;
+    u0 = (uint64_t)(U)((U)m.ulo + d);
+    return true;
+}
+
+template <typename T, int SB = BK_SLOTB>
+__device__ __forceinline__ void build_slots(const typename Comp<T>::C *spl, int BP, const BkMap &m,
+                                            uint32_t *rng) {
+    using CT = Comp<T>;
+    constexpr int NS = 1 << SB;
+    for (int i = threadIdx.x; i < NS; i += blockDim.x) {
+        uint32_t cnt[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            // splitters whose key lies below the start of slot i + e (slot 0 starts at -inf)
+            uint64_t u0 = 0;
+            if (i + e == 0) {
+                cnt[e] = 0;
+            } else {
+                const typename CT::C c = i + e < NS && slot_first<T, SB>(m, (uint32_t)(i + e), u0)
+                                             ? CT::slot_start(u0) : CT::inf();
+                cnt[e] = (uint32_t)bucket_of<T>(spl, BP, c);
+            }
+        }
+        // a slot whose (>= 2) splitters all hold one key K: see bucket_fast
+        const bool one = CT::ADAPT && cnt[1] >= cnt[0] + 2 && CT::key_of(spl[cnt[0]]) == CT::key_of(spl[cnt[1] - 1]);
+        rng[i] = cnt[0] | (uint32_t)one << 15 | (cnt[1] << 16);
+    }
+}
+
+// Bucket of (key, index).  In a one-key slot the copies of K may go to any bucket from the
+// first of K's splitters to the one after the last (every one of those buckets holds keys <= K
+// before it and >= K after it, and the buckets strictly inside hold only K).  The two outer
+// buckets take exactly the copies the composite order gives them (index <= the first run
+// splitter's, > the last one's), so they stay as full as a sample bucket should; the copies in
+// between are split over the inner buckets by index range, in proportion -- two splitter reads
+// and a division instead of a search over K's run (and a sub-tile's copies, adjacent in the
+// input, land together in one or two buckets).
+// Histogram and scatter use the same map and table, so they agree key for key.  (Which copy of
+// K lands where does not matter to a keys-only sort.)
+template <typename T>
+__device__ __forceinline__ int bucket_fast(const typename Comp<T>::C *spl, const uint32_t *rng, uint32_t slot,
                                            T key, const typename Comp<T>::C &c) {
-    const uint32_t r = rng[Comp<T>::slot_of(key, SB)];
-    int lo = (int)(r & 0xFFFF), hi = (int)(r >> 16);
+    const uint32_t r = rng[slot];
+    int lo = (int)(r & 0x7FFF), hi = (int)(r >> 16);
+#if DSORT_BK_ONEKEY
+    if (Comp<T>::ADAPT && (r & 0x8000)) {
+        const typename Comp<T>::C a = spl[lo], z = spl[hi - 1];
+        const T K = Comp<T>::key_of(a);
+        const uint32_t i = Comp<T>::idx_of(c), ia = Comp<T>::idx_of(a), iz = Comp<T>::idx_of(z);
+        if (key != K || i <= ia) return key <= K ? lo : hi;
+        if (i > iz) return hi;
+        // hi - lo - 1 inner buckets over the indices (ia, iz]
+        const float q = (float)(i - ia - 1) * ((float)(hi - lo - 1) / (float)(iz - ia));
+        const int j = (int)q;
+        return lo + 1 + (j < hi - lo - 2 ? j : hi - lo - 2);
+    }
+#endif
     while (lo < hi) {  // lower bound among the splitters of the slot
         const int mid = (lo + hi) >> 1;
         if (Comp<T>::lt(spl[mid], c)) lo = mid + 1;
         else hi = mid;
     }
     return lo;
+}
+
+// The slot map of a sort: linear unless the log map leaves fewer distinct splitter keys in its
+// most crowded slot (one workgroup; out = BkMap).
+template <typename T>
+__global__ void __launch_bounds__(BK_MAXB) bucket_slotmap_kernel(const typename Comp<T>::C *__restrict__ spl,
+                                                                  int B, uint64_t n, BkMap *__restrict__ out) {
+    using CT = Comp<T>;
+    using U = typename CT::U;
+    __shared__ uint32_t cnt[2][BK_SLOTS];
+    __shared__ uint32_t crowd[2];
+    const int j = threadIdx.x, nsp = B - 1;
+    for (int i = j; i < 2 * BK_SLOTS; i += blockDim.x) cnt[i / BK_SLOTS][i % BK_SLOTS] = 0;
+    if (j < 2) crowd[j] = 0;
+    const uint64_t invn = ((uint64_t)1 << 48) / (n > 0 ? n : 1);
+    BkMap mm[2] = {{0, (uint32_t)(CT::KB - BK_SLOTB), 0, invn}, {0, 0, 1, invn}};
+    if (!CT::ADAPT) {
+        if (j == 0) *out = mm[0];
+        return;
+    }
+    if (nsp >= 1) {
+        const U lo = CT::flip(CT::key_of(spl[0])), hi = CT::flip(CT::key_of(spl[nsp - 1]));
+        const U r = hi - lo;
+        const int bits = r == 0 ? 0 : (int)(sizeof(U) * 8) - (sizeof(U) == 8 ? __builtin_clzll((uint64_t)r)
+                                                                               : __builtin_clz((uint32_t)r));
+        mm[0] = BkMap{(uint64_t)lo, (uint32_t)(bits > BK_SLOTB ? bits - BK_SLOTB : 0), 0, invn};
+        mm[1] = BkMap{(uint64_t)lo, 0, 1, invn};
+    }
+    __syncthreads();
+    // count the distinct splitter keys of every slot under both maps
+    if (j < nsp && (j == 0 || CT::key_of(spl[j]) != CT::key_of(spl[j - 1]))) {
+        const T k = CT::key_of(spl[j]);
+        atomicAdd(&cnt[0][slot_at<T>(mm[0], k)], 1u);
+        atomicAdd(&cnt[1][slot_at<T>(mm[1], k)], 1u);
+    }
+    __syncthreads();
+    for (int i = j; i < 2 * BK_SLOTS; i += blockDim.x) atomicMax(&crowd[i / BK_SLOTS], cnt[i / BK_SLOTS][i % BK_SLOTS]);
+    __syncthreads();
+    if (j == 0) *out = crowd[1] < crowd[0] ? mm[1] : mm[0];
 }
 
 template <typename T>
@@ -246,26 +407,23 @@ __host__ __forceinline__ int bucket_wg_subs(uint64_t n) {
     return cap;
 }
 
-// counts[g * B + b] = keys of workgroup g's subs sub-tiles in bucket b.  The histogram has LDS to
-// spare, so its slot table can be finer than the scatter's (DSORT_BK_HSLOTB bits).
-#ifndef DSORT_BK_HSLOTB
-#define DSORT_BK_HSLOTB BK_SLOTB
-#endif
+// counts[g * B + b] = keys of workgroup g's subs sub-tiles in bucket b.  (The same slot table as
+// the scatter's: the one-key slots must agree.)
 template <typename T>
 __global__ void __launch_bounds__(BK_T) bucket_hist_kernel(const T *__restrict__ in, uint64_t n,
                                                            const typename Comp<T>::C *__restrict__ spl_g,
-                                                           int B, int BP, int subs,
-                                                           uint32_t *__restrict__ counts) {
+                                                           const BkMap *__restrict__ map, int B, int BP,
+                                                           int subs, uint32_t *__restrict__ counts) {
     using CT = Comp<T>;
     constexpr int KPT = Geo<T>::KPT, SUB = BK_T * KPT;
-    constexpr int HSB = DSORT_BK_HSLOTB;
     __shared__ typename CT::C spl[BK_MAXB];
-    __shared__ uint32_t rng[1 << HSB];
+    __shared__ uint32_t rng[BK_SLOTS];
+    const BkMap m = *map;
     __shared__ uint32_t hist[BK_MAXB];
     load_splitters<T>(spl_g, BP, spl);
     for (int b = threadIdx.x; b < B; b += BK_T) hist[b] = 0;
     __syncthreads();
-    build_slots<T, HSB>(spl, BP, rng);
+    build_slots<T>(spl, BP, m, rng);
     __syncthreads();
     const uint64_t g0 = (uint64_t)blockIdx.x * subs * SUB;
 #pragma unroll 1
@@ -277,10 +435,21 @@ __global__ void __launch_bounds__(BK_T) bucket_hist_kernel(const T *__restrict__
             const uint64_t i = b0 + (uint64_t)k * BK_T;
             key[k] = i < n ? in[i] : T(0);
         }
+        // (the mode branch outside the key loop: a slot array would cost the second workgroup)
+        if (!CT::ADAPT || m.mode == 0) {
 #pragma unroll
-        for (int k = 0; k < KPT; ++k) {
-            const uint64_t i = b0 + (uint64_t)k * BK_T;
-            if (i < n) atomicAdd(&hist[bucket_fast<T, HSB>(spl, rng, key[k], CT::make(key[k], i))], 1u);
+            for (int k = 0; k < KPT; ++k) {
+                const uint64_t i = b0 + (uint64_t)k * BK_T;
+                const uint32_t sl = slot_mode<T, BK_SLOTB, 0>(m, key[k]);
+                if (i < n) atomicAdd(&hist[bucket_fast<T>(spl, rng, sl, key[k], CT::make(key[k], i))], 1u);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < KPT; ++k) {
+                const uint64_t i = b0 + (uint64_t)k * BK_T;
+                const uint32_t sl = slot_mode<T, BK_SLOTB, 1>(m, key[k]);
+                if (i < n) atomicAdd(&hist[bucket_fast<T>(spl, rng, sl, key[k], CT::make(key[k], i))], 1u);
+            }
         }
     }
     __syncthreads();
@@ -399,7 +568,7 @@ __global__ void __launch_bounds__(BK_MAXB) bucket_offsets_kernel(const uint32_t 
 template <typename T>
 __global__ void __launch_bounds__(BK_T) bucket_scatter_kernel(const T *__restrict__ in, uint64_t n,
                                                               const typename Comp<T>::C *__restrict__ spl_g,
-                                                              int B, int BP, int subs,
+                                                              const BkMap *__restrict__ map, int B, int BP, int subs,
                                                               const uint64_t *__restrict__ offs,
                                                               T *__restrict__ out, T *__restrict__ out2) {
     using CT = Comp<T>;
@@ -420,8 +589,9 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_kernel(const T *__restric
     for (int b = threadIdx.x; b < B; b += BK_T) sgo[b] = make_uint2(0u, (uint32_t)offs[(uint64_t)blockIdx.x * B + b]);
 #endif
     load_splitters<T>(spl_g, BP, spl);
+    const BkMap m = *map;
     __syncthreads();
-    build_slots<T>(spl, BP, rng);
+    build_slots<T>(spl, BP, m, rng);
     for (int b = threadIdx.x; b < B; b += BK_T)
         bpure[b] = out2 && b > 0 && b + 1 < B && CT::key_of(spl[b - 1]) == CT::key_of(spl[b]);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -443,6 +613,8 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_kernel(const T *__restric
         uint32_t slot[KPT];
 #pragma unroll
         for (int k = 0; k < KPT; ++k) key[k] = nxt[k];
+        uint32_t sl[KPT];
+        slots_at<T, KPT>(m, key, sl);
         if (sub + 1 < subs) {
 #pragma unroll
             for (int k = 0; k < KPT; ++k) {
@@ -455,7 +627,7 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_kernel(const T *__restric
             const uint64_t i = s0 + threadIdx.x + (uint64_t)k * BK_T;
             bk[k] = -1;
             if (i < n) {
-                bk[k] = bucket_fast<T>(spl, rng, key[k], CT::make(key[k], i));
+                bk[k] = bucket_fast<T>(spl, rng, sl[k], key[k], CT::make(key[k], i));
                 slot[k] = atomicAdd(&hist[bk[k]], 1u);
             }
         }
@@ -562,7 +734,7 @@ constexpr int BK_LK = 16;      // int32 keys per 64-byte line
 constexpr int BK_MAXC = 3072;  // lines per sub-tile at most: (SUB + 30 * BK_MAXB) / 16
 static __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const int32_t *__restrict__ in, uint64_t n,
                                                                     const int64_t *__restrict__ spl_g,
-                                                                    int B, int BP, int subs,
+                                                                    const BkMap *__restrict__ map, int B, int BP, int subs,
                                                                     const uint64_t *__restrict__ offs,
                                                                     int32_t *__restrict__ out,
                                                                     int32_t *__restrict__ out2) {
@@ -607,8 +779,9 @@ static __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const
         gb = o - ph;  // (mod 2^32) the first line of the stream starts ph entries before o
     }
     load_splitters<int32_t>(spl_g, BP, spl);
+    const BkMap m = *map;
     __syncthreads();
-    build_slots<int32_t>(spl, BP, rng);
+    build_slots<int32_t>(spl, BP, m, rng);
     const uint64_t g0 = (uint64_t)g * subs * SUB;
     int32_t nxt[KPT];
 #pragma unroll
@@ -628,6 +801,8 @@ static __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const
         uint32_t slot[KPT];
 #pragma unroll
         for (int k = 0; k < KPT; ++k) key[k] = nxt[k];
+        uint32_t sl[KPT];
+        slots_at<int32_t, KPT>(m, key, sl);
         if (!last) {
 #pragma unroll
             for (int k = 0; k < KPT; ++k) {
@@ -640,7 +815,7 @@ static __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const
             const uint64_t i = s0 + tb + (uint64_t)k * BK_T;
             bk[k] = -1;
             if (i < n) {
-                bk[k] = bucket_fast<int32_t>(spl, rng, key[k], CT::make(key[k], i));
+                bk[k] = bucket_fast<int32_t>(spl, rng, sl[k], key[k], CT::make(key[k], i));
                 slot[k] = atomicAdd(&hm.hist[bk[k]], 1u);
             }
         }

@@ -1711,7 +1711,7 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
     const size_t o_smp = take((size_t)S * (sizeof(T) == 8 ? 24 : sizeof(C))), o_spl = take((size_t)BP * sizeof(C)),
                  o_cnt = take((size_t)G * B * 4), o_part = take((size_t)nchunk * B * 8),
                  o_offs = take((size_t)G * B * 8), o_bst = take((size_t)(B + 1) * 8),
-                 o_tt = take((size_t)tmax * sizeof(TileRef)), o_nt = take(4);
+                 o_tt = take((size_t)tmax * sizeof(TileRef)), o_nt = take(4), o_map = take(sizeof(BkMap));
     int rc = ensure(ctx, &ctx->bucket, &ctx->bucket_bytes, off, "bucket partition");
     if (rc) return rc;
     char *a = static_cast<char *>(ctx->bucket);
@@ -1723,6 +1723,7 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
     uint64_t *bst = reinterpret_cast<uint64_t *>(a + o_bst);
     TileRef *tt = reinterpret_cast<TileRef *>(a + o_tt);
     uint32_t *ntl = reinterpret_cast<uint32_t *>(a + o_nt);
+    BkMap *map = reinterpret_cast<BkMap *>(a + o_map);
     rc = ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, n * sizeof(T), "sort scratch");
     if (rc) return rc;
     T *scratch = static_cast<T *>(ctx->scratch);
@@ -1775,8 +1776,10 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
         hipLaunchKernelGGL(pair_splitter_kernel, dim3(1), dim3(BK_MAXB), 0, s, pcmp, pk, (uint64_t)n, S, B, BP, os,
                            spl);
     }
-    // 2. histograms, their scan, the scatter
-    hipLaunchKernelGGL(bucket_hist_kernel<T>, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, B, BP, subs, cnt);
+    // 2. the lookups' slot map, histograms, their scan, the scatter
+    hipLaunchKernelGGL(bucket_slotmap_kernel<T>, dim3(1), dim3(BK_MAXB), 0, s, spl, B, (uint64_t)n, map);
+    hipLaunchKernelGGL(bucket_hist_kernel<T>, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, map, B, BP,
+                       subs, cnt);
     hipLaunchKernelGGL(bucket_colsum_kernel, dim3((unsigned)nchunk), dim3(BK_MAXB), 0, s, cnt, (uint32_t)G, B, part);
     hipLaunchKernelGGL(bucket_scan_kernel, dim3(1), dim3(BK_MAXB), 0, s, part, (uint32_t)nchunk, B,
                        (uint32_t)TILE, (uint32_t)ALIGN, bst, tt, ntl);
@@ -1796,10 +1799,10 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
     T *direct = sub_keys<T>(ctx) && (const void *)d_in != (const void *)d_keys && n < (1ull << 31) ? d_keys : nullptr;
     if constexpr (std::is_same<T, int32_t>::value && DSORT_BK_LINES) {
         hipLaunchKernelGGL(bucket_scatter_lines_kernel, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl,
-                           B, BP, subs, offs, part_out, direct);
+                           map, B, BP, subs, offs, part_out, direct);
     } else {
-        hipLaunchKernelGGL(bucket_scatter_kernel<T>, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, B,
-                           BP, subs, offs, part_out, direct);
+        hipLaunchKernelGGL(bucket_scatter_kernel<T>, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, map,
+                           B, BP, subs, offs, part_out, direct);
     }
     DSORT_HIP(ctx, hipGetLastError());
     DSORT_HIP(ctx, hipEventSynchronize(ctx->bucket_ev));

@@ -266,3 +266,24 @@ def test_pure_buckets_heavy_keys(gpu_ctx, dtype, mode, n):
     opts = {"local": dict(), "scatter": dict(sub_gather=0)}[mode]
     with gpu_ctx.options(buckets=256, **opts):
         assert np.array_equal(_sort(gpu_ctx, a, False), np.sort(a))
+
+
+@pytest.mark.parametrize("dtype", [np.int32, np.int64])
+@pytest.mark.parametrize("mode", ["local", "scatter"])
+@pytest.mark.parametrize("n", [1 << 22, (1 << 22) + 999])
+def test_one_key_slots_skewed(gpu_ctx, dtype, mode, n):
+    """Skewed small keys (a Zipf head) with the type's extremes: the int64 lookups switch to the
+    log slot map, every heavy key gets a one-key slot whose copies are split over its run of
+    buckets by index (the outer two exactly as the composite order), and the tail and the
+    extremes share wide slots (dsort_bucket.h BkMap, bucket_fast)."""
+    rng = np.random.default_rng(n + (11 if dtype == np.int64 else 0))
+    info = np.iinfo(dtype)
+    a = np.minimum(rng.zipf(1.3, n), 1 << 20).astype(dtype)
+    r = rng.random(n)
+    a[r < 0.01] = info.max
+    a[(r >= 0.01) & (r < 0.02)] = info.min
+    a[(r >= 0.02) & (r < 0.05)] = rng.integers(info.min, info.max, int(((r >= 0.02) & (r < 0.05)).sum()),
+                                               dtype=dtype)
+    opts = {"local": dict(), "scatter": dict(sub_gather=0)}[mode]
+    with gpu_ctx.options(buckets=512, **opts):
+        assert np.array_equal(_sort(gpu_ctx, a, False), np.sort(a))
