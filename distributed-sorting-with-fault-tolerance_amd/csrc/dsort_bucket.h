@@ -146,6 +146,9 @@ struct BkMap {
 #ifndef DSORT_BK_ONEKEY
 #define DSORT_BK_ONEKEY 1
 #endif
+#ifndef DSORT_BK_RCP
+#define DSORT_BK_RCP 1
+#endif
 // log mode: mantissa bits M, the largest with (KB - M + 1) * 2^M slots in the table
 template <typename T, int SB>
 __host__ __device__ constexpr int log_m() {
@@ -257,7 +260,12 @@ __device__ __forceinline__ int bucket_fast(const typename Comp<T>::C *spl, const
         if (key != K || i <= ia) return key <= K ? lo : hi;
         if (i > iz) return hi;
         // hi - lo - 1 inner buckets over the indices (ia, iz]
+#if DSORT_BK_RCP
+        // (the hardware reciprocal: the same instruction in the histogram and the scatter)
+        const float q = (float)(i - ia - 1) * ((float)(hi - lo - 1) * __builtin_amdgcn_rcpf((float)(iz - ia)));
+#else
         const float q = (float)(i - ia - 1) * ((float)(hi - lo - 1) / (float)(iz - ia));
+#endif
         const int j = (int)q;
         return lo + 1 + (j < hi - lo - 2 ? j : hi - lo - 2);
     }
