@@ -66,10 +66,12 @@ def parse(argv=None):
     ap.add_argument("--kill-rank", type=int, default=None,
                     help="BASELINE config C5: fault-tolerance run (launch WITHOUT torchrun: the master "
                          "spawns one worker per GPU); this worker dies mid-sort")
-    ap.add_argument("--kill-after-pass", type=int, default=1,
-                    help="the dying worker SIGKILLs itself after this merge pass of its local sort")
+    ap.add_argument("--kill-after-stage", "--kill-after-pass", dest="kill_after_stage", type=int, default=0,
+                    help="the dying worker SIGKILLs itself after this stage of its local sort "
+                         "(DSORT_OPT_KILL_AFTER_STAGE; >= 2^25 keys per worker: 0 first-level partition, "
+                         "1 second-level partition, 2 tile sort); an unreachable stage is an error")
     ap.add_argument("--kill-stage", choices=["sort", "exchange"], default="sort",
-                    help="C5: die in the local sort (after --kill-after-pass) or inside the key exchange")
+                    help="C5: die in the local sort (after --kill-after-stage) or inside the key exchange")
     ap.add_argument("--reassign", choices=["first-live", "next-live"], default="first-live")
     ap.add_argument("--codec", action="store_true",
                     help="time the GPU text codec (output.txt format + %%d parse) on --keys sorted keys")
@@ -624,7 +626,7 @@ def report_multi(args, world, elapsed, per_rank, w):
 def run_fault(args):
     """BASELINE config C5 through the C master (dsort_master --mode samplesort, server.c's role,
     driven by ftsort.fault_run): a fault-free run, then a run in which worker `--kill-rank` dies in
-    its local sort (after merge pass --kill-after-pass) or inside the key exchange; the master
+    its local sort (after stage --kill-after-stage) or inside the key exchange; the master
     sees it (socket EOF / exit / heartbeat), reassigns its chunk from the pinned replica by the
     reference's rule, and the survivors abort the communicator, rebuild it and finish."""
     import ftsort
@@ -633,7 +635,7 @@ def run_fault(args):
     share = args.gpus > ndev  # one GPU box: the workers share it and exchange through the master
     devices = "share" if share else list(range(args.gpus))
     transport = "relay" if share else "rccl"
-    r = ftsort.fault_run(args.gpus, args.keys, args.kill_rank, args.kill_after_pass,
+    r = ftsort.fault_run(args.gpus, args.keys, args.kill_rank, args.kill_after_stage,
                          "i32" if args.dtype == "i32" else "i64", args.dist, transport, devices, args.reassign,
                          stage=args.kill_stage)
     if not r["ok"]:

@@ -347,12 +347,9 @@ static double now_ms() {
     return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
 }
 
-// The communicator mutex: held by a running exchange; dsort_comm_abort from another thread finds
-// it taken and only raises ctx->abort_req (see dsort.h).
-static std::mutex &comm_mutex(dsort_ctx *ctx) {
-    static std::mutex table[64];
-    return table[(reinterpret_cast<uintptr_t>(ctx) >> 6) & 63];
-}
+// The communicator mutex of a context: held by a running exchange or communicator set-up;
+// dsort_comm_abort from another thread finds it taken and only raises ctx->abort_req (dsort.h).
+static std::mutex &comm_mutex(dsort_ctx *ctx) { return ctx->comm_mu; }
 
 static void abort_comm_locked(dsort_ctx *ctx) {
     if (ctx->comm) ncclCommAbort(ctx->comm);
@@ -727,7 +724,7 @@ int dsort_set_option(dsort_ctx *ctx, int option, int64_t v) {
             o.max_logf = v;
             return DSORT_OK;
         case DSORT_OPT_KILL_AFTER_PASS:
-            if (v < -1) return set_err(ctx, DSORT_EINVAL, "DSORT_OPT_KILL_AFTER_PASS: -1 or a pass index");
+            if (v < -1) return set_err(ctx, DSORT_EINVAL, "DSORT_OPT_KILL_AFTER_STAGE: -1 or a stage index");
             o.kill_after_pass = v;
             return DSORT_OK;
         case DSORT_OPT_KILL_IN_EXCHANGE:
@@ -797,6 +794,9 @@ int dsort_get_stats(const dsort_ctx *cctx, dsort_stats *out) {
     out->merge_ms = el(1, 2);
     out->tile_sort_kernel_ms = el(7, 8);
     out->partition_ms = el(0, 7);
+    out->bucket_hist_ms = el(9, 10);
+    out->bucket_scatter_ms = el(11, 12);
+    out->sub_partition_ms = el(13, 14);
     if (ctx->ev_mask & 16u) {
         out->exchange_ms = el(2, 3);
         out->final_merge_ms = el(3, 4);
@@ -812,6 +812,13 @@ int dsort_synchronize(dsort_ctx *ctx) {
     if (!ctx) return DSORT_EINVAL;
     DSORT_HIP(ctx, hipStreamSynchronize(ctx->last_stream));
     DSORT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return DSORT_OK;
+}
+
+int dsort_sort_stages(const dsort_ctx *ctx, size_t n, int key_bytes, int *stages) {
+    if (!stages || (key_bytes != 4 && key_bytes != 8)) return DSORT_EINVAL;
+    static const dsort_opts defaults{};
+    *stages = sort_stages(ctx ? ctx->opt : defaults, n, key_bytes);
     return DSORT_OK;
 }
 
@@ -932,11 +939,17 @@ int dsort_comm_destroy(dsort_ctx *ctx) {
     ctx->has_transport = false;
     if (ctx->comm) {
         (void)hipStreamSynchronize(ctx->stream);
-        // non-blocking communicator: finalize, wait for it, then destroy
+        // non-blocking communicator: finalize, wait for it (never longer than the exchange
+        // deadline, 10 s without one, or an abort request: a peer that died after its last
+        // collective must not hold this rank in shutdown), then destroy -- else abort
+        const double limit = ctx->opt.comm_timeout_ms > 0 ? (double)ctx->opt.comm_timeout_ms : 10000.0;
+        const double deadline = now_ms() + limit;
         ncclResult_t r = ncclCommFinalize(ctx->comm);
         while (r == ncclInProgress) {
             ncclCommGetAsyncError(ctx->comm, &r);
-            if (r == ncclInProgress) usleep(50);
+            if (r != ncclInProgress) break;
+            if (ctx->abort_req.load() || now_ms() > deadline) break;
+            usleep(50);
         }
         if (r == ncclSuccess) ncclCommDestroy(ctx->comm);
         else ncclCommAbort(ctx->comm);

@@ -7,6 +7,7 @@
 #include <stddef.h>
 
 #include <atomic>
+#include <mutex>
 #include <string>
 
 #include "dsort.h"
@@ -51,7 +52,7 @@ struct dsort_opts {
     int64_t bucket_keys = 1 << 20;  // DSORT_OPT_BUCKET_KEYS
     int64_t bucket_os = 256;        // DSORT_OPT_BUCKET_OVERSAMPLE
     int64_t max_logf = -1;          // DSORT_OPT_MAX_FANIN_LOG2: -1 = per key type default
-    int64_t kill_after_pass = -1;   // DSORT_OPT_KILL_AFTER_PASS
+    int64_t kill_after_pass = -1;   // DSORT_OPT_KILL_AFTER_STAGE (= DSORT_OPT_KILL_AFTER_PASS)
     int64_t kill_in_exchange = -1;  // DSORT_OPT_KILL_IN_EXCHANGE
     int64_t comm_timeout_ms = 0;    // DSORT_OPT_COMM_TIMEOUT_MS
     int64_t sub_keys = -1;          // DSORT_OPT_SUB_KEYS: -1 = TILE / 8, 0 = no second level
@@ -64,7 +65,9 @@ struct dsort_ctx {
     dsort_opts opt;
     int nested = 0;  // > 0 inside a sort the library runs for itself (the splitter-sample sort):
                      // such a sort never buckets and never fires the fault injection
+    int stages_done = 0;            // kill points the running (outermost) sort has passed
     std::atomic<int> abort_req{0};  // dsort_comm_abort from another thread during an exchange
+    std::mutex comm_mu;             // held by a running exchange / communicator set-up (dsort.h)
     int device = 0;
     hipStream_t stream = nullptr;
     std::string err;
@@ -124,9 +127,11 @@ struct dsort_ctx {
     void *small_host = nullptr;  // pinned
     size_t small_host_bytes = 0;
     // stage timing
-    hipEvent_t ev[9] = {};  // 0 start, 1 tile sort done, 2 local sort done, 3 exchange done,
-                            // 4 final merge done, 5/6 around the key all-to-all, 7/8 around the
-                            // tile sort kernel
+    hipEvent_t ev[15] = {};  // 0 start, 1 tile sort done, 2 local sort done, 3 exchange done,
+                             // 4 final merge done, 5/6 around the key all-to-all, 7/8 around the
+                             // tile sort kernel, 9/10 around the first-level histogram, 11/12
+                             // around the first-level scatter, 13/14 around the second-level
+                             // partition
     unsigned ev_mask = 0;             // events recorded by the last call (bit i = ev[i])
     hipStream_t last_stream = nullptr;  // stream of the last asynchronous call
     static constexpr int kMaxKev = 128;  // per-launch events of the merge kernel (2 per pass)
@@ -144,30 +149,29 @@ hipStream_t pick_stream(dsort_ctx *ctx, void *stream);
 int hip_err(dsort_ctx *ctx, hipError_t e, const char *what);
 int ensure(dsort_ctx *ctx, void **buf, size_t *have, size_t need, const char *what);
 
-// Launchers (dsort_sort.hip).  All asynchronous on `s`.
-// Sorts d_in[0..n) into d_keys (d_in may equal d_keys).
+// The sort and the k-way merge (dsort_wave.hip), both key widths.  All asynchronous on `s`.
+// sort_device sorts d_in[0..n) into d_keys (d_in may equal d_keys).  merge_device with
+// keep_stats leaves the statistics and per-launch events of the preceding local sort alone (the
+// sample sort's final merge).
 template <typename T>
 int sort_device(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipStream_t s, bool timed);
 template <typename T>
 int merge_device(dsort_ctx *ctx, const T *d_in, const size_t *lens, int k, T *d_out,
                  hipStream_t s, bool keep_stats = false);
-// The wave-register bitonic kernels (dsort_wave.hip); sort_device/merge_device route both key
-// widths here.  wave_merge_* with keep_stats leaves the statistics and per-launch events of
-// the preceding local sort alone (the sample sort's final merge).
-int wave_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys, size_t n, hipStream_t s,
-                  bool timed);
-int wave_merge_i32(dsort_ctx *ctx, const int32_t *d_in, const size_t *lens, int k, int32_t *d_out,
-                   hipStream_t s, bool keep_stats = false);
-int wave_sort_i64(dsort_ctx *ctx, const int64_t *d_in, int64_t *d_keys, size_t n, hipStream_t s,
-                  bool timed);
-int wave_merge_i64(dsort_ctx *ctx, const int64_t *d_in, const size_t *lens, int k, int64_t *d_out,
-                   hipStream_t s, bool keep_stats = false);
 // Fault injection for the fault-tolerance tests and bench (BASELINE config C5): with
-// DSORT_OPT_KILL_AFTER_PASS = k the process SIGKILLs itself right after merge pass k of a local
-// (non-nested) sort has finished on the GPU -- a worker dying mid-sort.  No effect otherwise.
-void fault_point(dsort_ctx *ctx, hipStream_t s, int pass_done);
+// DSORT_OPT_KILL_AFTER_STAGE = k the process SIGKILLs itself right after stage k of a local
+// (non-nested) sort has finished on the GPU -- a worker dying mid-sort.  The stages of a sort, in
+// order (sort_stages counts them):
+//   bucketed sort (>= 2^25 keys)  0 first-level partition, 1 second-level partition, 2 tile sort
+//     (with DSORT_OPT_SUB_KEYS = 0: 0 partition, 1 tile sort, 2 + p merge pass p)
+//   merge path                    0 tile sort, 1 + p merge pass p
+// A kill stage the sort never reaches makes the sort return DSORT_EINVAL (sort_device).
+void fault_point(dsort_ctx *ctx, hipStream_t s, int stage);
+// Kill points of a top-level sort of n keys of key_bytes bytes under `opt` (the bucketed path
+// without the second level has data-dependent merge passes: the guaranteed minimum).
+int sort_stages(const dsort_opts &opt, uint64_t n, int key_bytes);
 // Largest log2 fan-in of one merge pass: the option, else the key type's default.
-int max_logf(const dsort_ctx *ctx, int type_default, int type_cap);
+int max_logf(const dsort_opts &opt, int type_default, int type_cap);
 
 }  // namespace dsort
 

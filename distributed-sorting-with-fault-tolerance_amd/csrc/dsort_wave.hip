@@ -35,6 +35,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <csignal>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -1318,22 +1319,27 @@ static int ceil_log2(uint64_t x) {
 // log2(F) of each pass: as few passes as the cap allows (default F <= 16), the bits spread
 // evenly over them.
 template <typename T>
-static std::vector<int> plan_passes(const dsort_ctx *ctx, uint64_t runs) {
+static std::vector<int> plan_passes(const dsort_opts &opt, uint64_t runs) {
     std::vector<int> out;
     const int bits = ceil_log2(runs);
     if (bits == 0) return out;
-    const int cap = max_logf(ctx, 4, WG<T>::MAXLOGF);
+    const int cap = max_logf(opt, 4, WG<T>::MAXLOGF);
     const int P = (bits + cap - 1) / cap;
     for (int p = 0; p < P; ++p) out.push_back(bits / P + (p < bits % P ? 1 : 0));
     return out;
 }
 
-// Events 7 / 8 around the tile sort kernel (dsort_stats.tile_sort_kernel_ms, partition_ms).
-static int tile_sort_event(dsort_ctx *ctx, hipStream_t s, bool timed, int which) {
+// Stage event i of a timed sort (dsort_internal.h: ctx->ev): 7 / 8 around the tile sort kernel
+// (dsort_stats.tile_sort_kernel_ms, partition_ms), 9 / 10 the first-level histogram, 11 / 12 the
+// first-level scatter, 13 / 14 the second-level partition.
+static int stage_event(dsort_ctx *ctx, hipStream_t s, bool timed, int i) {
     if (!timed || !ctx->ev_ok) return DSORT_OK;
-    DSORT_HIP(ctx, hipEventRecord(ctx->ev[7 + which], s));
-    ctx->ev_mask |= 1u << (7 + which);
+    DSORT_HIP(ctx, hipEventRecord(ctx->ev[i], s));
+    ctx->ev_mask |= 1u << i;
     return DSORT_OK;
+}
+static int tile_sort_event(dsort_ctx *ctx, hipStream_t s, bool timed, int which) {
+    return stage_event(ctx, s, timed, 7 + which);
 }
 
 // The tile sort of `grid` tiles (an upper bound when the count lives on the device): the bin
@@ -1417,17 +1423,17 @@ static int launch_pass_w(dsort_ctx *ctx, const T *src, T *dst, const PassDesc &p
 // tiles (7 merge levels: F = 16, then F = 8), and the buckets of <= 64 runs take F = 8 twice
 // (per-bucket fan-in, below).  int64: 1024 buckets of about 128 8K-key tiles.  A nested sort (the
 // splitter samples) never buckets.
-static int bucket_count(const dsort_ctx *ctx, uint64_t n) {
-    if (ctx->nested) return 0;
-    const int64_t forced = ctx->opt.buckets;
+static int bucket_count(const dsort_opts &opt, uint64_t n) {
+    const int64_t forced = opt.buckets;
     if (forced == 0) return 0;
-    const uint64_t tk = ctx->opt.bucket_keys > 0 ? (uint64_t)ctx->opt.bucket_keys : (1ull << 20);
+    const uint64_t tk = opt.bucket_keys > 0 ? (uint64_t)opt.bucket_keys : (1ull << 20);
     uint64_t B = forced > 0 ? (uint64_t)forced : ceil_div(n, tk);
     if (forced < 0 && n < (1ull << 25)) return 0;
     if (n >= (1ull << 32)) return 0;  // 32-bit bucket positions in the scatter
     if (B > (uint64_t)bk::BK_MAXB) B = bk::BK_MAXB;
     return B >= 2 ? (int)B : 0;
 }
+static int bucket_count(const dsort_ctx *ctx, uint64_t n) { return ctx->nested ? 0 : bucket_count(ctx->opt, n); }
 
 // Samples per bucket for the int32 splitters (sorted on the GPU): the relative spread of the
 // bucket sizes is about 1/sqrt(os) (DSORT_OPT_BUCKET_OVERSAMPLE).
@@ -1451,10 +1457,12 @@ static int wave_merge(dsort_ctx *ctx, const T *d_in, const size_t *lens, int k, 
 // ---- second partition level (dsort_sub.h) -------------------------------------------------
 // Nominal keys per sub-bucket: TILE / 8 unless DSORT_OPT_SUB_KEYS says otherwise (0 = off).
 template <typename T>
-static uint64_t sub_keys(const dsort_ctx *ctx) {
-    const int64_t v = ctx->opt.sub_keys;
+static uint64_t sub_keys(const dsort_opts &opt) {
+    const int64_t v = opt.sub_keys;
     return v < 0 ? (uint64_t)TILE_OF<T> / 8 : (uint64_t)v;
 }
+template <typename T>
+static uint64_t sub_keys(const dsort_ctx *ctx) { return sub_keys<T>(ctx->opt); }
 
 // Runs of an oversized sub-bucket as the packer cut it (sb_scan_kernel): the room of the first
 // tile, then whole tiles.
@@ -1604,9 +1612,11 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
     if (local) {
         // 2. every chunk partitioned in place (cnt = the prefix tables), sub-bucket starts, tiles
         if (nch) {
+            if ((rc = stage_event(ctx, s, timed, 13))) return rc;
             hipLaunchKernelGGL(sb_local_kernel<T>, dim3((unsigned)nch), dim3(SB_LT), 0, s, src, dch, dbi, SS, spl, rng,
                                sfn, cnt);
             DSORT_HIP(ctx, hipGetLastError());
+            if ((rc = stage_event(ctx, s, timed, 14))) return rc;
         }
         hipLaunchKernelGGL(sb_scan_kernel<true>, dim3((unsigned)B), dim3(SB_MAXS), 0, s, dbi, SS, cnt, nullptr, TILE, 1,
                            0u, tt, num, nullptr, num + 1);
@@ -1619,6 +1629,7 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         const uint32_t ntiles = hn[0], novf = hn[1];
         if (novf) return sub_sort<T>(ctx, src, d_keys, n, hb, B, m, s, timed, false, pure, pure_done);
         if (ntiles > tmax) return set_err(ctx, DSORT_EHIP, "sub-bucket packing overflow");
+        fault_point(ctx, s, 1);  // second-level partition done
         ctx->stats.merge_passes = 0;
         // 3. tile sort: gathered from the chunks into d_keys
         if (ntiles) {
@@ -1631,11 +1642,12 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
             DSORT_HIP(ctx, hipEventRecord(ctx->ev[2], s));
             ctx->ev_mask |= 6u;
         }
-        fault_point(ctx, s, 0);  // the tile sort is the last stage: it counts as pass 0
+        fault_point(ctx, s, 2);  // tile sort done
         return DSORT_OK;
     }
     // 2. histograms, sub-bucket starts, tiles
     if (nch) {
+        if ((rc = stage_event(ctx, s, timed, 13))) return rc;
         hipLaunchKernelGGL(sb_hist_kernel<T>, dim3((unsigned)nch), dim3(SB_T), 0, s, src, dch, dbi, SS, spl, rng,
                            sfn, cnt);
         DSORT_HIP(ctx, hipGetLastError());
@@ -1650,10 +1662,12 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         hipLaunchKernelGGL(sb_scatter_kernel<T>, dim3((unsigned)nch), dim3(SB_T), 0, s, src, d_keys, dch,
                            (uint32_t)nch, dbi, SS, spl, rng, sfn, offs);
         DSORT_HIP(ctx, hipGetLastError());
+        if ((rc = stage_event(ctx, s, timed, 14))) return rc;
     }
     DSORT_HIP(ctx, hipEventSynchronize(ctx->sub_ev));
     const uint32_t ntiles = hn[0], novf = hn[1];
     if (ntiles > tmax || novf > nsubs) return set_err(ctx, DSORT_EHIP, "sub-bucket packing overflow");
+    fault_point(ctx, s, 1);  // second-level partition done
     ctx->stats.merge_passes = 0;
     if (ntiles) {
         rc = tile_sort<T, false>(ctx, d_keys, d_keys, n, static_cast<const uint4 *>(tt), num, Gather{}, ntiles, s,
@@ -1664,7 +1678,7 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[1], s));
         ctx->ev_mask |= 2u;
     }
-    fault_point(ctx, s, 0);  // the tile sort is the last stage: it counts as pass 0
+    fault_point(ctx, s, 2);  // tile sort done (the oversized sub-buckets' merges follow)
     // 4. oversized sub-buckets: their tile-sorted pieces merged (src is free scratch now)
     if (novf) {
         std::vector<Ovf> ov(novf);
@@ -1778,8 +1792,10 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
     }
     // 2. the lookups' slot map, histograms, their scan, the scatter
     hipLaunchKernelGGL(bucket_slotmap_kernel<T>, dim3(1), dim3(BK_MAXB), 0, s, spl, B, (uint64_t)n, map);
+    if ((rc = stage_event(ctx, s, timed, 9))) return rc;
     hipLaunchKernelGGL(bucket_hist_kernel<T>, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, map, B, BP,
                        subs, cnt);
+    if ((rc = stage_event(ctx, s, timed, 10))) return rc;
     hipLaunchKernelGGL(bucket_colsum_kernel, dim3((unsigned)nchunk), dim3(BK_MAXB), 0, s, cnt, (uint32_t)G, B, part);
     hipLaunchKernelGGL(bucket_scan_kernel, dim3(1), dim3(BK_MAXB), 0, s, part, (uint32_t)nchunk, B,
                        (uint32_t)TILE, (uint32_t)ALIGN, bst, tt, ntl);
@@ -1797,6 +1813,7 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
     // Pure buckets (one key, see below) go straight to d_keys, in their final places, when the
     // second level runs (it skips them) and d_keys is not the input the scatter still reads.
     T *direct = sub_keys<T>(ctx) && (const void *)d_in != (const void *)d_keys && n < (1ull << 31) ? d_keys : nullptr;
+    if ((rc = stage_event(ctx, s, timed, 11))) return rc;
     if constexpr (std::is_same<T, int32_t>::value && DSORT_BK_LINES) {
         hipLaunchKernelGGL(bucket_scatter_lines_kernel, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl,
                            map, B, BP, subs, offs, part_out, direct);
@@ -1805,6 +1822,8 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
                            B, BP, subs, offs, part_out, direct);
     }
     DSORT_HIP(ctx, hipGetLastError());
+    if ((rc = stage_event(ctx, s, timed, 12))) return rc;
+    fault_point(ctx, s, 0);  // first-level partition done
     DSORT_HIP(ctx, hipEventSynchronize(ctx->bucket_ev));
     if (hb[B] != n) return set_err(ctx, DSORT_EHIP, "bucket partition lost keys");
     if (const uint64_t m = sub_keys<T>(ctx)) {
@@ -1829,7 +1848,7 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
         for (uint64_t o = h; o < len; o += TILE) runs[b].push_back(len - o < (uint64_t)TILE ? len - o : TILE);
         maxruns = runs[b].size() > maxruns ? runs[b].size() : maxruns;
     }
-    const std::vector<int> pbits = plan_passes<T>(ctx, maxruns);
+    const std::vector<int> pbits = plan_passes<T>(ctx->opt, maxruns);
     const int passes = (int)pbits.size();
     ctx->stats.merge_passes = passes;
     T *bufs[2] = {d_keys, scratch};
@@ -1842,6 +1861,7 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[1], s));
         ctx->ev_mask |= 2u;
     }
+    fault_point(ctx, s, 1);  // tile sort done
     // 4. group tables of every pass (one staging buffer, one copy).  Every bucket gets its own
     // fan-in per pass: the passes after the first keep the global plan's fan-in and the first
     // takes only the levels the bucket still needs (a bucket of <= 64 runs merges F = 8 twice
@@ -1943,7 +1963,7 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
             if (rc) return rc;
             if (q + 1 == plan.size() || plan_pass[q + 1] != plan_pass[q]) {  // pass complete
                 cur ^= 1;
-                fault_point(ctx, s, plan_pass[q]);
+                fault_point(ctx, s, 2 + plan_pass[q]);
             }
         }
     }
@@ -1971,7 +1991,7 @@ static int wave_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipStre
     }
     if (const int B = bucket_count(ctx, n)) return bucket_sort<T>(ctx, d_in, d_keys, n, s, timed, B);
     const uint64_t tiles = ceil_div(n, TILE);
-    const std::vector<int> plan = plan_passes<T>(ctx, tiles);
+    const std::vector<int> plan = plan_passes<T>(ctx->opt, tiles);
     const int passes = (int)plan.size();
     ctx->stats.merge_passes = passes;
     T *scratch = nullptr;
@@ -1997,6 +2017,7 @@ static int wave_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipStre
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[1], s));
         ctx->ev_mask |= 2u;
     }
+    fault_point(ctx, s, 0);  // tile sort done
     constexpr uint64_t MTN = MTNOM_OF<T>;
     uint64_t Rr = TILE;
     for (int p = 0; p < passes; ++p) {
@@ -2009,7 +2030,7 @@ static int wave_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipStre
         if (rc) return rc;
         Rr <<= plan[p];
         cur ^= 1;
-        fault_point(ctx, s, p);
+        fault_point(ctx, s, 1 + p);  // merge pass p done
     }
     if (timed && ctx->ev_ok) {
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[2], s));
@@ -2123,19 +2144,67 @@ extern "C" int dsort_debug_bkstamps(void *host, size_t bytes) {
 }
 #endif
 
-int wave_sort_i32(dsort_ctx *ctx, const int32_t *d_in, int32_t *d_keys, size_t n, hipStream_t s, bool timed) {
-    return wv::wave_sort<int32_t>(ctx, d_in, d_keys, n, s, timed);
+// ------------------------------------------------------------------------------------------
+// Entry points of the worker sort and the master merge (dsort_internal.h).
+// Replace merge_sort()/merge() (reference client.c:140-173) and the merge loop of merge_chunks()
+// (server.c:481-515).  Same result: the input multiset in ascending signed order; equal keys
+// from different runs are emitted lower run first, like the reference's `<=` (client.c:152) and
+// lowest-index-wins argmin (server.c:504) -- unobservable for keys-only data.
+// ------------------------------------------------------------------------------------------
+int max_logf(const dsort_opts &opt, int type_default, int type_cap) {
+    const int64_t o = opt.max_logf;
+    const int x = o < 0 ? type_default : (int)o;
+    return x < 1 ? 1 : (x > type_cap ? type_cap : x);
 }
-int wave_sort_i64(dsort_ctx *ctx, const int64_t *d_in, int64_t *d_keys, size_t n, hipStream_t s, bool timed) {
-    return wv::wave_sort<int64_t>(ctx, d_in, d_keys, n, s, timed);
+
+void fault_point(dsort_ctx *ctx, hipStream_t s, int stage) {
+    if (ctx->nested) return;
+    if (ctx->opt.kill_after_pass == stage) {
+        (void)hipStreamSynchronize(s);  // the stage has finished on the GPU: the worker dies after it
+        raise(SIGKILL);
+    }
+    if (stage + 1 > ctx->stages_done) ctx->stages_done = stage + 1;
 }
-int wave_merge_i32(dsort_ctx *ctx, const int32_t *d_in, const size_t *lens, int k, int32_t *d_out, hipStream_t s,
-                   bool keep_stats) {
-    return wv::wave_merge<int32_t>(ctx, d_in, lens, k, d_out, s, keep_stats);
+
+int sort_stages(const dsort_opts &opt, uint64_t n, int key_bytes) {
+    if (n < 2) return 0;
+    const bool w8 = key_bytes == 8;
+    if (wv::bucket_count(opt, n)) {
+        const uint64_t m = w8 ? wv::sub_keys<int64_t>(opt) : wv::sub_keys<int32_t>(opt);
+        return m ? 3 : 2;
+    }
+    const uint64_t tile = w8 ? wv::TILE_OF<int64_t> : wv::TILE_OF<int32_t>;
+    const uint64_t tiles = wv::ceil_div(n, tile);
+    const size_t passes = w8 ? wv::plan_passes<int64_t>(opt, tiles).size() : wv::plan_passes<int32_t>(opt, tiles).size();
+    return 1 + (int)passes;
 }
-int wave_merge_i64(dsort_ctx *ctx, const int64_t *d_in, const size_t *lens, int k, int64_t *d_out, hipStream_t s,
-                   bool keep_stats) {
-    return wv::wave_merge<int64_t>(ctx, d_in, lens, k, d_out, s, keep_stats);
+
+template <typename T>
+int sort_device(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipStream_t s, bool timed) {
+    const bool top = ctx->nested == 0;
+    if (top) ctx->stages_done = 0;
+    const int rc = wv::wave_sort<T>(ctx, d_in, d_keys, n, s, timed);
+    if (rc || !top || ctx->opt.kill_after_pass < 0) return rc;
+    // the kill stage was never reached: a fault-injection run that would silently not fail
+    return set_err(ctx, DSORT_EINVAL,
+                   "DSORT_OPT_KILL_AFTER_STAGE = " + std::to_string(ctx->opt.kill_after_pass) + ": this sort of " +
+                       std::to_string(n) + " keys has " + std::to_string(ctx->stages_done) +
+                       " stages (kill points 0.." + std::to_string(ctx->stages_done - 1) + ")");
 }
+
+// k-way merge of back-to-back runs of arbitrary lengths (the master merge, server.c:481-515,
+// and the multi-GPU receive merge); lower runs win ties at every level.
+template <typename T>
+int merge_device(dsort_ctx *ctx, const T *d_in, const size_t *lens, int k, T *d_out, hipStream_t s,
+                 bool keep_stats) {
+    return wv::wave_merge<T>(ctx, d_in, lens, k, d_out, s, keep_stats);
+}
+
+template int sort_device<int32_t>(dsort_ctx *, const int32_t *, int32_t *, size_t, hipStream_t, bool);
+template int sort_device<int64_t>(dsort_ctx *, const int64_t *, int64_t *, size_t, hipStream_t, bool);
+template int merge_device<int32_t>(dsort_ctx *, const int32_t *, const size_t *, int, int32_t *, hipStream_t,
+                                   bool);
+template int merge_device<int64_t>(dsort_ctx *, const int64_t *, const size_t *, int, int64_t *, hipStream_t,
+                                   bool);
 
 }  // namespace dsort

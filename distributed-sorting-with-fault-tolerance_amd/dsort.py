@@ -27,7 +27,7 @@ ERRORS = {-1: "EINVAL", -2: "ENOMEM", -3: "EHIP", -4: "ECOMM", -5: "ENODEV", -6:
 # every symbol include/dsort.h declares (checked by tests/test_abi.py)
 EXPORTS = [
     "dsort_init", "dsort_finalize", "dsort_last_error", "dsort_version", "dsort_get_stats",
-    "dsort_synchronize", "dsort_set_option", "dsort_get_option", "dsort_sort_i32", "dsort_sort_i64", "dsort_sort_dev_i32",
+    "dsort_synchronize", "dsort_set_option", "dsort_get_option", "dsort_sort_stages", "dsort_sort_i32", "dsort_sort_i64", "dsort_sort_dev_i32",
     "dsort_sort_dev_i64", "dsort_sort_dev_copy_i32", "dsort_sort_dev_copy_i64",
     "dsort_merge_i32", "dsort_merge_i64", "dsort_merge_dev_i32", "dsort_merge_dev_i64",
     "dsort_comm_unique_id", "dsort_comm_init", "dsort_comm_init_transport", "dsort_comm_abort",
@@ -46,7 +46,8 @@ EXPORTS = [
 
 # dsort_set_option / dsort_get_option (include/dsort.h)
 OPTIONS = {"buckets": 1, "bucket_keys": 2, "bucket_oversample": 3,
-           "max_fanin_log2": 5, "kill_after_pass": 6, "kill_in_exchange": 7, "comm_timeout_ms": 8,
+           "max_fanin_log2": 5, "kill_after_stage": 6, "kill_after_pass": 6, "kill_in_exchange": 7,
+           "comm_timeout_ms": 8,
            "sub_keys": 9, "sub_oversample": 10, "sub_gather": 11}
 
 
@@ -62,7 +63,9 @@ class Stats(ctypes.Structure):
                 ("tile_keys", ctypes.c_int), ("keys_in", ctypes.c_size_t),
                 ("keys_out", ctypes.c_size_t), ("alltoall_ms", ctypes.c_double),
                 ("keys_sent", ctypes.c_size_t), ("tile_sort_kernel_ms", ctypes.c_double),
-                ("partition_ms", ctypes.c_double), ("tile_sort_keys", ctypes.c_size_t)]
+                ("partition_ms", ctypes.c_double), ("tile_sort_keys", ctypes.c_size_t),
+                ("bucket_hist_ms", ctypes.c_double), ("bucket_scatter_ms", ctypes.c_double),
+                ("sub_partition_ms", ctypes.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -156,6 +159,7 @@ def load():
         "dsort_synchronize": (ctypes.c_int, [P]),
         "dsort_set_option": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int64]),
         "dsort_get_option": (ctypes.c_int, [P, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]),
+        "dsort_sort_stages": (ctypes.c_int, [P, SZ, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
         "dsort_sort_i32": (ctypes.c_int, [P, P, SZ]),
         "dsort_sort_i64": (ctypes.c_int, [P, P, SZ]),
         "dsort_sort_dev_i32": (ctypes.c_int, [P, P, SZ, P]),
@@ -322,6 +326,12 @@ class Context:
         finally:
             for k, v in old.items():
                 self.set_option(k, v)
+
+    def sort_stages(self, n, key_bytes=4):
+        """Kill points of a sort of n keys under this context's options (dsort_sort_stages)."""
+        m = ctypes.c_int()
+        self.check(self.lib.dsort_sort_stages(self.h, n, key_bytes, ctypes.byref(m)))
+        return m.value
 
     # ---------------- host-buffer entry points (reference drop-ins) ----------------------
     def sort(self, keys):

@@ -39,8 +39,8 @@ def reassign(dead, world, rule="first-live"):
 
 
 def run_master(nworkers, n_total, dtype="i32", dist="uniform", transport="rccl", devices=None,
-               rule="first-live", kill_rank=None, kill_stage="sort", kill_after_pass=0,
-               kill_exchange_stage=2, output=None, timeout_s=600, extra=(), env=None):
+               rule="first-live", kill_rank=None, kill_stage="sort", kill_after_stage=0,
+               kill_exchange_stage=2, output=None, timeout_s=600, extra=(), env=None, kill_in_recovery=None):
     """One run of the C master; returns its JSON report (plus 'stderr_tail')."""
     cmd = [MASTER, "--mode", "samplesort", "--gpus", str(nworkers), "--keys", str(n_total),
            "--dtype", dtype, "--dist", dist, "--transport", transport, "--reassign", rule]
@@ -48,8 +48,10 @@ def run_master(nworkers, n_total, dtype="i32", dist="uniform", transport="rccl",
         cmd += ["--devices", devices if isinstance(devices, str) else ",".join(str(d) for d in devices)]
     if kill_rank is not None:
         cmd += ["--kill-rank", str(kill_rank), "--kill-stage", kill_stage]
-        cmd += ["--kill-after-pass", str(kill_after_pass)] if kill_stage == "sort" else \
+        cmd += ["--kill-after-stage", str(kill_after_stage)] if kill_stage == "sort" else \
                ["--kill-exchange-stage", str(kill_exchange_stage)]
+    if kill_in_recovery is not None:
+        cmd += ["--kill-in-recovery", str(kill_in_recovery)]
     if output:
         cmd += ["--output", output]
     cmd += list(extra)
@@ -64,13 +66,14 @@ def run_master(nworkers, n_total, dtype="i32", dist="uniform", transport="rccl",
     return rep
 
 
-def fault_run(nworkers, n_total, kill_rank, kill_after_pass, dtype="i32", dist="uniform", transport="rccl",
+def fault_run(nworkers, n_total, kill_rank, kill_after_stage, dtype="i32", dist="uniform", transport="rccl",
               devices=None, rule="first-live", stage="sort", kill_exchange_stage=2):
-    """A fault-free run, then a run with `kill_rank` dying in its local sort (after merge pass
-    `kill_after_pass`) or inside the exchange; recovery time = the difference of the two ends
+    """A fault-free run, then a run with `kill_rank` dying in its local sort (after stage
+    `kill_after_stage`, dsort.h DSORT_OPT_KILL_AFTER_STAGE) or inside the exchange; recovery time =
+    the difference of the two ends
     (each the slowest survivor's DONE at the master, from GO)."""
     free = run_master(nworkers, n_total, dtype, dist, transport, devices, rule)
     fault = run_master(nworkers, n_total, dtype, dist, transport, devices, rule, kill_rank=kill_rank,
-                       kill_stage=stage, kill_after_pass=kill_after_pass, kill_exchange_stage=kill_exchange_stage)
+                       kill_stage=stage, kill_after_stage=kill_after_stage, kill_exchange_stage=kill_exchange_stage)
     return {"fault_free": free, "fault": fault, "recovery_ms": fault["t_end_ms"] - free["t_end_ms"],
             "ok": free["ok"] and fault["ok"] and fault["dead"] == [kill_rank]}

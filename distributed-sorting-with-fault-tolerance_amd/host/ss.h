@@ -56,11 +56,12 @@ typedef struct ss_job {
     uint32_t transport;                     /* 0 rccl, 1 relay through the master             */
     uint32_t source;                        /* 0 uniform, 1 zipf (worker generates its chunk
                                                into the replica), 2 replica already filled   */
-    int32_t kill_after_pass;                /* fault injection for this worker, -1 off        */
+    int32_t kill_after_pass;                /* fault injection: DSORT_OPT_KILL_AFTER_STAGE, -1 off */
     int32_t kill_in_exchange;               /* -1 off, 1 / 2 = DSORT_OPT_KILL_IN_EXCHANGE     */
     int64_t comm_timeout_ms;
     uint32_t heartbeat_ms;
-    uint32_t pad;
+    int32_t kill_in_recovery;               /* fault injection: 1 = die on the first recovery PLAN
+                                               (a second failure while the survivors rebuild)   */
     char shm_name[64];
     char uid[128];                          /* RCCL unique id of this epoch                   */
 } ss_job;

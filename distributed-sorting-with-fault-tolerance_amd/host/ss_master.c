@@ -3,8 +3,8 @@
  *
  *   dsort_master --mode samplesort --gpus N [--keys K] [--dtype i32|i64] [--dist uniform|zipf]
  *                [--input FILE] [--transport rccl|relay] [--devices LIST|share] [--worker PATH]
- *                [--kill-rank R [--kill-stage sort|exchange] [--kill-after-pass K]
- *                 [--kill-exchange-stage 1|2]] [--reassign first-live|next-live]
+ *                [--kill-rank R [--kill-stage sort|exchange] [--kill-after-stage K]
+ *                 [--kill-exchange-stage 1|2]] [--kill-in-recovery R2] [--reassign first-live|next-live]
  *                [--heartbeat-ms MS] [--timeout-ms MS] [--comm-timeout-ms MS] [--seed S]
  *                [--output FILE]
  *
@@ -52,6 +52,7 @@ typedef struct wstate {
     int alive;
     double last_seen;
     int ready, done;
+    double fail_at; /* DONE of the current epoch with a non-zero status: when it came */
     ss_ready rd;
     ss_done dn;
     /* relay request of the current epoch */
@@ -73,13 +74,17 @@ typedef struct mopt {
     int share;      /* all workers on GPU 0 */
     int devices[SS_MAX_WORKERS];
     const char *worker;
-    int kill_rank, kill_after_pass, kill_exchange_stage;
+    int kill_rank, kill_after_pass, kill_exchange_stage, kill_in_recovery;
     int next_live;
     int hb_ms, timeout_ms;
     int64_t comm_timeout_ms;
     uint64_t seed;
     const char *output;
 } mopt;
+
+/* A DONE with an error status waits this long for a peer's death that would explain it (the
+ * master sees a death within milliseconds: socket EOF, process exit) before the worker is fenced. */
+#define SS_FAIL_GRACE_MS 1000.0
 
 static double now_ms(void) {
     struct timespec ts;
@@ -96,7 +101,8 @@ static void usage_ss(void) {
     fprintf(stderr,
             "usage: dsort_master --mode samplesort --gpus N [--keys K] [--dtype i32|i64] [--dist uniform|zipf]\n"
             "       [--input FILE] [--transport rccl|relay] [--devices 0,1,..|share] [--worker PATH]\n"
-            "       [--kill-rank R [--kill-stage sort|exchange] [--kill-after-pass K] [--kill-exchange-stage 1|2]]\n"
+            "       [--kill-rank R [--kill-stage sort|exchange] [--kill-after-stage K] [--kill-exchange-stage 1|2]]\n"
+            "       [--kill-in-recovery R2]\n"
             "       [--reassign first-live|next-live] [--heartbeat-ms MS] [--timeout-ms MS]\n"
             "       [--comm-timeout-ms MS] [--seed S] [--output FILE]\n");
     exit(2);
@@ -134,6 +140,7 @@ int samplesort_master(int argc, char **argv, const char *argv0) {
     o.kill_rank = -1;
     o.kill_after_pass = -1;
     o.kill_exchange_stage = -1;
+    o.kill_in_recovery = -1;
     o.hb_ms = 50;
     o.timeout_ms = 5000;
     o.seed = 0x5EED2026ull;
@@ -165,7 +172,8 @@ int samplesort_master(int argc, char **argv, const char *argv0) {
         } else if (!strcmp(a, "--worker")) o.worker = NEXT();
         else if (!strcmp(a, "--kill-rank")) o.kill_rank = atoi(NEXT());
         else if (!strcmp(a, "--kill-stage")) kill_stage_exchange = !strcmp(NEXT(), "exchange");
-        else if (!strcmp(a, "--kill-after-pass")) o.kill_after_pass = atoi(NEXT());
+        else if (!strcmp(a, "--kill-after-stage") || !strcmp(a, "--kill-after-pass")) o.kill_after_pass = atoi(NEXT());
+        else if (!strcmp(a, "--kill-in-recovery")) o.kill_in_recovery = atoi(NEXT());
         else if (!strcmp(a, "--kill-exchange-stage")) o.kill_exchange_stage = atoi(NEXT());
         else if (!strcmp(a, "--reassign")) o.next_live = !strcmp(NEXT(), "next-live");
         else if (!strcmp(a, "--heartbeat-ms")) o.hb_ms = atoi(NEXT());
@@ -186,6 +194,10 @@ int samplesort_master(int argc, char **argv, const char *argv0) {
         if (!kill_stage_exchange && o.kill_after_pass < 0) o.kill_after_pass = 0;
         if (kill_stage_exchange) o.kill_after_pass = -1;
         else o.kill_exchange_stage = -1;
+    }
+    if (o.kill_rank >= o.n || o.kill_in_recovery >= o.n || (o.kill_in_recovery >= 0 && o.kill_in_recovery == o.kill_rank)) {
+        fprintf(stderr, "master: --kill-rank / --kill-in-recovery must name two different workers of %d\n", o.n);
+        return 2;
     }
     if (!have_devices)
         for (int i = 0; i < o.n; ++i) o.devices[i] = o.share ? 0 : i;
@@ -215,6 +227,19 @@ int samplesort_master(int argc, char **argv, const char *argv0) {
         }
         o.keys = (uint64_t)nk;
         o.key_bytes = 4;
+    }
+    if (o.kill_rank >= 0 && o.kill_after_pass >= 0) {
+        /* a kill stage the victim's local sort never reaches would be a fault run without a fault */
+        const uint64_t q = o.keys / (uint64_t)o.n, rm = o.keys % (uint64_t)o.n;
+        const uint64_t len = q + ((uint64_t)o.kill_rank < rm ? 1 : 0);
+        int stages = 0;
+        if (dsort_sort_stages(NULL, len, o.key_bytes, &stages) || o.kill_after_pass >= stages) {
+            fprintf(stderr, "master: --kill-after-stage %d: the local sort of worker %d (%llu keys) has %d stages "
+                    "(kill points 0..%d)\n", o.kill_after_pass, o.kill_rank, (unsigned long long)len, stages,
+                    stages - 1);
+            free(parsed);
+            return 2;
+        }
     }
     const size_t kb = (size_t)o.key_bytes;
     const size_t shm_bytes = o.keys > 0 ? o.keys * kb : 1;
@@ -335,6 +360,7 @@ int samplesort_master(int argc, char **argv, const char *argv0) {
             j.source = o.input ? 2u : (uint32_t)o.dist;
             j.kill_after_pass = r == o.kill_rank ? o.kill_after_pass : -1;
             j.kill_in_exchange = r == o.kill_rank ? o.kill_exchange_stage : -1;
+            j.kill_in_recovery = r == o.kill_in_recovery ? 1 : 0;
             j.comm_timeout_ms = o.comm_timeout_ms;
             j.heartbeat_ms = (uint32_t)o.hb_ms;
             snprintf(j.shm_name, sizeof j.shm_name, "%s", shm_name);
@@ -393,6 +419,7 @@ int samplesort_master(int argc, char **argv, const char *argv0) {
                     if (d.epoch == epoch) {
                         w->dn = d;
                         w->done = 1;
+                        if (d.status != 0 && w->fail_at <= 0) w->fail_at = now;
                         if (now - t_go > t_end) t_end = now - t_go;
                     }
                 } else if ((h.type == SS_RELAY_AG || h.type == SS_RELAY_A2A) && (uint32_t)h.status >> 20 == epoch) {
@@ -419,6 +446,14 @@ int samplesort_master(int argc, char **argv, const char *argv0) {
                     W[r].alive = 0;
                     newly = 1;
                 } else if (go_sent && o.timeout_ms > 0 && now - W[r].last_seen > o.timeout_ms) {
+                    kill(W[r].pid, SIGKILL);
+                    W[r].alive = 0;
+                    newly = 1;
+                } else if (W[r].fail_at > 0 && now - W[r].fail_at > SS_FAIL_GRACE_MS) {
+                    /* its exchange failed (DSORT_ECOMM / DSORT_ETIMEOUT) and no peer died that
+                     * would explain it: fence the worker (kill) and reassign its chunks */
+                    fprintf(stderr, "master: worker %d reported status %d for epoch %u; fenced\n", r + 1,
+                            W[r].dn.status, epoch);
                     kill(W[r].pid, SIGKILL);
                     W[r].alive = 0;
                     newly = 1;
@@ -463,6 +498,7 @@ int samplesort_master(int argc, char **argv, const char *argv0) {
                             if (owner[c] == r) p.chunks[p.nchunks++] = (uint32_t)c;
                         memcpy(p.uid, uid, sizeof p.uid);
                         W[r].done = 0;
+                        W[r].fail_at = 0;
                         W[r].has_req = 0;
                         send_to(&W[r], SS_PLAN, 0, &p, sizeof p);
                         printf("Reassigning: epoch %u, worker %d now rank %u of %d, chunks", epoch, r + 1, p.rank, live);

@@ -16,6 +16,7 @@
 #include <errno.h>
 #include <fcntl.h>
 #include <pthread.h>
+#include <signal.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -37,6 +38,7 @@ typedef struct wk {
     pthread_cond_t cv;
     int go, bye, closed, slice_req, stop;
     int plan_pending;
+    int initing;         /* inside dsort_comm_init* (the heartbeat thread re-raises a lost abort) */
     ss_plan plan;
     uint32_t epoch;      /* epoch of the communicator in use */
     int world;           /* ranks of that epoch */
@@ -131,7 +133,12 @@ static void *heartbeat_main(void *arg) {
         while (!w->stop && !w->closed)
             if (pthread_cond_timedwait(&w->cv, &w->mu, &ts) == ETIMEDOUT) break;
         const int done = w->stop || w->closed;
+        /* a PLAN for a newer epoch while the communicator of this one is being built: the
+         * reader's abort may have come before dsort_comm_init took the communicator lock and been
+         * lost; repeat it until the set-up returns (an init waiting for a dead peer never would) */
+        const int stuck = w->initing && w->plan_pending && w->plan.epoch > w->epoch;
         pthread_mutex_unlock(&w->mu);
+        if (stuck) dsort_comm_abort(w->ctx);
         if (done || send_frame(w, SS_HB, NULL, 0)) return NULL;
     }
 }
@@ -228,16 +235,32 @@ static void chunk_range(uint64_t n, uint32_t world, uint32_t c, uint64_t *off, u
         }                                                                                         \
     } while (0)
 
+/* The communicator of `epoch`.  Returns COMM_SUPERSEDED (and builds nothing, or drops what it
+ * built) when a PLAN for a newer epoch is pending, else the dsort_comm_init* code. */
+#define COMM_SUPERSEDED 1
 static int comm_up(wk *w, const ss_job *job, uint32_t epoch, int world, int rank, const char *uid,
                    dsort_transport *tx) {
     dsort_ctx *ctx = w->ctx;
     pthread_mutex_lock(&w->mu);
-    w->epoch = epoch;
+    if (w->plan_pending && w->plan.epoch > epoch) {
+        pthread_mutex_unlock(&w->mu);
+        return COMM_SUPERSEDED;
+    }
+    w->epoch = epoch; /* with initing, under one lock: the heartbeat's check sees both */
     w->world = world;
     w->relay_seq = 0;
+    w->initing = 1;
     pthread_mutex_unlock(&w->mu);
-    if (job->transport == 0) return dsort_comm_init(ctx, world, rank, uid);
-    return dsort_comm_init_transport(ctx, world, rank, tx);
+    int rc = job->transport == 0 ? dsort_comm_init(ctx, world, rank, uid) : dsort_comm_init_transport(ctx, world, rank, tx);
+    pthread_mutex_lock(&w->mu);
+    w->initing = 0;
+    const int newer = w->plan_pending && w->plan.epoch > epoch;
+    pthread_mutex_unlock(&w->mu);
+    if (newer) {
+        dsort_comm_abort(ctx);
+        rc = COMM_SUPERSEDED;
+    }
+    return rc;
 }
 
 int samplesort_worker(const char *host, int port, int device, int verbose) {
@@ -404,9 +427,13 @@ int samplesort_worker(const char *host, int port, int device, int verbose) {
                 if (bye || have_plan) break;
             }
             if (!have_plan) break;
-            /* recovery epoch: drop the communicator, rebuild the run from the chunks now owned */
-            dsort_comm_abort(ctx);
+            if (job.kill_in_recovery) raise(SIGKILL); /* fault injection: a second failure during recovery */
+            /* recovery epoch: drop the communicator, rebuild the run from the chunks now owned.  A
+             * PLAN for a newer epoch (another worker died meanwhile) restarts from that plan: the
+             * chunks already merged stay owned, the new ones are added. */
             const double t_rb = now_ms();
+        rebuild:
+            dsort_comm_abort(ctx);
             for (uint32_t i = 0; i < plan.nchunks; ++i) {
                 const uint32_t c = plan.chunks[i];
                 int have = 0;
@@ -433,8 +460,14 @@ int samplesort_worker(const char *host, int port, int device, int verbose) {
                 run_len += len;
                 owned[nowned++] = c;
             }
-            t_rebuild = now_ms() - t_rb;
             rc = comm_up(&w, &job, plan.epoch, (int)plan.world, (int)plan.rank, plan.uid, &tx);
+            if (rc == COMM_SUPERSEDED) {
+                pthread_mutex_lock(&w.mu);
+                plan = w.plan;
+                pthread_mutex_unlock(&w.mu);
+                goto rebuild;
+            }
+            t_rebuild = now_ms() - t_rb;
             if (rc) fprintf(stderr, "worker: communicator of epoch %u failed (%d): %s\n", plan.epoch, rc, dsort_last_error(ctx));
         }
     }

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define DSORT_ABI_VERSION 2
+#define DSORT_ABI_VERSION 3
 
 #define DSORT_OK 0
 #define DSORT_EINVAL (-1)   /* bad argument */
@@ -69,6 +69,11 @@ typedef struct dsort_stats {
     double partition_ms;    /* bucketed sort: the partition passes before the tile sort   */
     size_t tile_sort_keys;  /* keys the tile sort sorted (bucketed sort: a bucket of one key
                                value -- a heavy duplicate -- is not tile-sorted)             */
+    /* ABI 3: the partition kernels alone (HIP events around their launches; 0 when the sort
+     * did not run them) */
+    double bucket_hist_ms;    /* first-level histogram                                      */
+    double bucket_scatter_ms; /* first-level scatter                                        */
+    double sub_partition_ms;  /* second-level partition (local partition, or hist + scatter) */
 } dsort_stats;
 
 /* ---------------------------------------------------------------- lifecycle ---------- */
@@ -90,8 +95,13 @@ int dsort_synchronize(dsort_ctx *ctx);
 #define DSORT_OPT_BUCKET_OVERSAMPLE 3 /* splitter samples per bucket, 1..4096 (default 256)            */
 /* 4: retired (skewed bucket sizes of the round-1 merge plan); rejected as unknown               */
 #define DSORT_OPT_MAX_FANIN_LOG2 5    /* cap on log2(F) of one merge pass; -1 = per key type default   */
-#define DSORT_OPT_KILL_AFTER_PASS 6   /* fault injection (config C5): SIGKILL the calling process right
-                                         after merge pass k of a local sort; -1 = off (default)        */
+#define DSORT_OPT_KILL_AFTER_STAGE 6  /* fault injection (config C5): SIGKILL the calling process right
+                                         after stage k of a local sort has finished on the GPU; -1 =
+                                         off (default).  Stages: bucketed sort (>= 2^25 keys) 0 first-
+                                         level partition, 1 second-level partition, 2 tile sort; below
+                                         2^25 keys 0 tile sort, 1 + p merge pass p (dsort_sort_stages).
+                                         A stage the sort never reaches makes it return DSORT_EINVAL */
+#define DSORT_OPT_KILL_AFTER_PASS DSORT_OPT_KILL_AFTER_STAGE /* ABI 2 name                        */
 #define DSORT_OPT_KILL_IN_EXCHANGE 7  /* fault injection: SIGKILL inside the sample-sort exchange, at
                                          stage 1 (samples all-gathered) or 2 (counts exchanged, keys
                                          about to move); -1 = off (default)                            */
@@ -109,6 +119,12 @@ int dsort_set_option(dsort_ctx *ctx, int option, int64_t value);
 int dsort_get_option(const dsort_ctx *ctx, int option, int64_t *value);
 
 /* ---------------------------------------------------------------- worker sort -------- */
+/* Number of stages (fault-injection kill points, DSORT_OPT_KILL_AFTER_STAGE) a sort of n keys of
+ * key_bytes (4 or 8) bytes passes through under ctx's options (ctx NULL: the defaults).  With
+ * DSORT_OPT_SUB_KEYS = 0 the bucketed sort's merge passes depend on the data: the guaranteed
+ * minimum. */
+int dsort_sort_stages(const dsort_ctx *ctx, size_t n, int key_bytes, int *stages);
+
 /* Drop-in for `merge_sort(chunk, 0, n-1)` (client.c:117 -> client.c:166-173): sorts the
  * caller-owned HOST buffer in place, ascending.  Copies to HBM, sorts on the GPU, copies
  * back; returns when `host_keys` holds the result. */
@@ -146,7 +162,7 @@ int dsort_merge_dev_i64(dsort_ctx *ctx, const int64_t *d_in, const size_t lens[]
 /* One process per GPU.  Rank 0 creates the 128-byte RCCL unique id and ships it to the other
  * ranks by any side channel (the bench uses torch.distributed's store; the C master of
  * `dsort_master --mode samplesort` creates it and sends it in every worker's JOB frame over its
- * TCP control socket, host/master.c); every rank then calls dsort_comm_init.  The communicator
+ * TCP control socket, host/ss_master.c); every rank then calls dsort_comm_init.  The communicator
  * is non-blocking: every wait of the exchange polls the stream, RCCL's asynchronous error and the
  * abort flag (dsort_comm_abort from another thread), so a dead peer surfaces as DSORT_ECOMM or,
  * with DSORT_OPT_COMM_TIMEOUT_MS, DSORT_ETIMEOUT instead of a hang. */

@@ -136,13 +136,34 @@ int dsort_comm_init_transport(dsort_ctx *ctx, int nranks, int rank, const dsort_
 int dsort_comm_abort(dsort_ctx *ctx) { (void)ctx; g_has_tx = 0; return DSORT_OK; }
 int dsort_comm_destroy(dsort_ctx *ctx) { (void)ctx; g_has_tx = 0; return DSORT_OK; }
 
+/* The double's sort has the library's three bucketed-sort kill points (dsort.h,
+ * DSORT_OPT_KILL_AFTER_STAGE), as three real stages: 0 the lower half sorted, 1 the upper half
+ * sorted, 2 the halves merged.  A stage never reached is an error, as in the library. */
+int dsort_sort_stages(const dsort_ctx *ctx, size_t n, int key_bytes, int *stages) {
+    (void)ctx;
+    if (!stages || (key_bytes != 4 && key_bytes != 8)) return DSORT_EINVAL;
+    *stages = n < 2 ? 0 : 3;
+    return DSORT_OK;
+}
 #define DOUBLE_SORT(T, SFX)                                                                          \
     int dsort_sort_dev_copy_##SFX(dsort_ctx *ctx, const T *in, T *out, size_t n, void *s) {            \
         (void)ctx; (void)s;                                                                          \
         if (n && in != out) memmove(out, in, n * sizeof(T));                                        \
-        if (oracle_merge_sort_##SFX(out, n)) return DSORT_ENOMEM;                                    \
-        if (g_kill_after_pass >= 0) raise(SIGKILL); /* "after merge pass k": the only pass here */ \
-        return DSORT_OK;                                                                             \
+        if (n < 2) return g_kill_after_pass >= 0 ? DSORT_EINVAL : DSORT_OK;                          \
+        const size_t h = n / 2;                                                                      \
+        if (oracle_merge_sort_##SFX(out, h)) return DSORT_ENOMEM;                                    \
+        if (g_kill_after_pass == 0) raise(SIGKILL);                                                  \
+        if (oracle_merge_sort_##SFX(out + h, n - h)) return DSORT_ENOMEM;                            \
+        if (g_kill_after_pass == 1) raise(SIGKILL);                                                  \
+        T *tmp = (T *)malloc(n * sizeof(T));                                                         \
+        if (!tmp) return DSORT_ENOMEM;                                                               \
+        const T *runs[2] = {out, out + h};                                                           \
+        const size_t lens[2] = {h, n - h};                                                           \
+        oracle_merge_runs_##SFX(2, runs, lens, tmp);                                                 \
+        memcpy(out, tmp, n * sizeof(T));                                                             \
+        free(tmp);                                                                                   \
+        if (g_kill_after_pass == 2) raise(SIGKILL);                                                  \
+        return g_kill_after_pass >= 0 ? DSORT_EINVAL : DSORT_OK;                                     \
     }                                                                                                \
     int dsort_merge_dev_##SFX(dsort_ctx *ctx, const T *in, const size_t lens[], int k, T *out, void *s) { \
         (void)ctx; (void)s;                                                                          \

@@ -92,3 +92,22 @@ def test_write_text(dsort_mod, tmp_path, oracle):
     p = tmp_path / "output.txt"
     dsort_mod.write_text_i32(str(p), a)
     assert p.read_bytes() == oracle.format(a)
+
+
+def test_sort_stages(dsort_mod):
+    """Kill points of a sort (DSORT_OPT_KILL_AFTER_STAGE) under the default options, no GPU needed:
+    the bucketed path (>= 2^25 keys) has three, the merge path one per pass plus the tile sort."""
+    lib = dsort_mod.load()
+
+    def stages(n, w):
+        m = ctypes.c_int()
+        assert lib.dsort_sort_stages(None, n, w, ctypes.byref(m)) == 0
+        return m.value
+
+    assert stages(0, 4) == 0 and stages(1, 8) == 0
+    assert stages(1 << 30, 4) == 3 and stages(1 << 29, 4) == 3 and stages(1 << 25, 8) == 3
+    assert stages(16384, 4) == 1                   # one tile: the tile sort only
+    assert stages(1 << 20, 4) == 3                 # 64 tiles: tile sort + 2 merge passes (F <= 16)
+    assert stages((1 << 25) - 1, 4) == 1 + 3       # 2048 tiles: 11 bits in 3 passes
+    m = ctypes.c_int()
+    assert lib.dsort_sort_stages(None, 100, 2, ctypes.byref(m)) == -1

@@ -1,0 +1,138 @@
+"""Fault machinery of the library on the MI355X (pytest -m gpu):
+
+  * the kill points of a local sort (DSORT_OPT_KILL_AFTER_STAGE, dsort.h): every stage of the
+    bucketed path (>= 2^25 keys: first-level partition, second-level partition, tile sort) and of
+    the merge path really SIGKILLs the process after that stage, and a stage the sort never reaches
+    is an error (DSORT_EINVAL), not a silent fault-free run -- the reference's fault moment is "any
+    time the socket fails" (server.c:358-395, 421-449);
+  * the RCCL communicator's abort and rebuild (the survivor path of server.c:421-449 in the
+    multi-GPU design): a non-blocking communicator is built, sorts, is aborted from a second thread
+    (ncclCommAbort), and a fresh one (new unique id, ncclCommInitRankConfig) sorts again -- at one
+    rank, the size of this box."""
+import os
+import subprocess
+import sys
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from conftest import PKG, REPO
+
+sys.path.insert(0, PKG)
+pytestmark = pytest.mark.gpu
+SEED = 0x5EED2026
+
+_KILL_CHILD = r"""
+import sys
+sys.path.insert(0, {pkg!r})
+import torch
+import dsort
+n, w, stage = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
+ctx = dsort.Context(0)
+t = torch.empty(n, dtype=torch.int32 if w == 4 else torch.int64, device="cuda")
+ctx.gen_uniform(t, {seed}, 0)
+out = torch.empty_like(t)
+torch.cuda.synchronize()
+print("stages", ctx.sort_stages(n, w), flush=True)
+ctx.set_option("kill_after_stage", stage)
+try:
+    ctx.sort_dev(t, out)
+    torch.cuda.synchronize()
+    print("returned ok", flush=True)
+except dsort.DsortError as e:
+    print("error", e, flush=True)
+    sys.exit(3)
+"""
+
+
+def _kill_child(n, w, stage):
+    code = _KILL_CHILD.format(pkg=PKG, seed=SEED)
+    return subprocess.run([sys.executable, "-c", code, str(n), str(w), str(stage)], capture_output=True, text=True,
+                          timeout=120, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+
+
+@pytest.mark.parametrize("n,w,stage", [(1 << 25, 4, 0), (1 << 25, 4, 1), (1 << 25, 4, 2), (1 << 25, 8, 1),
+                                       (1 << 20, 4, 0), (1 << 20, 4, 2)])
+def test_kill_point_fires(n, w, stage):
+    p = _kill_child(n, w, stage)
+    assert p.returncode == -9, p.stdout + p.stderr  # SIGKILL, after the stage finished
+    assert "returned ok" not in p.stdout
+
+
+@pytest.mark.parametrize("n,w,stage", [(1 << 25, 4, 3), (1 << 20, 4, 3), (1, 4, 0)])
+def test_unreachable_kill_point_is_an_error(n, w, stage):
+    p = _kill_child(n, w, stage)
+    assert p.returncode == 3 and "EINVAL" in p.stdout and "stages" in p.stdout, p.stdout + p.stderr
+
+
+def _sorted_slice_ok(ctx, ptr, nout, fp_in):
+    import ctypes
+
+    import dsort
+    c, fs, fx = dsort.U64(), dsort.U64(), dsort.U64()
+    ctx.check(ctx.lib.dsort_count_descents_i32(ctx.h, ptr, nout, ctypes.byref(c)))
+    ctx.check(ctx.lib.dsort_fingerprint_i32(ctx.h, ptr, nout, ctypes.byref(fs), ctypes.byref(fx)))
+    return c.value == 0 and (fs.value, fx.value) == fp_in
+
+
+def test_rccl_abort_and_rebuild_one_rank(gpu_ctx):
+    """dsort_comm_init (non-blocking RCCL) -> sample sort -> dsort_comm_abort from a second thread
+    while a sample sort runs -> the communicator is gone (DSORT_ECOMM) -> dsort_comm_init with a new
+    unique id -> sample sort again (dsort_api.hip: abort_comm_locked, exch_wait, dsort_comm_init)."""
+    import torch
+
+    import dsort
+    ctx = gpu_ctx
+    n = 1 << 26
+    t = torch.empty(n, dtype=torch.int32, device="cuda")
+    ctx.gen_uniform(t, SEED, 0)
+    fp_in = ctx.fingerprint(t)
+    ctx.comm_init(1, 0, dsort.Context.unique_id())
+    ptr, nout = ctx.sample_sort_dev(t)
+    ctx.synchronize()
+    assert nout == n and _sorted_slice_ok(ctx, ptr, nout, fp_in)
+    res = {}
+
+    def run():
+        try:
+            res["ok"] = ctx.sample_sort_dev(t)
+            ctx.synchronize()
+        except dsort.DsortError as e:
+            res["err"] = str(e)
+
+    th = threading.Thread(target=run)
+    th.start()
+    time.sleep(0.003)
+    ctx.comm_abort()  # another thread: raises the flag (exchange running) or aborts the idle comm
+    th.join(60)
+    assert not th.is_alive()
+    assert "ok" in res or "ECOMM" in res["err"], res
+    # the communicator is gone either way (an abort that came after the exchange is taken by the
+    # next call)
+    with pytest.raises(dsort.DsortError, match="ECOMM"):
+        ctx.sample_sort_dev(t)
+    ctx.comm_init(1, 0, dsort.Context.unique_id())  # a fresh ncclCommInitRankConfig
+    ptr, nout = ctx.sample_sort_dev(t)
+    ctx.synchronize()
+    assert nout == n and _sorted_slice_ok(ctx, ptr, nout, fp_in)
+    # idle abort (ncclCommAbort on a live communicator), then re-init once more, then destroy
+    ctx.comm_abort()
+    ctx.comm_init(1, 0, dsort.Context.unique_id())
+    ptr, nout = ctx.sample_sort_dev(t)
+    ctx.synchronize()
+    assert _sorted_slice_ok(ctx, ptr, nout, fp_in)
+    ctx.comm_destroy()
+    del t
+    torch.cuda.empty_cache()
+
+
+def test_c_master_rccl_one_gpu_with_comm_deadline():
+    """dsort_master --mode samplesort over RCCL on this box's one GPU with an exchange deadline
+    (DSORT_OPT_COMM_TIMEOUT_MS: every polled wait of the exchange and the communicator set-up)."""
+    import ftsort
+    r = ftsort.run_master(1, (1 << 25) + 7, transport="rccl", devices=[0], timeout_s=180,
+                          extra=["--comm-timeout-ms", "60000"])
+    assert r["ok"], r
+    assert r["transport"] == "rccl" and r["epochs"] == 1 and r["slices"] == [(1 << 25) + 7]

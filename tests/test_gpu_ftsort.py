@@ -38,13 +38,36 @@ def test_fault_free_run_sorts(tmp_path, oracle):
 def test_worker_killed_mid_sort_is_recovered(rule, kill):
     import ftsort
 
-    n = 1 << 22  # 2^20 keys per worker: 64 tiles, two merge passes; the kill follows pass 0
-    r = _run(4, n, rule=rule, kill_rank=kill, kill_stage="sort", kill_after_pass=0)
+    n = 1 << 22  # 2^20 keys per worker: 64 tiles, two merge passes; the kill follows the tile sort
+    r = _run(4, n, rule=rule, kill_rank=kill, kill_stage="sort", kill_after_stage=0)
     assert r["ok"], r
     assert r["dead"] == [kill] and r["epochs"] == 2
     assert r["owners"][kill] == ftsort.reassign({kill}, 4, rule)[kill]
     assert len(r["slices"]) == 3 and sum(r["slices"]) == n
     assert r["t_fault_seen_ms"] >= 0 and r["t_survivors_notified_ms"] >= 0
+
+
+@pytest.mark.parametrize("kstage", [0, 1])
+def test_large_worker_killed_mid_local_sort(kstage):
+    """Config C5's path at a worker size of the bucketed sort (2^25 keys per worker: two partition
+    levels and the tile sort): worker 1 dies after its first-level partition (stage 0) or after its
+    second-level partition (stage 1) -- in the middle of its local sort -- and the run recovers."""
+    import ftsort
+
+    n = 3 << 25
+    r = _run(3, n, kill_rank=1, kill_stage="sort", kill_after_stage=kstage)
+    assert r["ok"], r
+    assert r["dead"] == [1] and r["epochs"] == 2 and sum(r["slices"]) == n
+    assert r["owners"][1] == ftsort.reassign({1}, 3)[1]
+
+
+def test_second_failure_during_recovery():
+    """Worker 1 dies in its local sort, worker 3 dies on receiving the recovery plan: the survivors
+    must move on to the third epoch and still sort everything."""
+    n = 4_000_037
+    r = _run(4, n, kill_rank=1, kill_stage="sort", kill_after_stage=0, kill_in_recovery=3)
+    assert r["ok"], r
+    assert sorted(r["dead"]) == [1, 3] and r["epochs"] == 3 and sum(r["slices"]) == n
 
 
 @pytest.mark.parametrize("stage", [1, 2])
@@ -58,7 +81,7 @@ def test_worker_killed_inside_exchange_is_recovered(stage):
 
 
 def test_zipf_int64_fault_run():
-    r = _run(3, 2_000_003, dtype="i64", dist="zipf", kill_rank=2, kill_stage="sort", kill_after_pass=0)
+    r = _run(3, 2_000_003, dtype="i64", dist="zipf", kill_rank=2, kill_stage="sort", kill_after_stage=0)
     assert r["ok"], r
     assert r["dead"] == [2]
 

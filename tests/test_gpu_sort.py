@@ -190,6 +190,30 @@ def test_full_size_properties(gpu_ctx, n, dt, dist):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("n,dt,dist", [(1 << 28, "i32", "uniform"), (1 << 30, "i32", "uniform"),
+                                       (1 << 30, "i64", "zipf")])
+def test_full_size_bit_exact_vs_torch_sort(gpu_ctx, n, dt, dist):
+    """north_star asks for bit-exact output at the metric's sizes: the default (bucketed) path of
+    dsort_sort_dev_copy compared element for element with torch.sort (rocPRIM's radix sort -- an
+    independent implementation) on config C2 (2^28 int32), the metric size (2^30 int32) and
+    config C4 on one GPU (2^30 Zipf int64).  The fingerprint test above stays as well."""
+    import torch
+    tdt = torch.int32 if dt == "i32" else torch.int64
+    t = torch.empty(n, dtype=tdt, device="cuda")
+    if dist == "zipf":
+        gpu_ctx.gen_zipf_i64(t, 0x5EED2026, 0)
+    else:
+        gpu_ctx.gen_uniform(t, 0x5EED2026, 0)
+    out = torch.empty_like(t)
+    gpu_ctx.sort_dev(t, out)
+    torch.cuda.synchronize()
+    assert gpu_ctx.stats()["merge_passes"] == 0  # the two-level partition path, no merge pass
+    ref = torch.sort(t).values
+    assert torch.equal(out, ref)
+    del t, out, ref
+    torch.cuda.empty_cache()
+
+
 def test_zipf_i64_sort(gpu_ctx):
     import torch
     n = (1 << 24) + 17

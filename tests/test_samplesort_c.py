@@ -75,6 +75,43 @@ def test_worker_killed_is_recovered(libdir, tmp_path, oracle, rule, kill, owner,
     assert out.read_bytes() == b"".join(b"%d\n" % int(k) for k in expected(oracle, n))
 
 
+@pytest.mark.parametrize("kstage", [0, 1, 2])
+def test_worker_killed_at_every_sort_stage(libdir, tmp_path, oracle, kstage):
+    """The library's three kill points of a bucketed local sort (first-level partition, second-level
+    partition, tile sort; dsort.h DSORT_OPT_KILL_AFTER_STAGE), each a real stage of the double's sort."""
+    n = 30_011
+    out = tmp_path / "out.txt"
+    r, p = run_master(libdir, tmp_path, "--gpus", "3", "--keys", str(n), "--kill-rank", "1", "--kill-stage", "sort",
+                      "--kill-after-stage", str(kstage), "--output", str(out))
+    assert r["ok"], p.stdout + p.stderr
+    assert r["dead"] == [1] and r["epochs"] == 2 and sum(r["slices"]) == n
+    assert out.read_bytes() == b"".join(b"%d\n" % int(k) for k in expected(oracle, n))
+
+
+def test_unreachable_kill_stage_is_an_error(libdir, tmp_path):
+    """A kill stage the victim's sort never reaches is refused up front (no silent fault-free run)."""
+    env = dict(os.environ, LD_LIBRARY_PATH=libdir + ":" + os.environ.get("LD_LIBRARY_PATH", ""))
+    p = subprocess.run([MASTER, "--mode", "samplesort", "--transport", "relay", "--devices", "share", "--gpus", "3",
+                        "--keys", "3000", "--kill-rank", "2", "--kill-after-stage", "3"],
+                       cwd=tmp_path, env=env, capture_output=True, text=True, timeout=60)
+    assert p.returncode == 2 and "has 3 stages" in p.stderr, p.stderr
+
+
+@pytest.mark.parametrize("first_stage", [["--kill-stage", "sort", "--kill-after-stage", "1"],
+                                         ["--kill-stage", "exchange", "--kill-exchange-stage", "2"]])
+def test_second_failure_during_recovery(libdir, tmp_path, oracle, first_stage):
+    """Worker 1 dies; worker 3 dies as soon as it receives the recovery plan, while the other
+    survivors rebuild: they must take the next plan (no hang on the first recovery epoch's
+    communicator) and the output is still the sorted input (ss_worker.c:437)."""
+    n = 50_021
+    out = tmp_path / "out.txt"
+    r, p = run_master(libdir, tmp_path, "--gpus", "4", "--keys", str(n), "--kill-rank", "1", *first_stage,
+                      "--kill-in-recovery", "3", "--output", str(out))
+    assert r["ok"], p.stdout + p.stderr
+    assert sorted(r["dead"]) == [1, 3] and r["survivors"] == 2 and r["epochs"] == 3
+    assert out.read_bytes() == b"".join(b"%d\n" % int(k) for k in expected(oracle, n))
+
+
 def test_input_file_kat(libdir, tmp_path):
     """The reference's input.txt through the C sample sort: output.txt byte-identical to the
     reference's own output.txt (SURVEY.md §4 KAT)."""
