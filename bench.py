@@ -20,10 +20,12 @@ The sorted output is verified outside the timed region (ascending + multiset fin
 boundaries).
 
 Rank 0 prints ONE JSON line with two extra objects:
-  roofline      live HIP-event timing of the dominant kernel (the tile sort, one launch over all
-                tiles: 2 x key bytes per key; at N > 1 the local sort's, slowest rank) against
-                8 TB/s, and at N > 1 the key exchange's bytes over xGMI against (N-1) links x
-                153 GB/s;
+  roofline      live HIP-event timing of every kernel of the sort (first-level histogram and
+                scatter, second-level partition, tile sort: algorithmic bytes = 1 or 2 x key
+                bytes per key) against 8 TB/s; `kernel` is the slowest of them (at N > 1 the
+                slowest stage of any rank's local sort); `all_kernels_frac` = the committed PMC
+                bytes of the whole sort over its device time; at N > 1 the key
+                exchange's bytes over xGMI against (N-1) links x 153 GB/s;
   cpu_baseline  the reference's own algorithm (client.c merge_sort on 4 threads + server.c
                 merge_chunks, compiled from the reference sources into oracle/_ref) on a bounded
                 sample, plus the reference's TCP server + 4 clients on input.txt (config C1),
@@ -370,29 +372,60 @@ def cpu_baseline(sample_keys, target_keys):
     }
 
 
-# the tile sort kernel of the default (gathering) path, as rocprofv3 names it
-TILE_SORT_KERNEL = {4: "bin_sort_kernel<int, true>", 8: "bin_sort_kernel<long, true>"}
+# The kernels of the default (bucketed) sort, as rocprofv3 names them, per key width: the stage
+# they run (dsort_stats field of their HIP-event time) and their algorithmic bytes per key
+# (w = key bytes): the histogram reads every key once, the other three read and write every key
+# (the second level and the tile sort only the keys outside single-key buckets).
+STAGE_KERNELS = {
+    4: [("bucket_hist_kernel<int>", "bucket_hist_ms", 1, "n"),
+        ("bucket_scatter_lines_kernel", "bucket_scatter_ms", 2, "n"),
+        ("sb_local_kernel<int>", "sub_partition_ms", 2, "tile_sort_keys"),
+        ("bin_sort_kernel<int, true>", "tile_sort_kernel_ms", 2, "tile_sort_keys")],
+    8: [("bucket_hist_kernel<long>", "bucket_hist_ms", 1, "n"),
+        ("bucket_scatter_kernel<long>", "bucket_scatter_ms", 2, "n"),
+        ("sb_local_kernel<long>", "sub_partition_ms", 2, "tile_sort_keys"),
+        ("bin_sort_kernel<long, true>", "tile_sort_kernel_ms", 2, "tile_sort_keys")],
+}
+# the generator and runtime copies are not part of the sort
+NOT_SORT = ("gen_uniform", "gen_zipf", "__amd_rocclr", "fingerprint", "descents")
+PMC_FILES = ("r3_pmc_traffic.json", "r2_pmc_traffic.json")
 
 
-def pmc_traffic(kernel, n, w):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC passes
-    (FETCH_SIZE x2 + WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md), scaled to this run's
-    key count; None when absent or measured on another key width."""
-    for name in ("r2_pmc_traffic.json", "r1_pmc_traffic.json"):
+def _pmc_doc(w):
+    """The newest committed rocprofv3 PMC traffic table for key width w (bytes per launch:
+    FETCH_SIZE x 2 + WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md), or None."""
+    for name in PMC_FILES:
         path = os.path.join(REPO, "profiles", name)
         try:
             with open(path) as f:
                 doc = json.load(f)
-            if w != doc.get("key_bytes", 4) and "int64" in doc:
-                doc = doc["int64"]
-            rec = doc["kernels"][kernel]
-        except (OSError, KeyError, ValueError):
+        except (OSError, ValueError):
             continue
-        if w != doc.get("key_bytes", 4):
-            return None
-        return round(rec.get("traffic_bytes_per_launch", rec.get("traffic_bytes_per_pass", rec.get("traffic_bytes")))
-                     * n / doc.get("keys", 1 << 30))
+        if w != doc.get("key_bytes", 4) and "int64" in doc:
+            doc = doc["int64"]
+        if w == doc.get("key_bytes", 4):
+            doc["file"] = "profiles/" + name
+            return doc
     return None
+
+
+def pmc_traffic(kernel, n, w):
+    """HBM bytes per launch of `kernel` from the newest PMC table, scaled to this run's key count;
+    None when absent or measured on another key width."""
+    doc = _pmc_doc(w)
+    if not doc or kernel not in doc["kernels"]:
+        return None
+    rec = doc["kernels"][kernel]
+    return round(rec["traffic_bytes_per_launch"] * n / doc.get("keys", 1 << 30))
+
+
+def pmc_sort_bytes(n, w):
+    """HBM bytes of one whole sort: every kernel of the PMC table but the generator / copies."""
+    doc = _pmc_doc(w)
+    if not doc:
+        return None, None
+    tot = sum(r["traffic_bytes_per_launch"] for k, r in doc["kernels"].items() if not k.startswith(NOT_SORT))
+    return round(tot * n / doc.get("keys", 1 << 30)), doc["file"]
 
 
 # ------------------------------------------------------------------------- GPU runs
@@ -432,26 +465,25 @@ def run_single(args):
     if not ok:
         raise SystemExit("bench: sorted output failed verification")
     torch.cuda.synchronize()
-    kms, klaunch, bms, tot, npass, tsk, pms, tkeys = 0.0, 0, 0.0, 0.0, 0, 0.0, 0.0, 0
+    acc = {k: 0.0 for k in ("merge_kernel_ms", "block_sort_ms", "total_ms", "tile_sort_kernel_ms", "partition_ms",
+                            "bucket_hist_ms", "bucket_scatter_ms", "sub_partition_ms")}
+    npass, tkeys = 0, 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         ctx.sort_dev(t_in, out)
         st = ctx.stats()  # reads the HIP events of this step (syncs the stream)
-        kms += st["merge_kernel_ms"]
-        klaunch += st["merge_kernel_launches"]
-        bms += st["block_sort_ms"]
-        tot += st["total_ms"]
+        for k in acc:
+            acc[k] += st[k]
         npass += st["merge_passes"]
-        tsk += st["tile_sort_kernel_ms"]
-        pms += st["partition_ms"]
         tkeys += st["tile_sort_keys"]
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     stats = ctx.stats()
     ctx.close()
-    return t1 - t0, {"kernel_ms": kms, "launches": klaunch, "block_ms": bms, "device_ms": tot,
-                     "passes": stats["merge_passes"], "npass": npass, "tile": stats["tile_keys"], "w": w,
-                     "tile_sort_ms": tsk, "partition_ms": pms, "tile_sort_keys": tkeys // max(args.steps, 1)}
+    k = {key: v / max(args.steps, 1) for key, v in acc.items()}  # per step
+    k.update({"passes": stats["merge_passes"], "npass": npass, "tile": stats["tile_keys"], "w": w,
+              "tile_sort_keys": tkeys // max(args.steps, 1), "n": n})
+    return t1 - t0, k
 
 
 def run_multi(args, rank, world):
@@ -502,13 +534,16 @@ def run_multi(args, rank, world):
     torch.cuda.synchronize()
     dist.barrier()
     t0 = time.perf_counter()
-    acc = {"exchange_ms": 0.0, "alltoall_ms": 0.0, "final_merge_ms": 0.0, "merge_kernel_ms": 0.0,
-           "merge_kernel_launches": 0, "merge_passes": 0, "sent": 0, "tile_sort_kernel_ms": 0.0}
+    timed = ("exchange_ms", "alltoall_ms", "final_merge_ms", "merge_kernel_ms", "tile_sort_kernel_ms",
+             "bucket_hist_ms", "bucket_scatter_ms", "sub_partition_ms")
+    acc = {k: 0.0 for k in timed}
+    acc.update({"merge_kernel_launches": 0, "merge_passes": 0, "sent": 0, "tile_sort_keys": 0})
     for _ in range(args.steps):
         ptr, nout = ctx.sample_sort_dev(t_in)
         st = ctx.stats()  # synchronizes this rank's stream
-        for k in ("exchange_ms", "alltoall_ms", "final_merge_ms", "merge_kernel_ms", "tile_sort_kernel_ms"):
+        for k in timed:
             acc[k] += st[k]
+        acc["tile_sort_keys"] += st["tile_sort_keys"]
         acc["merge_kernel_launches"] += st["merge_kernel_launches"]
         acc["merge_passes"] += st["merge_passes"]
         acc["sent"] += st["keys_sent"]
@@ -520,7 +555,9 @@ def run_multi(args, rank, world):
     # per-rank figures of the roofline, gathered (rank 0 reports the slowest rank)
     steps = max(args.steps, 1)
     mine = torch.tensor([acc["tile_sort_kernel_ms"] / steps, acc["alltoall_ms"] / steps, acc["exchange_ms"] / steps,
-                         acc["final_merge_ms"] / steps, acc["sent"] / steps, sz], dtype=torch.float64)
+                         acc["final_merge_ms"] / steps, acc["sent"] / steps, sz,
+                         acc["bucket_hist_ms"] / steps, acc["bucket_scatter_ms"] / steps,
+                         acc["sub_partition_ms"] / steps, acc["tile_sort_keys"] / steps], dtype=torch.float64)
     everyone = [torch.zeros_like(mine) for _ in range(world)]
     dist.all_gather(everyone, mine)
     A = torch.stack(allinfo)
@@ -549,36 +586,58 @@ def result_header(args, world):
             "data": f"synthetic {args.dist} keys, splitmix64(seed={SEED:#x} + global index)"}
 
 
+def stage_roofline(k, w, n):
+    """Per-stage HIP-event times of the sort's kernels (the average launch of each over the timed
+    steps) against their algorithmic bytes, and the slowest of them."""
+    stages = []
+    for kernel, field, per_key, keys_field in STAGE_KERNELS[w]:
+        ms = k.get(field, 0.0)
+        if ms <= 0:
+            continue
+        nb = per_key * w * k[keys_field]
+        ach = nb / (ms * 1e-3) / 1e9
+        stages.append({"kernel": kernel, "avg_launch_ms": round(ms, 4), "algorithmic_bytes_per_launch": nb,
+                       "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
+                       "traffic": pmc_traffic(kernel, n, w)})
+    return stages
+
+
 def report_single(args, elapsed, k):
     result = result_header(args, 1)
     n = args.keys
     step_ms = 1000.0 * elapsed / args.steps
     result.update({"value": n * args.steps / elapsed, "ms_per_step": step_ms})
-    # the dominant kernel is the tile sort: one launch reads and writes every key once (the
-    # sub-bucket path gathers its tiles from the locally partitioned chunks); merge passes only
-    # run for oversized sub-buckets or with DSORT_OPT_SUB_KEYS = 0
-    tile_ms = k["tile_sort_ms"] / args.steps
-    # the keys the tile sort sorted: all of them, less the buckets of a single key (heavy
-    # duplicates), which the second level skips
-    bytes_tile = 2 * k["w"] * k["tile_sort_keys"]
-    achieved = bytes_tile / (tile_ms * 1e-3) / 1e9 if tile_ms > 0 else 0.0
-    npass = k["npass"]
     cfg = "C2-style" if args.dtype == "i32" else "C4-style"
     result["config"] = {"workload": f"{cfg} single-GPU sort of {n} {args.dist} {result['dtype']} keys "
                                     f"(BASELINE metric size); tile {k['tile']} keys, {k['passes']} merge passes",
                         "keys": n, "parallelism": "1 GPU"}
-    result["roofline"] = {
-        "bound": "hbm", "kernel": "bin_sort_kernel (tile sort, one launch over all tiles; bitonic "
-                                  "block_sort_w_kernel for the tiles it declines)",
-        "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(TILE_SORT_KERNEL[k["w"]], n, k["w"]),
-        "avg_launch_ms": round(tile_ms, 4), "algorithmic_bytes_per_launch": bytes_tile,
-        "tile_sort_keys": k["tile_sort_keys"],
-        "partition_ms": round(k["partition_ms"] / args.steps, 3),
-        "merge_passes": npass // max(args.steps, 1),
-        "merge_kernel_ms": round(k["kernel_ms"] / args.steps, 4),
-        "whole_sort_single_pass_bound_frac": round(2 * k["w"] * n / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-    }
+    w = k["w"]
+    stages = stage_roofline(k, w, n)
+    if stages:  # the bucketed path: the dominant kernel is the slowest stage
+        dom = max(stages, key=lambda r: r["avg_launch_ms"])
+    else:  # below 2^25 keys: tile sort + merge passes
+        tile_ms = k["tile_sort_kernel_ms"]
+        nb = 2 * w * k["tile_sort_keys"]
+        ach = nb / (tile_ms * 1e-3) / 1e9 if tile_ms > 0 else 0.0
+        dom = {"kernel": STAGE_KERNELS[w][3][0], "avg_launch_ms": round(tile_ms, 4),
+               "algorithmic_bytes_per_launch": nb, "achieved": round(ach, 1),
+               "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(STAGE_KERNELS[w][3][0], n, w)}
+    roof = {"bound": "hbm", "kernel": dom["kernel"], "achieved": dom["achieved"], "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": dom["frac"], "traffic": dom["traffic"],
+            "avg_launch_ms": dom["avg_launch_ms"], "algorithmic_bytes_per_launch": dom["algorithmic_bytes_per_launch"],
+            "timing": "HIP events around each kernel launch on the sort's stream, averaged over the timed steps",
+            "stages": stages, "tile_sort_keys": k["tile_sort_keys"],
+            "partition_ms": round(k["partition_ms"], 3), "device_ms": round(k["total_ms"], 3),
+            "merge_passes": k["npass"] // max(args.steps, 1), "merge_kernel_ms": round(k["merge_kernel_ms"], 4),
+            "whole_sort_single_pass_bound_frac": round(2 * w * n / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    # SURVEY.md §8d primary: every sort kernel's PMC bytes over the sort's device time
+    pb, src = pmc_sort_bytes(n, w)
+    if pb and k["total_ms"] > 0:
+        roof["all_kernels_frac"] = round(pb / (k["total_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        roof["all_kernels"] = {"pmc_bytes_per_sort": pb, "device_ms": round(k["total_ms"], 3), "pmc_source": src,
+                               "rule": "sum of FETCH_SIZE x2 + WRITE_SIZE over the sort's kernels / device time "
+                                       "of the sort (HIP events, first splitter kernel to last tile) / 8 TB/s"}
+    result["roofline"] = roof
     if not args.no_cpu_baseline and args.dtype == "i32":
         result["cpu_baseline"] = cpu_baseline(args.cpu_sample_keys, n)
     print(json.dumps(result), flush=True)
@@ -592,16 +651,30 @@ def report_multi(args, world, elapsed, per_rank, w):
     result["config"] = {"workload": f"sample sort of {n} {args.dist} {result['dtype']} keys over {world} GPUs "
                                     "(equal contiguous chunks, splitters, RCCL all-to-all over xGMI, merge)",
                         "keys": n, "keys_per_gpu": n // world, "parallelism": f"samplesort x{world}"}
-    slow = int(np.argmax(per_rank[:, 0]))
-    tile_ms = float(per_rank[slow, 0])
-    n_gpu = float(per_rank[slow, 5])
-    bpl = 2 * w * n_gpu  # the local tile sort reads and writes the rank's chunk once
-    ach = bpl / (tile_ms * 1e-3) / 1e9 if tile_ms > 0 else None
-    roof = {"bound": "hbm", "kernel": "bin_sort_kernel (local tile sort, slowest rank)",
-            "achieved": round(ach, 1) if ach else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None,
-            "traffic": pmc_traffic(TILE_SORT_KERNEL[w], int(n_gpu), w), "avg_launch_ms": round(tile_ms, 4),
-            "algorithmic_bytes_per_launch": int(bpl),
+    # the local sort's stages on every rank (HIP events); the dominant kernel is the slowest stage
+    # of the slowest rank
+    best = None
+    for r in range(world):
+        kr = {"tile_sort_kernel_ms": float(per_rank[r, 0]), "bucket_hist_ms": float(per_rank[r, 6]),
+              "bucket_scatter_ms": float(per_rank[r, 7]), "sub_partition_ms": float(per_rank[r, 8]),
+              "n": float(per_rank[r, 5]), "tile_sort_keys": float(per_rank[r, 9])}
+        for st in stage_roofline(kr, w, int(kr["n"])):
+            if best is None or st["avg_launch_ms"] > best[1]["avg_launch_ms"]:
+                best = (r, st)
+    if best is None:  # below 2^25 keys per rank: the tile sort
+        slow = int(np.argmax(per_rank[:, 0]))
+        tile_ms, n_gpu = float(per_rank[slow, 0]), float(per_rank[slow, 5])
+        bpl = 2 * w * n_gpu
+        ach = bpl / (tile_ms * 1e-3) / 1e9 if tile_ms > 0 else 0.0
+        best = (slow, {"kernel": STAGE_KERNELS[w][3][0], "avg_launch_ms": round(tile_ms, 4),
+                       "algorithmic_bytes_per_launch": int(bpl), "achieved": round(ach, 1),
+                       "frac": round(ach / HBM_PEAK_GBS, 4),
+                       "traffic": pmc_traffic(STAGE_KERNELS[w][3][0], int(n_gpu), w)})
+    rk, dom = best
+    roof = {"bound": "hbm", "kernel": dom["kernel"] + f" (local sort, rank {rk}: the slowest stage of any rank)",
+            "achieved": dom["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": dom["frac"],
+            "traffic": dom["traffic"], "avg_launch_ms": dom["avg_launch_ms"],
+            "algorithmic_bytes_per_launch": int(dom["algorithmic_bytes_per_launch"]),
             "whole_sort_single_pass_bound_frac": round(
                 2 * w * n / (step_ms * 1e-3) / 1e9 / (HBM_PEAK_GBS * world), 4)}
     if world > 1:
