@@ -33,23 +33,11 @@ constexpr int BK_T = 1024;               // threads of the partition kernels
 constexpr int BK_MAXB = 1024;            // buckets at most (<= threads, one bucket per thread)
 constexpr int BK_OS = 32;                // samples per bucket
 constexpr int BK_CHUNK = 64;             // workgroups per column-sum chunk
-#ifndef DSORT_BK_BID
-#define DSORT_BK_BID 0                   // scatter: LDS holds bucket ids, not global positions
-#endif
 
-// Scatter sub-tile per key width: KPT keys per thread, SUB = BK_T * KPT keys staged in LDS.
+// Scatter sub-tile per key width: KPT keys per thread, SUB = BK_T * KPT keys staged in LDS
+// (int32: 56 KiB next to the 64 KiB line carry of the line scatter; 12 and 13 measured slower).
 template <typename T> struct Geo;
-#ifndef DSORT_BK_LINES
-#define DSORT_BK_LINES 1                 // int32 scatter writes whole 64-byte lines (carry in LDS)
-#endif
-#ifndef DSORT_BK_KPT32
-#if DSORT_BK_LINES
-#define DSORT_BK_KPT32 14                // 56 KiB sub-tile + 64 KiB line carry
-#else
-#define DSORT_BK_KPT32 16
-#endif
-#endif
-template <> struct Geo<int32_t> { static constexpr int KPT = DSORT_BK_KPT32; };
+template <> struct Geo<int32_t> { static constexpr int KPT = 14; };
 template <> struct Geo<int64_t> { static constexpr int KPT = 8; };
 
 struct TileRef {
@@ -131,10 +119,7 @@ __device__ __forceinline__ int bucket_of(const typename Comp<T>::C *spl, int BP,
 //                    slot and every key binary-searches hundreds of splitters.
 // int32 keeps the fixed map (the top SLOTB bits, ulo = 0) and no one-key slots: its histogram
 // runs at the HBM rate and the extra lookup work measured +0.5 ms there at 2^30 uniform keys.
-#ifndef DSORT_BK_SLOTB
-#define DSORT_BK_SLOTB 11
-#endif
-constexpr int BK_SLOTB = DSORT_BK_SLOTB;
+constexpr int BK_SLOTB = 11;
 constexpr int BK_SLOTS = 1 << BK_SLOTB;
 
 struct BkMap {
@@ -143,12 +128,6 @@ struct BkMap {
     uint32_t mode;  // 0 linear, 1 log
     uint64_t invn;  // 2^48 / n: index -> 16-bit fraction of the input
 };
-#ifndef DSORT_BK_ONEKEY
-#define DSORT_BK_ONEKEY 1
-#endif
-#ifndef DSORT_BK_RCP
-#define DSORT_BK_RCP 1
-#endif
 // log mode: mantissa bits M, the largest with (KB - M + 1) * 2^M slots in the table
 template <typename T, int SB>
 __host__ __device__ constexpr int log_m() {
@@ -252,24 +231,18 @@ __device__ __forceinline__ int bucket_fast(const typename Comp<T>::C *spl, const
                                            T key, const typename Comp<T>::C &c) {
     const uint32_t r = rng[slot];
     int lo = (int)(r & 0x7FFF), hi = (int)(r >> 16);
-#if DSORT_BK_ONEKEY
     if (Comp<T>::ADAPT && (r & 0x8000)) {
         const typename Comp<T>::C a = spl[lo], z = spl[hi - 1];
         const T K = Comp<T>::key_of(a);
         const uint32_t i = Comp<T>::idx_of(c), ia = Comp<T>::idx_of(a), iz = Comp<T>::idx_of(z);
         if (key != K || i <= ia) return key <= K ? lo : hi;
         if (i > iz) return hi;
-        // hi - lo - 1 inner buckets over the indices (ia, iz]
-#if DSORT_BK_RCP
-        // (the hardware reciprocal: the same instruction in the histogram and the scatter)
+        // hi - lo - 1 inner buckets over the indices (ia, iz] (the hardware reciprocal: the same
+        // instruction in the histogram and the scatter; IEEE division measured 0.25 ms slower)
         const float q = (float)(i - ia - 1) * ((float)(hi - lo - 1) * __builtin_amdgcn_rcpf((float)(iz - ia)));
-#else
-        const float q = (float)(i - ia - 1) * ((float)(hi - lo - 1) / (float)(iz - ia));
-#endif
         const int j = (int)q;
         return lo + 1 + (j < hi - lo - 2 ? j : hi - lo - 2);
     }
-#endif
     while (lo < hi) {  // lower bound among the splitters of the slot
         const int mid = (lo + hi) >> 1;
         if (Comp<T>::lt(spl[mid], c)) lo = mid + 1;
@@ -388,16 +361,12 @@ __device__ __forceinline__ void load_splitters(const typename Comp<T>::C *spl_g,
 // among subs values up to that cap the one with the fewest sub-tiles per CU over all rounds wins
 // (2^30 int32: 14 sub-tiles, 21 rounds = 294 sub-tiles per CU, instead of 16 with 18.3 rounds =
 // 19 x 16 = 304).
-#ifndef DSORT_BK_BALANCE
-#define DSORT_BK_BALANCE 1
-#endif
 constexpr uint64_t BK_CUS = 256;  // MI355X compute units
 template <typename T>
 __host__ __forceinline__ int bucket_wg_subs(uint64_t n) {
     const uint64_t sub = (uint64_t)BK_T * Geo<T>::KPT;
     const uint64_t v = n / (2048 * sub);
     const int cap = v < 4 ? 4 : (v > 16 ? 16 : (int)v);
-#if DSORT_BK_BALANCE
     if (cap > 4) {
         const uint64_t nsub = (n + sub - 1) / sub;
         int best = cap;
@@ -411,7 +380,6 @@ __host__ __forceinline__ int bucket_wg_subs(uint64_t n) {
         }
         return best;
     }
-#endif
     return cap;
 }
 
@@ -588,14 +556,8 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_kernel(const T *__restric
     __shared__ uint32_t hist[BK_MAXB];   // sub-tile histogram
     __shared__ uint32_t wsum[BK_T / 64];
     __shared__ T lk[SUB];                // the sub-tile grouped by bucket
-#if DSORT_BK_BID
-    __shared__ uint16_t lb[SUB];         // bucket of every LDS entry
-    // thread b keeps bucket b's next global position in a register (B <= BK_T)
-    uint32_t gy = threadIdx.x < (unsigned)B ? (uint32_t)offs[(uint64_t)blockIdx.x * B + threadIdx.x] : 0u;
-#else
     __shared__ uint32_t lg[SUB];         // global position of every LDS entry
     for (int b = threadIdx.x; b < B; b += BK_T) sgo[b] = make_uint2(0u, (uint32_t)offs[(uint64_t)blockIdx.x * B + b]);
-#endif
     load_splitters<T>(spl_g, BP, spl);
     const BkMap m = *map;
     __syncthreads();
@@ -651,30 +613,6 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_kernel(const T *__restric
         __syncthreads();
         uint32_t woff = 0;
         for (int i = 0; i < w; ++i) woff += wsum[i];
-#if DSORT_BK_BID
-        // (LDS start - global start) of bucket b in this sub-tile; written after the barrier
-        // that follows the previous sub-tile's stores, read after the next one
-        if (threadIdx.x < (unsigned)B) {
-            sgo[threadIdx.x] = make_uint2(woff + incl - hv, gy - (woff + incl - hv));
-            gy += hv;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < KPT; ++k) {
-            if (bk[k] >= 0) {
-                const uint32_t lp = sgo[bk[k]].x + slot[k];
-                lk[lp] = key[k];
-                lb[lp] = (uint16_t)bk[k];
-            }
-        }
-        __syncthreads();
-        const uint32_t cnt = s0 + SUB <= n ? SUB : (uint32_t)(n - s0);
-#pragma unroll
-        for (int k = 0; k < KPT; ++k) {
-            const uint32_t p = threadIdx.x + k * BK_T;
-            if (p < cnt) out[sgo[lb[p]].y + p] = lk[p];
-        }
-#else
         if (threadIdx.x < (unsigned)B) sgo[threadIdx.x].x = woff + incl - hv;
         __syncthreads();
 #pragma unroll
@@ -699,47 +637,41 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_kernel(const T *__restric
         // advance every bucket's global position by this sub-tile's keys (sgo.x is not read
         // again before the next scan, which follows two barriers)
         if (threadIdx.x < (unsigned)B) sgo[threadIdx.x].y += hv;
-#endif
     }
 }
 
 
-// The int32 scatter with whole-line writes.  The per-sub-tile scatter above writes every
-// bucket's ~20 keys of a sub-tile as a piece of a 128-byte line: the rest of that line comes
-// from the neighbouring sub-tiles, so most lines reach memory in several partial writes, and
-// the scattered stores cost 1.3 of its 3.7 ms at 2^30 keys (measured against an ablation with
-// coalesced stores).  Here every bucket of the workgroup's range is a stream of 64-byte lines
-// (16 keys, aligned in memory): a sub-tile writes only the whole lines of each bucket (the
-// bucket's carried keys + its new keys) and carries the rest (< 16 keys per bucket) in LDS to
-// the next sub-tile.  Only the first and last line of each bucket in the workgroup's range can
-// be partial; the first is padded at the front with "phantom" entries up to the line boundary
-// (never written).  The lines are written by 4 lanes each (16-byte stores), consecutive lanes on
-// consecutive 16-byte pieces; a lane finds its line's bucket in a line->bucket map built by a
-// max-scan over the buckets' first lines.
-#ifndef DSORT_BK_XCD
-#define DSORT_BK_XCD 0
-#endif
-// Workgroup -> key range.  Workgroups are dispatched round-robin over the 8 XCDs; with
-// DSORT_BK_XCD every XCD takes a contiguous block of ranges instead, so the workgroups sharing
-// an L2 write adjacent pieces of every bucket (a bijection on [0, G) for any G).
-__device__ __forceinline__ uint32_t wg_order(uint32_t bid, uint32_t G) {
-#if DSORT_BK_XCD
-    constexpr uint32_t NX = 8;
-    const uint32_t q = G / NX, r = G % NX, x = bid % NX, i = bid / NX;
-    return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
-#else
-    (void)G;
-    return bid;
-#endif
+// Inclusive sum over a wave (DPP row shifts, then the row broadcasts of lane 15 and 31).
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    return v;
 }
 
-#ifdef DSORT_STAMPS
-// Diagnostic build only: per-workgroup phase cycle sums of the line scatter (wave 0), read back
-// by dsort_debug_bkstamps().
-__device__ unsigned long long g_bkstamps[8192 * 16];
-#endif
-constexpr int BK_LK = 16;      // int32 keys per 64-byte line
-constexpr int BK_MAXC = 3072;  // lines per sub-tile at most: (SUB + 30 * BK_MAXB) / 16
+// The int32 scatter with whole-line writes.  Every bucket of a workgroup's range is a stream of
+// aligned 64-byte lines (16 keys): a sub-tile writes only the whole lines of each bucket (the
+// bucket's carried keys + its new keys) and carries the rest (< 16 keys per bucket) in LDS to the
+// next sub-tile, so HBM sees whole-line writes only (a per-sub-tile scatter writes each bucket's
+// ~14 keys as a piece of a line the neighbouring sub-tiles complete: partial-line writes).  Only
+// the first and last line of each bucket in the workgroup's range can be partial; the first is
+// padded at the front with "phantom" entries up to the line boundary (never written).
+// Per sub-tile, five barriers (round 2 had nine):
+//   classify + rank (slot table, splitters, one LDS atomic per key)      | A
+//   owner b: its count, whole lines and carry; one wave scan (DPP)       | B
+//   owner b: its LDS start (into the dense count array), line-map entries for its lines | C
+//   keys to LDS grouped by bucket                                        | D
+//   line phase: 4 lanes per line, 16-byte stores                         | E
+//   carry phase: owner b copies its stream's tail into its carry slot.
+// (Measured and dropped, round 3: a thread per line entry with 4-byte stores, and 16-byte aligned
+// stream regions with 16-byte LDS reads, which need 3 pad entries per bucket and so a 12-key
+// sub-tile per thread: 3.6 ms vs 3.0 ms at 2^30.)
+constexpr int BK_LK = 16;                                       // int32 keys per 64-byte line
+constexpr int BK_LSUB = BK_T * Geo<int32_t>::KPT;               // keys per sub-tile
+constexpr int BK_MAPN = (BK_LSUB + 30 * BK_MAXB) / BK_LK;       // lines per sub-tile, at most
 static __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const int32_t *__restrict__ in, uint64_t n,
                                                                     const int64_t *__restrict__ spl_g,
                                                                     const BkMap *__restrict__ map, int B, int BP, int subs,
@@ -747,49 +679,37 @@ static __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const
                                                                     int32_t *__restrict__ out,
                                                                     int32_t *__restrict__ out2) {
     using CT = Comp<int32_t>;
-    constexpr int KPT = Geo<int32_t>::KPT, SUB = BK_T * KPT;
-    __shared__ uint8_t bpure[BK_MAXB];  // bucket between two splitters of one key: written to out2
-    static_assert((SUB + 30 * BK_MAXB) / BK_LK <= BK_MAXC, "line map too small");
-    static_assert(SUB < (1 << 15), "packed scan fields");
+    constexpr int KPT = Geo<int32_t>::KPT, SUB = BK_LSUB;
+    static_assert(SUB < (1 << 16), "packed scan fields");
+    // (a non-last sub-tile writes <= (SUB + 15 B) / 16 lines, the last <= (SUB + 30 B) / 16)
     __shared__ int64_t spl[BK_MAXB];
     __shared__ uint32_t rng[BK_SLOTS];
-    __shared__ uint4 st[BK_MAXB];  // per bucket: LDS start, carry|phantom|new keys, first line, line base
-    __shared__ union {
-        uint32_t hist[BK_MAXB];   // sub-tile histogram (until the scan)
-        uint16_t map[BK_MAXC];    // line -> bucket + 1 (after the scan)
-    } hm;
+    __shared__ uint32_t hist[BK_MAXB];               // sub-tile histogram, then the LDS starts
+    __shared__ uint2 st[BK_MAXB];                    // per bucket: LDS start | first line << 16, vc|ph|pure|L
+    __shared__ uint32_t sgb[BK_MAXB];                // per bucket: global index of stream entry 0
+    __shared__ uint16_t lmap[BK_MAPN];               // line -> bucket
     __shared__ uint32_t wsum[BK_T / 64];
-    __shared__ int32_t lk[SUB];                  // the sub-tile's new keys grouped by bucket
-    __shared__ int32_t carry[BK_MAXB * BK_LK];   // per bucket: keys not yet written (< 16)
+    __shared__ int32_t lk[SUB];                      // the sub-tile's new keys grouped by bucket
+    __shared__ int32_t carry[BK_MAXB * BK_LK];       // per bucket: stream entries not yet written (< 16)
     const int tb = threadIdx.x, lane = tb & 63, w = tb >> 6;
-    const uint32_t g = wg_order(blockIdx.x, gridDim.x);
+    const uint32_t g = blockIdx.x;
     const bool owner = tb < B;  // thread b owns bucket b's line stream
-#ifdef DSORT_STAMPS
-    uint64_t st_acc[10] = {}, st_t0 = __builtin_amdgcn_s_memtime();
-#define BKST(k)                                                   \
-    do {                                                          \
-        const uint64_t t1_ = __builtin_amdgcn_s_memtime();        \
-        st_acc[k] += t1_ - st_t0;                                 \
-        st_t0 = t1_;                                              \
-    } while (0)
-#else
-#define BKST(k) \
-    do {        \
-    } while (0)
-#endif
-    uint32_t vc = 0, ph = 0, gb = 0;
+    // owner state: vc = stream entries held in carry (phantoms included), ph = phantoms still in
+    // front (the stream's first line not written yet), gb = global index of stream entry 0 (mod 2^32)
+    uint32_t vc = 0, ph = 0, gb = 0, pure = 0;
     if (owner) {
         const uint32_t o = (uint32_t)offs[(uint64_t)g * B + tb];
-        const bool pure = out2 && tb > 0 && tb + 1 < B && CT::key_of(spl_g[tb - 1]) == CT::key_of(spl_g[tb]);
-        bpure[tb] = pure;
+        pure = out2 && tb > 0 && tb + 1 < B && CT::key_of(spl_g[tb - 1]) == CT::key_of(spl_g[tb]);
         ph = (uint32_t)(((uintptr_t)((pure ? out2 : out) + o) >> 2) & (BK_LK - 1));
         vc = ph;
-        gb = o - ph;  // (mod 2^32) the first line of the stream starts ph entries before o
+        gb = o - ph;
+        hist[tb] = 0;
     }
     load_splitters<int32_t>(spl_g, BP, spl);
     const BkMap m = *map;
     __syncthreads();
     build_slots<int32_t>(spl, BP, m, rng);
+    __syncthreads();
     const uint64_t g0 = (uint64_t)g * subs * SUB;
     int32_t nxt[KPT];
 #pragma unroll
@@ -802,11 +722,8 @@ static __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const
         const uint64_t s0 = g0 + (uint64_t)sub * SUB;
         if (s0 >= n) break;  // workgroup-uniform
         const bool last = sub + 1 == subs || s0 + SUB >= n;
-        if (owner) hm.hist[tb] = 0;
-        __syncthreads();
         int32_t key[KPT];
-        int bk[KPT];
-        uint32_t slot[KPT];
+        uint32_t pk[KPT];  // rank | bucket << 16; ~0 past the input
 #pragma unroll
         for (int k = 0; k < KPT; ++k) key[k] = nxt[k];
         uint32_t sl[KPT];
@@ -821,27 +738,21 @@ static __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const
 #pragma unroll
         for (int k = 0; k < KPT; ++k) {
             const uint64_t i = s0 + tb + (uint64_t)k * BK_T;
-            bk[k] = -1;
+            pk[k] = ~0u;
             if (i < n) {
-                bk[k] = bucket_fast<int32_t>(spl, rng, sl[k], key[k], CT::make(key[k], i));
-                slot[k] = atomicAdd(&hm.hist[bk[k]], 1u);
+                const int b = bucket_fast<int32_t>(spl, rng, sl[k], key[k], CT::make(key[k], i));
+                pk[k] = atomicAdd(&hist[b], 1u) | (uint32_t)b << 16;
             }
         }
-        __syncthreads();
-        BKST(0);
-        // one scan of (new keys, lines to write) per bucket, packed in 16-bit halves
-        const uint32_t hv = owner ? hm.hist[tb] : 0;
-        const uint32_t L = vc + hv;  // entries of the stream not yet written
+        __syncthreads();  // A
+        // owner: new keys, whole lines to write, entries carried to the next sub-tile
+        const uint32_t hv = owner ? hist[tb] : 0;
+        const uint32_t L = vc + hv;  // stream entries not yet written
         const uint32_t nl = !owner ? 0 : last ? (L > ph ? (L + BK_LK - 1) / BK_LK : 0) : L / BK_LK;
         const uint32_t pv = hv | nl << 16;
-        uint32_t incl = pv;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(incl, o);
-            if (lane >= o) incl += y;
-        }
+        const uint32_t incl = wave_incl_sum(pv);
         if (lane == 63) wsum[w] = incl;
-        __syncthreads();
-        BKST(1);
+        __syncthreads();  // B
         uint32_t woff = 0, all = 0;
 #pragma unroll
         for (int i = 0; i < BK_T / 64; ++i) {
@@ -851,49 +762,25 @@ static __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const
         }
         const uint32_t ex = woff + incl - pv;
         const uint32_t lks = ex & 0xFFFF, p0 = ex >> 16, C = all >> 16;
-        if (owner) st[tb] = make_uint4(lks, vc | ph << 5 | hv << 10, p0, gb);
-        for (uint32_t i = tb; i < C; i += BK_T) hm.map[i] = 0;  // the histogram is dead
-        __syncthreads();
-        BKST(2);
+        if (owner) {
+            st[tb] = make_uint2(lks | p0 << 16, vc | ph << 5 | pure << 10 | L << 11);
+            sgb[tb] = gb;
+            hist[tb] = lks;  // the placement's LDS starts (a dense array: fewer bank conflicts)
+            for (uint32_t i = 0; i < nl; ++i) lmap[p0 + i] = (uint16_t)tb;
+        }
+        __syncthreads();  // C
 #pragma unroll
         for (int k = 0; k < KPT; ++k)
-            if (bk[k] >= 0) lk[st[bk[k]].x + slot[k]] = key[k];
-        if (nl) hm.map[p0] = (uint16_t)(tb + 1);
-        __syncthreads();
-        BKST(3);
-        // max-scan of the map: every line gets the bucket of the last first-line at or before it
-        uint32_t m[3];
-#pragma unroll
-        for (int t = 0; t < 3; ++t) {
-            const uint32_t i = 3 * tb + t;
-            m[t] = i < C ? hm.map[i] : 0;
-            if (t) m[t] = m[t] > m[t - 1] ? m[t] : m[t - 1];
-        }
-        uint32_t mx = m[2];
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(mx, o);
-            if (lane >= o) mx = y > mx ? y : mx;
-        }
-        const uint32_t below = __shfl_up(mx, 1);
-        if (lane == 63) wsum[w] = mx;
-        __syncthreads();
-        BKST(4);
-        uint32_t pre = lane ? below : 0;
-        for (int i = 0; i < w; ++i) pre = wsum[i] > pre ? wsum[i] : pre;
-#pragma unroll
-        for (int t = 0; t < 3; ++t) {
-            const uint32_t i = 3 * tb + t;
-            if (i < C) hm.map[i] = (uint16_t)(m[t] > pre ? m[t] : pre);
-        }
-        __syncthreads();
-        BKST(5);
+            if (pk[k] != ~0u) lk[hist[pk[k] >> 16] + (pk[k] & 0xFFFF)] = key[k];
+        __syncthreads();  // D
+        if (owner) hist[tb] = 0;  // (the next sub-tile's atomics follow barrier E)
         // whole lines: 4 lanes per line, 4 keys (16 bytes) per lane
         for (uint32_t it = tb; it < 4 * C; it += BK_T) {
             const uint32_t j = it >> 2, q = it & 3;
-            const int b = (int)hm.map[j] - 1;
-            const uint4 sb = st[b];
-            const uint32_t cv = sb.y & 31, cp = (sb.y >> 5) & 31, cL = cv + (sb.y >> 10);
-            const uint32_t e0 = (j - sb.z) * BK_LK + 4 * q;
+            const uint32_t b = lmap[j];
+            const uint2 sb = st[b];
+            const uint32_t cv = sb.y & 31, cp = (sb.y >> 5) & 31, cL = sb.y >> 11, lb = sb.x & 0xFFFF;
+            const uint32_t e0 = (j - (sb.x >> 16)) * BK_LK + 4 * q;
             int32_t v[4];
             bool ok[4];
             bool full = true;
@@ -902,10 +789,10 @@ static __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const
                 const uint32_t e = e0 + t;
                 ok[t] = e >= cp && e < cL;
                 full = full && ok[t];
-                v[t] = !ok[t] ? 0 : e < cv ? carry[b * BK_LK + e] : lk[sb.x + e - cv];
+                v[t] = e < cv ? carry[b * BK_LK + e] : lk[lb + e - cv];
             }
-            const uint32_t gi = sb.w + e0;  // mod 2^32
-            int32_t *tgt = bpure[b] ? out2 : out;
+            const uint32_t gi = sgb[b] + e0;  // mod 2^32
+            int32_t *tgt = (sb.y >> 10) & 1 ? out2 : out;
             if (full) {
                 *reinterpret_cast<int4 *>(tgt + gi) = make_int4(v[0], v[1], v[2], v[3]);
             } else {
@@ -914,26 +801,18 @@ static __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const
                     if (ok[t]) tgt[(uint32_t)(gi + t)] = v[t];
             }
         }
-        BKST(6);
         if (last) break;
-        __syncthreads();
-        BKST(7);
-        // carry the tail of every stream: entries [16 nl, L) -> carry[0, L - 16 nl)
+        __syncthreads();  // E
+        // carry the tail of every stream: entries [16 nl, L) -> carry[0, L - 16 nl) (the entries
+        // below vc of a stream that wrote no line are there already)
         if (owner) {
             const uint32_t nv = L - nl * BK_LK;
-            for (uint32_t e2 = nl ? 0 : vc; e2 < nv; ++e2)
-                carry[tb * BK_LK + e2] = lk[lks + nl * BK_LK + e2 - vc];
+            for (uint32_t e2 = nl ? 0 : vc; e2 < nv; ++e2) carry[tb * BK_LK + e2] = lk[lks + nl * BK_LK + e2 - vc];
             if (nl) ph = 0;
             gb += nl * BK_LK;
             vc = nv;
         }
-        BKST(8);
     }
-#ifdef DSORT_STAMPS
-    if (tb == 0 && blockIdx.x < 8192)
-        for (int k = 0; k < 10; ++k) g_bkstamps[blockIdx.x * 16 + k] = st_acc[k];
-#endif
-#undef BKST
 }
 
 }  // namespace bk

@@ -37,13 +37,7 @@ constexpr int SB_MAXS = 1024;          // sub-buckets per bucket at most
 constexpr int SB_SLOTB = 10;           // slot table: 1024 key slots per bucket
 constexpr int SB_SLOTS = 1 << SB_SLOTB;
 constexpr int SB_ST = 4;               // sub-tiles per chunk
-#ifndef DSORT_SB_KPT32
-#define DSORT_SB_KPT32 16
-#endif
-#ifndef DSORT_SB_KPT64
-#define DSORT_SB_KPT64 8
-#endif
-template <typename T> constexpr int SB_KPT = sizeof(T) == 4 ? DSORT_SB_KPT32 : DSORT_SB_KPT64;  // keys per thread per sub-tile
+template <typename T> constexpr int SB_KPT = sizeof(T) == 4 ? 16 : 8;  // keys per thread per sub-tile
 template <typename T> constexpr int SB_SUB = SB_T * SB_KPT<T>;   // keys of a sub-tile
 template <typename T> constexpr int SB_CH = SB_ST * SB_SUB<T>;   // keys of a chunk
 
@@ -457,10 +451,7 @@ __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restric
 // dsort_debug_sbstamps().
 __device__ unsigned long long g_sbstamps[(1u << 18) * 8];
 #endif
-#ifndef DSORT_SB_LT
-#define DSORT_SB_LT 512
-#endif
-constexpr int SB_LT = DSORT_SB_LT;
+constexpr int SB_LT = 512;
 // keys per thread: the chunk (int32 62 KiB, int64 52 KiB) + tables fit two workgroups per CU
 template <typename T> constexpr int SB_LKPT = sizeof(T) == 4 ? 31 : 13;
 

@@ -55,17 +55,11 @@ constexpr int WK = 64 * R;         // keys per wave: one bitonic window
 constexpr int kWaveMaxLogF = 5;    // fan-in cap of one merge pass
 constexpr int kWaveMaxF = 1 << kWaveMaxLogF;
 
-#ifndef DSORT_MWAVES
-#define DSORT_MWAVES 16
-#endif
 // Per key type: waves of the tile sort and of the merge tile, and the occupancy they are
 // compiled for (waves per SIMD: two workgroups per CU).
 template <typename T> struct WG;
-#ifndef DSORT_WAVES32
-#define DSORT_WAVES32 16
-#endif
 template <> struct WG<int32_t> {
-    static constexpr int WAVES = DSORT_WAVES32, MWAVES = DSORT_MWAVES, OCC = 8, MAXLOGF = 5;
+    static constexpr int WAVES = 16, MWAVES = 16, OCC = 8, MAXLOGF = 5;
 };
 template <> struct WG<int64_t> {
     // F = 32 would need 32 run heads of 64-bit keys per lane next to the window: it spills, so
@@ -88,6 +82,14 @@ constexpr int ROW_MIRROR = 0x140;  // lane ^ 15
 constexpr int ROW_HMIRROR = 0x141; // lane ^ 7
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+// Workgroup -> work item such that XCD x (workgroups bid with bid % 8 == x, the hardware's
+// round-robin) takes the contiguous block of items x * (G / 8) + ... : a bijection on [0, G).
+__device__ __forceinline__ uint32_t xcd_block(uint32_t bid, uint32_t G) {
+    constexpr uint32_t NX = 8;
+    const uint32_t q = G / NX, r = G % NX, x = bid % NX, i = bid / NX;
+    return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
+}
 
 #ifdef DSORT_STAMPS
 // Diagnostic build only: per-workgroup phase timestamps of mergew (s_memtime), read back by
@@ -518,10 +520,6 @@ template <> struct V16<int64_t> {
 // halves at offset 8, a second merge at offset 0 only when a bin of more than 9 keys left a
 // descent.  About 45 compare-exchange operations per key instead of the ~180 of the bitonic tile
 // sort.  Details and the fallback: bin_sort_tile.
-#ifndef DSORT_BIN_SORT
-#define DSORT_BIN_SORT 1
-#endif
-
 
 template <typename T>
 __device__ __forceinline__ T wave_min(T v) {
@@ -1011,11 +1009,8 @@ __device__ __forceinline__ bool load_tile(const T *in, uint64_t n, const uint4 *
 
 // The bin sort of every tile (bin_sort_tile); a tile it declines is appended to fb (*nfb) for
 // the bitonic kernel.  Separate from the bitonic kernel so that each keeps its own registers.
-#ifndef DSORT_BIN_OCC
-#define DSORT_BIN_OCC WG<T>::OCC
-#endif
 template <typename T, bool GATHER>
-__global__ void __launch_bounds__(64 * WG<T>::WAVES, DSORT_BIN_OCC) bin_sort_kernel(const T *in, T *out, uint64_t n,
+__global__ void __launch_bounds__(64 * WG<T>::WAVES, WG<T>::OCC) bin_sort_kernel(const T *in, T *out, uint64_t n,
                                                                      const uint4 *tiles, const uint32_t *ntiles,
                                                                      sb::Gather ga, uint32_t *fb, uint32_t *nfb) {
     constexpr int TILE = TILE_OF<T>;
@@ -1025,14 +1020,18 @@ __global__ void __launch_bounds__(64 * WG<T>::WAVES, DSORT_BIN_OCC) bin_sort_ker
     T x[R];
     uint64_t base;
     int valid;
-    if (!load_tile<T, GATHER>(in, n, tiles, ntiles, ga, blockIdx.x, cw, reinterpret_cast<uint32_t *>(s), x, base,
-                              valid))
+    // Gathered tiles: each XCD takes a contiguous block of tiles (workgroups are dealt round-robin
+    // over the 8 XCDs).  Consecutive tiles of a bucket end and start inside the same 128-byte lines
+    // of every chunk: run on one XCD at about the same time, such a line comes from HBM once and
+    // from that XCD's L2 the second time.
+    const uint32_t j = GATHER ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    if (!load_tile<T, GATHER>(in, n, tiles, ntiles, ga, j, cw, reinterpret_cast<uint32_t *>(s), x, base, valid))
         return;
     if (valid == 0) return;
     // a duplicate run inside a gathered tile shows as two equal neighbouring splitters
     bool hint = false;
     if constexpr (GATHER) {
-        const sb::GTile gt = ga.tiles[blockIdx.x];
+        const sb::GTile gt = ga.tiles[j];
         const sb::Spl<T> *sp = static_cast<const sb::Spl<T> *>(ga.spl) + (uint64_t)gt.b * ga.SS;
         const int jl = gt.j0 > 0 ? (int)gt.j0 - 1 : 0, jh = (int)gt.j1 - 1;  // splitters around the tile
         const int nspl = (int)ga.bi[gt.b].nsub - 1;
@@ -1041,7 +1040,7 @@ __global__ void __launch_bounds__(64 * WG<T>::WAVES, DSORT_BIN_OCC) bin_sort_ker
         hint = __ballot(hint) != 0;
     }
     if (!bin_sort_tile<T>(x, valid, s, cw, out + base, hint, threadIdx.x) && threadIdx.x == 0)
-        fb[atomicAdd(nfb, 1u)] = blockIdx.x;
+        fb[atomicAdd(nfb, 1u)] = j;
 }
 
 // The bitonic tile sort: tile fb[blockIdx.x] (fb = the bin sort's declined tiles) or tile
@@ -1353,7 +1352,7 @@ static int tile_sort(dsort_ctx *ctx, const T *in, T *out, uint64_t n, const uint
     if (rc) return rc;
     // The library's own small sorts (timed = false: the splitter samples) take the bitonic sort
     // alone: it needs no read-back, so the host never waits in the middle of a sort for them.
-    if (DSORT_BIN_SORT && grid && timed) {
+    if (grid && timed) {
         rc = ensure(ctx, &ctx->tfb, &ctx->tfb_bytes, ((size_t)grid + 1) * 4, "tile fallback list");
         if (rc) return rc;
         if (!ctx->tfb_host) DSORT_HIP(ctx, hipHostMalloc((void **)&ctx->tfb_host, 64, hipHostMallocDefault));
@@ -1814,7 +1813,7 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
     // second level runs (it skips them) and d_keys is not the input the scatter still reads.
     T *direct = sub_keys<T>(ctx) && (const void *)d_in != (const void *)d_keys && n < (1ull << 31) ? d_keys : nullptr;
     if ((rc = stage_event(ctx, s, timed, 11))) return rc;
-    if constexpr (std::is_same<T, int32_t>::value && DSORT_BK_LINES) {
+    if constexpr (std::is_same<T, int32_t>::value) {
         hipLaunchKernelGGL(bucket_scatter_lines_kernel, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl,
                            map, B, BP, subs, offs, part_out, direct);
     } else {
@@ -2138,9 +2137,6 @@ extern "C" int dsort_debug_stamps(void *host, size_t bytes) {
 }
 extern "C" int dsort_debug_sbstamps(void *host, size_t bytes) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(sb::g_sbstamps), bytes) == hipSuccess ? 0 : -1;
-}
-extern "C" int dsort_debug_bkstamps(void *host, size_t bytes) {
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(bk::g_bkstamps), bytes) == hipSuccess ? 0 : -1;
 }
 #endif
 

@@ -50,6 +50,8 @@ for _ in range(a.reps):
         best = st
 torch.cuda.synchronize()
 n = max(best["merge_kernel_launches"], 1)
-print(f"{tag:>24s}: total {best['total_ms']:.3f} ms  block {best['block_sort_ms']:.3f}  "
+print(f"{tag:>24s}: total {best['total_ms']:.3f} ms  hist {best['bucket_hist_ms']:.3f}  "
+      f"scatter {best['bucket_scatter_ms']:.3f}  sub {best['sub_partition_ms']:.3f}  "
+      f"tile {best['tile_sort_kernel_ms']:.3f}  partition {best['partition_ms']:.3f}  "
       f"merge-kernel avg {best['merge_kernel_ms'] / n:.3f} ms x{best['merge_kernel_launches']}  "
       f"passes {best['merge_passes']}", flush=True)
