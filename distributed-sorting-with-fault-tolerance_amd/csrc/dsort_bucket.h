@@ -1,30 +1,30 @@
-// dsort_bucket.h -- the sample-splitter partition pass in front of the sorts (namespace
-// dsort::bk; included by dsort_wave.hip for int32 and dsort_sort.hip for int64, whose drivers run
-// their own tile sort and k-way passes inside the buckets).
+// dsort_bucket.h -- the first partition level of the bucketed sort (namespace dsort::bk; included
+// by dsort_wave.hip, whose driver runs the second level (dsort_sub.h) and the tile sort inside
+// the buckets).
 //
 // The multi-GPU design cuts the keys into key ranges with sample-sort splitters and sorts every
 // range on its own GPU.  The same idea inside one GPU's HBM: B buckets (about
-// 2^21 keys each) by splitters taken from a regular sample, in (key, input index) order so that
+// 2^20 keys each) by splitters taken from a regular sample, in (key, input index) order so that
 // duplicates are spread over buckets like any other key; one partition pass writes every bucket
-// contiguously; then the tile sort and the k-way merge passes run inside every bucket.  A
-// partition pass resolves log2(B) bits of the order in about one read + one write of the keys
-// (plus a read for the histogram), where a merge pass resolves log2(F) = 4: at 2^30 keys the
-// 16 bits of merging above the 16384-key tiles become 9 bits of partition + 7 bits of merging,
-// 2 merge passes instead of 4.
+// contiguously.  A partition pass resolves log2(B) bits of the order in about one read + one
+// write of the keys (plus a read for the histogram).
 //
-// Kernels (all keyed by the composite c = key * 2^32 + input index, unique per key):
-//   bucket_sample_kernel   s regular samples -> composites (sorted by the int64 sort)
-//   bucket_splitter_kernel splitter b = sample (b+1)*s/B - 1; padded with +inf to BP
-//   bucket_hist_kernel     per 65536-key workgroup: keys per bucket (LDS atomics)
-//   bucket_colsum_kernel   per 64 workgroups: column sums        } exclusive scan of the
-//   bucket_scan_kernel     one workgroup: chunk prefixes, bucket   } histograms in (bucket,
-//                          starts, tile table of the tile sort     }  workgroup) order
-//   bucket_offsets_kernel  per-workgroup bucket offsets          }
-//   bucket_scatter_kernel  per 16384-key sub-tile: keys grouped by bucket in LDS, then written
-//                          to their buckets (consecutive lanes on consecutive keys of a bucket)
+// Kernels (all keyed by the composite c = (key, input index), unique per key):
+//   bucket_sample_kernel / pair_*   s regular samples -> composites (sorted by the int64 sort)
+//   bucket_splitter_kernel          splitter b = sample (b+1)*s/B - 1; padded with +inf to BP
+//   bucket_slotmap_kernel           the lookups' slot map (int64: linear or log, one-key slots)
+//   bucket_hist_kernel              per workgroup range: keys per bucket (LDS atomics)
+//   bucket_colsum_kernel            per 64 workgroups: column sums        } exclusive scan of the
+//   bucket_scan_kernel              one workgroup: chunk prefixes, bucket } histograms in (bucket,
+//                                   starts, tile table of the tile sort   }  workgroup) order
+//   bucket_offsets_kernel           per-workgroup bucket offsets          }
+//   bucket_scatter_lines_kernel     per sub-tile: keys grouped by bucket in LDS, every bucket of
+//                                   the workgroup's range written as whole 64-byte lines
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <type_traits>
 
 namespace dsort {
 namespace bk {
@@ -38,7 +38,7 @@ constexpr int BK_CHUNK = 64;             // workgroups per column-sum chunk
 // (int32: 56 KiB next to the 64 KiB line carry of the line scatter; 12 and 13 measured slower).
 template <typename T> struct Geo;
 template <> struct Geo<int32_t> { static constexpr int KPT = 14; };
-template <> struct Geo<int64_t> { static constexpr int KPT = 8; };
+template <> struct Geo<int64_t> { static constexpr int KPT = 6; };  // 48 KiB next to the 64 KiB carry
 
 struct TileRef {
     uint64_t base;   // first key of the tile
@@ -534,113 +534,6 @@ __global__ void __launch_bounds__(BK_MAXB) bucket_offsets_kernel(const uint32_t 
     }
 }
 
-// Per sub-tile (BK_T * KPT keys): every key takes a slot of its bucket (atomic on the sub-tile
-// histogram), which gives both its global position (the bucket's next position in this
-// workgroup's range + slot) and its LDS position in the sub-tile laid out bucket by bucket
-// (scan + slot).  Key and global position go to LDS there; then consecutive threads write
-// consecutive LDS entries, i.e. consecutive keys of a bucket to consecutive addresses.  The order
-// of keys inside a bucket is not kept (the bucket is sorted afterwards; the keys carry no
-// payload).  The next sub-tile's keys are loaded while the current one is placed.
-template <typename T>
-__global__ void __launch_bounds__(BK_T) bucket_scatter_kernel(const T *__restrict__ in, uint64_t n,
-                                                              const typename Comp<T>::C *__restrict__ spl_g,
-                                                              const BkMap *__restrict__ map, int B, int BP, int subs,
-                                                              const uint64_t *__restrict__ offs,
-                                                              T *__restrict__ out, T *__restrict__ out2) {
-    using CT = Comp<T>;
-    constexpr int KPT = Geo<T>::KPT, SUB = BK_T * KPT;
-    __shared__ typename CT::C spl[BK_MAXB];
-    __shared__ uint8_t bpure[BK_MAXB];  // bucket between two splitters of one key: written to out2
-    __shared__ uint32_t rng[BK_SLOTS];
-    __shared__ uint2 sgo[BK_MAXB];       // (sub-tile scan, next global position) per bucket; n < 2^32
-    __shared__ uint32_t hist[BK_MAXB];   // sub-tile histogram
-    __shared__ uint32_t wsum[BK_T / 64];
-    __shared__ T lk[SUB];                // the sub-tile grouped by bucket
-    __shared__ uint32_t lg[SUB];         // global position of every LDS entry
-    for (int b = threadIdx.x; b < B; b += BK_T) sgo[b] = make_uint2(0u, (uint32_t)offs[(uint64_t)blockIdx.x * B + b]);
-    load_splitters<T>(spl_g, BP, spl);
-    const BkMap m = *map;
-    __syncthreads();
-    build_slots<T>(spl, BP, m, rng);
-    for (int b = threadIdx.x; b < B; b += BK_T)
-        bpure[b] = out2 && b > 0 && b + 1 < B && CT::key_of(spl[b - 1]) == CT::key_of(spl[b]);
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint64_t g0 = (uint64_t)blockIdx.x * subs * SUB;
-    T nxt[KPT];
-#pragma unroll
-    for (int k = 0; k < KPT; ++k) {
-        const uint64_t i = g0 + threadIdx.x + (uint64_t)k * BK_T;
-        nxt[k] = i < n ? in[i] : T(0);
-    }
-#pragma unroll 1
-    for (int sub = 0; sub < subs; ++sub) {
-        const uint64_t s0 = g0 + (uint64_t)sub * SUB;
-        if (s0 >= n) break;  // workgroup-uniform
-        for (int b = threadIdx.x; b < B; b += BK_T) hist[b] = 0;
-        __syncthreads();
-        T key[KPT];
-        int bk[KPT];
-        uint32_t slot[KPT];
-#pragma unroll
-        for (int k = 0; k < KPT; ++k) key[k] = nxt[k];
-        uint32_t sl[KPT];
-        slots_at<T, KPT>(m, key, sl);
-        if (sub + 1 < subs) {
-#pragma unroll
-            for (int k = 0; k < KPT; ++k) {
-                const uint64_t i = s0 + SUB + threadIdx.x + (uint64_t)k * BK_T;
-                nxt[k] = i < n ? in[i] : T(0);
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < KPT; ++k) {
-            const uint64_t i = s0 + threadIdx.x + (uint64_t)k * BK_T;
-            bk[k] = -1;
-            if (i < n) {
-                bk[k] = bucket_fast<T>(spl, rng, sl[k], key[k], CT::make(key[k], i));
-                slot[k] = atomicAdd(&hist[bk[k]], 1u);
-            }
-        }
-        __syncthreads();
-        // exclusive scan of the sub-tile histogram (one bucket per thread)
-        const uint32_t hv = threadIdx.x < (unsigned)B ? hist[threadIdx.x] : 0;
-        uint32_t incl = hv;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(incl, o);
-            if (lane >= o) incl += y;
-        }
-        if (lane == 63) wsum[w] = incl;
-        __syncthreads();
-        uint32_t woff = 0;
-        for (int i = 0; i < w; ++i) woff += wsum[i];
-        if (threadIdx.x < (unsigned)B) sgo[threadIdx.x].x = woff + incl - hv;
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < KPT; ++k) {
-            if (bk[k] >= 0) {
-                const uint2 so = sgo[bk[k]];
-                lk[so.x + slot[k]] = key[k];
-                // (bit 31: a pure bucket, to out2; out2 is only given when n < 2^31)
-                lg[so.x + slot[k]] = (so.y + slot[k]) | (uint32_t)bpure[bk[k]] << 31;
-            }
-        }
-        __syncthreads();
-        const uint32_t cnt = s0 + SUB <= n ? SUB : (uint32_t)(n - s0);
-#pragma unroll
-        for (int k = 0; k < KPT; ++k) {
-            const uint32_t p = threadIdx.x + k * BK_T;
-            if (p < cnt) {
-                const uint32_t gp = lg[p];
-                (gp >> 31 ? out2 : out)[gp & 0x7FFFFFFFu] = lk[p];
-            }
-        }
-        // advance every bucket's global position by this sub-tile's keys (sgo.x is not read
-        // again before the next scan, which follows two barriers)
-        if (threadIdx.x < (unsigned)B) sgo[threadIdx.x].y += hv;
-    }
-}
-
-
 // Inclusive sum over a wave (DPP row shifts, then the row broadcasts of lane 15 and 31).
 __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
@@ -652,11 +545,12 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
     return v;
 }
 
-// The int32 scatter with whole-line writes.  Every bucket of a workgroup's range is a stream of
-// aligned 64-byte lines (16 keys): a sub-tile writes only the whole lines of each bucket (the
+// The scatter with whole-line writes (both key widths).  Every bucket of a workgroup's range is a stream of
+// aligned 64-byte lines (16 int32 / 8 int64 keys): a sub-tile writes only the whole lines of each bucket (the
 // bucket's carried keys + its new keys) and carries the rest (< 16 keys per bucket) in LDS to the
 // next sub-tile, so HBM sees whole-line writes only (a per-sub-tile scatter writes each bucket's
-// ~14 keys as a piece of a line the neighbouring sub-tiles complete: partial-line writes).  Only
+// ~14 keys as a piece of a line the neighbouring sub-tiles complete: partial-line writes, 34 % of
+// the int64 scatter's write requests in round 2).  Only
 // the first and last line of each bucket in the workgroup's range can be partial; the first is
 // padded at the front with "phantom" entries up to the line boundary (never written).
 // Per sub-tile, five barriers (round 2 had nine):
@@ -669,28 +563,34 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
 // (Measured and dropped, round 3: a thread per line entry with 4-byte stores, and 16-byte aligned
 // stream regions with 16-byte LDS reads, which need 3 pad entries per bucket and so a 12-key
 // sub-tile per thread: 3.6 ms vs 3.0 ms at 2^30.)
-constexpr int BK_LK = 16;                                       // int32 keys per 64-byte line
-constexpr int BK_LSUB = BK_T * Geo<int32_t>::KPT;               // keys per sub-tile
-constexpr int BK_MAPN = (BK_LSUB + 30 * BK_MAXB) / BK_LK;       // lines per sub-tile, at most
-static __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const int32_t *__restrict__ in, uint64_t n,
-                                                                    const int64_t *__restrict__ spl_g,
+// Line geometry per key width: LK keys per 64-byte line, SUB keys per sub-tile, map entries.
+template <typename T> struct LineGeo {
+    static constexpr int LK = 64 / (int)sizeof(T);                  // keys per 64-byte line
+    static constexpr int KPL = 16 / (int)sizeof(T);                 // keys per 16-byte lane store
+    static constexpr int SUB = BK_T * Geo<T>::KPT;                  // keys per sub-tile
+    static constexpr int MAPN = (SUB + 2 * (LK - 1) * BK_MAXB) / LK; // lines per sub-tile, at most
+};
+template <typename T>
+__global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__restrict__ in, uint64_t n,
+                                                                    const typename Comp<T>::C *__restrict__ spl_g,
                                                                     const BkMap *__restrict__ map, int B, int BP, int subs,
                                                                     const uint64_t *__restrict__ offs,
-                                                                    int32_t *__restrict__ out,
-                                                                    int32_t *__restrict__ out2) {
-    using CT = Comp<int32_t>;
-    constexpr int KPT = Geo<int32_t>::KPT, SUB = BK_LSUB;
-    static_assert(SUB < (1 << 16), "packed scan fields");
-    // (a non-last sub-tile writes <= (SUB + 15 B) / 16 lines, the last <= (SUB + 30 B) / 16)
-    __shared__ int64_t spl[BK_MAXB];
+                                                                    T *__restrict__ out, T *__restrict__ out2) {
+    using CT = Comp<T>;
+    using G = LineGeo<T>;
+    using V = typename std::conditional<sizeof(T) == 4, int4, longlong2>::type;
+    constexpr int KPT = Geo<T>::KPT, SUB = G::SUB, LK = G::LK, KPL = G::KPL;
+    static_assert(SUB + LK < (1 << 16) && LK <= 16, "packed fields");
+    // (a non-last sub-tile writes <= (SUB + (LK-1) B) / LK lines, the last <= (SUB + 2 (LK-1) B) / LK)
+    __shared__ typename CT::C spl[BK_MAXB];
     __shared__ uint32_t rng[BK_SLOTS];
     __shared__ uint32_t hist[BK_MAXB];               // sub-tile histogram, then the LDS starts
     __shared__ uint2 st[BK_MAXB];                    // per bucket: LDS start | first line << 16, vc|ph|pure|L
     __shared__ uint32_t sgb[BK_MAXB];                // per bucket: global index of stream entry 0
-    __shared__ uint16_t lmap[BK_MAPN];               // line -> bucket
+    __shared__ uint16_t lmap[G::MAPN];               // line -> bucket
     __shared__ uint32_t wsum[BK_T / 64];
-    __shared__ int32_t lk[SUB];                      // the sub-tile's new keys grouped by bucket
-    __shared__ int32_t carry[BK_MAXB * BK_LK];       // per bucket: stream entries not yet written (< 16)
+    __shared__ T lk[SUB];                            // the sub-tile's new keys grouped by bucket
+    __shared__ T carry[BK_MAXB * LK];                // per bucket: stream entries not yet written (< LK)
     const int tb = threadIdx.x, lane = tb & 63, w = tb >> 6;
     const uint32_t g = blockIdx.x;
     const bool owner = tb < B;  // thread b owns bucket b's line stream
@@ -700,39 +600,39 @@ static __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const
     if (owner) {
         const uint32_t o = (uint32_t)offs[(uint64_t)g * B + tb];
         pure = out2 && tb > 0 && tb + 1 < B && CT::key_of(spl_g[tb - 1]) == CT::key_of(spl_g[tb]);
-        ph = (uint32_t)(((uintptr_t)((pure ? out2 : out) + o) >> 2) & (BK_LK - 1));
+        ph = (uint32_t)(((uintptr_t)((pure ? out2 : out) + o) / sizeof(T)) & (LK - 1));
         vc = ph;
         gb = o - ph;
         hist[tb] = 0;
     }
-    load_splitters<int32_t>(spl_g, BP, spl);
+    load_splitters<T>(spl_g, BP, spl);
     const BkMap m = *map;
     __syncthreads();
-    build_slots<int32_t>(spl, BP, m, rng);
+    build_slots<T>(spl, BP, m, rng);
     __syncthreads();
     const uint64_t g0 = (uint64_t)g * subs * SUB;
-    int32_t nxt[KPT];
+    T nxt[KPT];
 #pragma unroll
     for (int k = 0; k < KPT; ++k) {
         const uint64_t i = g0 + tb + (uint64_t)k * BK_T;
-        nxt[k] = i < n ? in[i] : 0;
+        nxt[k] = i < n ? in[i] : T(0);
     }
 #pragma unroll 1
     for (int sub = 0; sub < subs; ++sub) {
         const uint64_t s0 = g0 + (uint64_t)sub * SUB;
         if (s0 >= n) break;  // workgroup-uniform
         const bool last = sub + 1 == subs || s0 + SUB >= n;
-        int32_t key[KPT];
+        T key[KPT];
         uint32_t pk[KPT];  // rank | bucket << 16; ~0 past the input
 #pragma unroll
         for (int k = 0; k < KPT; ++k) key[k] = nxt[k];
         uint32_t sl[KPT];
-        slots_at<int32_t, KPT>(m, key, sl);
+        slots_at<T, KPT>(m, key, sl);
         if (!last) {
 #pragma unroll
             for (int k = 0; k < KPT; ++k) {
                 const uint64_t i = s0 + SUB + tb + (uint64_t)k * BK_T;
-                nxt[k] = i < n ? in[i] : 0;
+                nxt[k] = i < n ? in[i] : T(0);
             }
         }
 #pragma unroll
@@ -740,7 +640,7 @@ static __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const
             const uint64_t i = s0 + tb + (uint64_t)k * BK_T;
             pk[k] = ~0u;
             if (i < n) {
-                const int b = bucket_fast<int32_t>(spl, rng, sl[k], key[k], CT::make(key[k], i));
+                const int b = bucket_fast<T>(spl, rng, sl[k], key[k], CT::make(key[k], i));
                 pk[k] = atomicAdd(&hist[b], 1u) | (uint32_t)b << 16;
             }
         }
@@ -748,7 +648,7 @@ static __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const
         // owner: new keys, whole lines to write, entries carried to the next sub-tile
         const uint32_t hv = owner ? hist[tb] : 0;
         const uint32_t L = vc + hv;  // stream entries not yet written
-        const uint32_t nl = !owner ? 0 : last ? (L > ph ? (L + BK_LK - 1) / BK_LK : 0) : L / BK_LK;
+        const uint32_t nl = !owner ? 0 : last ? (L > ph ? (L + LK - 1) / LK : 0) : L / LK;
         const uint32_t pv = hv | nl << 16;
         const uint32_t incl = wave_incl_sum(pv);
         if (lane == 63) wsum[w] = incl;
@@ -774,42 +674,44 @@ static __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const
             if (pk[k] != ~0u) lk[hist[pk[k] >> 16] + (pk[k] & 0xFFFF)] = key[k];
         __syncthreads();  // D
         if (owner) hist[tb] = 0;  // (the next sub-tile's atomics follow barrier E)
-        // whole lines: 4 lanes per line, 4 keys (16 bytes) per lane
+        // whole lines: 4 lanes per line, 16 bytes per lane
         for (uint32_t it = tb; it < 4 * C; it += BK_T) {
             const uint32_t j = it >> 2, q = it & 3;
             const uint32_t b = lmap[j];
             const uint2 sb = st[b];
             const uint32_t cv = sb.y & 31, cp = (sb.y >> 5) & 31, cL = sb.y >> 11, lb = sb.x & 0xFFFF;
-            const uint32_t e0 = (j - (sb.x >> 16)) * BK_LK + 4 * q;
-            int32_t v[4];
-            bool ok[4];
+            const uint32_t e0 = (j - (sb.x >> 16)) * LK + KPL * q;
+            T v[KPL];
+            bool ok[KPL];
             bool full = true;
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
+            for (int t = 0; t < KPL; ++t) {
                 const uint32_t e = e0 + t;
                 ok[t] = e >= cp && e < cL;
                 full = full && ok[t];
-                v[t] = e < cv ? carry[b * BK_LK + e] : lk[lb + e - cv];
+                v[t] = e < cv ? carry[b * LK + e] : lk[lb + e - cv];
             }
             const uint32_t gi = sgb[b] + e0;  // mod 2^32
-            int32_t *tgt = (sb.y >> 10) & 1 ? out2 : out;
+            T *tgt = (sb.y >> 10) & 1 ? out2 : out;
             if (full) {
-                *reinterpret_cast<int4 *>(tgt + gi) = make_int4(v[0], v[1], v[2], v[3]);
+                V vv;
+                __builtin_memcpy(&vv, v, sizeof(V));
+                *reinterpret_cast<V *>(tgt + gi) = vv;
             } else {
 #pragma unroll
-                for (int t = 0; t < 4; ++t)
+                for (int t = 0; t < KPL; ++t)
                     if (ok[t]) tgt[(uint32_t)(gi + t)] = v[t];
             }
         }
         if (last) break;
         __syncthreads();  // E
-        // carry the tail of every stream: entries [16 nl, L) -> carry[0, L - 16 nl) (the entries
+        // carry the tail of every stream: entries [LK nl, L) -> carry[0, L - LK nl) (the entries
         // below vc of a stream that wrote no line are there already)
         if (owner) {
-            const uint32_t nv = L - nl * BK_LK;
-            for (uint32_t e2 = nl ? 0 : vc; e2 < nv; ++e2) carry[tb * BK_LK + e2] = lk[lks + nl * BK_LK + e2 - vc];
+            const uint32_t nv = L - nl * LK;
+            for (uint32_t e2 = nl ? 0 : vc; e2 < nv; ++e2) carry[tb * LK + e2] = lk[lks + nl * LK + e2 - vc];
             if (nl) ph = 0;
-            gb += nl * BK_LK;
+            gb += nl * LK;
             vc = nv;
         }
     }

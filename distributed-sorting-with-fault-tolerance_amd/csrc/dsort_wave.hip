@@ -1813,13 +1813,8 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
     // second level runs (it skips them) and d_keys is not the input the scatter still reads.
     T *direct = sub_keys<T>(ctx) && (const void *)d_in != (const void *)d_keys && n < (1ull << 31) ? d_keys : nullptr;
     if ((rc = stage_event(ctx, s, timed, 11))) return rc;
-    if constexpr (std::is_same<T, int32_t>::value) {
-        hipLaunchKernelGGL(bucket_scatter_lines_kernel, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl,
-                           map, B, BP, subs, offs, part_out, direct);
-    } else {
-        hipLaunchKernelGGL(bucket_scatter_kernel<T>, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, map,
-                           B, BP, subs, offs, part_out, direct);
-    }
+    hipLaunchKernelGGL(bucket_scatter_lines_kernel<T>, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, map,
+                       B, BP, subs, offs, part_out, direct);
     DSORT_HIP(ctx, hipGetLastError());
     if ((rc = stage_event(ctx, s, timed, 12))) return rc;
     fault_point(ctx, s, 0);  // first-level partition done
