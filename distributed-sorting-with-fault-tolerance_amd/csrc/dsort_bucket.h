@@ -26,6 +26,8 @@
 
 #include <type_traits>
 
+#include "dsort_internal.h"
+
 namespace dsort {
 namespace bk {
 
@@ -441,6 +443,7 @@ static __global__ void __launch_bounds__(BK_MAXB) bucket_colsum_kernel(const uin
     const uint32_t g0 = blockIdx.x * BK_CHUNK;
     const uint32_t g1 = g0 + BK_CHUNK < G ? g0 + BK_CHUNK : G;
     uint64_t sum = 0;
+#pragma unroll 8
     for (uint32_t g = g0; g < g1; ++g) sum += counts[(uint64_t)g * B + b];
     part[(uint64_t)blockIdx.x * B + b] = sum;
 }
@@ -490,10 +493,18 @@ static __global__ void __launch_bounds__(BK_MAXB) bucket_scan_kernel(uint64_t *_
     const int b = threadIdx.x;
     uint64_t tot = 0;
     if (b < B) {
-        for (uint32_t c = 0; c < nchunk; ++c) {
-            const uint64_t v = part[(uint64_t)c * B + b];
-            part[(uint64_t)c * B + b] = tot;
-            tot += v;
+        // column b's chunk sums -> exclusive prefixes, 8 loads in flight at a time (a serial chain
+        // of dependent round trips took 92 us per sort at 2^30)
+        constexpr uint32_t U = 8;
+        for (uint32_t c0 = 0; c0 < nchunk; c0 += U) {
+            uint64_t v[U];
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) v[u] = c0 + u < nchunk ? part[(uint64_t)(c0 + u) * B + b] : 0;
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) {
+                if (c0 + u < nchunk) part[(uint64_t)(c0 + u) * B + b] = tot;
+                tot += v[u];
+            }
         }
     }
     uint64_t allk, allt;
@@ -528,22 +539,13 @@ __global__ void __launch_bounds__(BK_MAXB) bucket_offsets_kernel(const uint32_t 
     const uint32_t g0 = blockIdx.x * BK_CHUNK;
     const uint32_t g1 = g0 + BK_CHUNK < G ? g0 + BK_CHUNK : G;
     uint64_t run = bstart[b] + part[(uint64_t)blockIdx.x * B + b];
+#pragma unroll 8
     for (uint32_t g = g0; g < g1; ++g) {
         offs[(uint64_t)g * B + b] = (O)run;
         run += counts[(uint64_t)g * B + b];
     }
 }
 
-// Inclusive sum over a wave (DPP row shifts, then the row broadcasts of lane 15 and 31).
-__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
-    return v;
-}
 
 // The scatter with whole-line writes (both key widths).  Every bucket of a workgroup's range is a stream of
 // aligned 64-byte lines (16 int32 / 8 int64 keys): a sub-tile writes only the whole lines of each bucket (the

@@ -143,6 +143,17 @@ struct dsort_ctx {
 
 namespace dsort {
 
+// Inclusive sum over a wave (DPP row shifts, then the row broadcasts of lane 15 and 31).
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    return v;
+}
+
 int set_err(dsort_ctx *ctx, int code, const std::string &msg);
 // the stream argument of the C-ABI: NULL = the context's stream, DSORT_NULL_STREAM = stream 0
 hipStream_t pick_stream(dsort_ctx *ctx, void *stream);

@@ -142,6 +142,7 @@ template <typename T>
 __global__ void __launch_bounds__(SB_T) sb_sample_kernel(const T *__restrict__ src, const BInfo *__restrict__ bi,
                                                          T *__restrict__ smp, int64_t *__restrict__ cmp) {
     const BInfo b = bi[blockIdx.x];
+#pragma unroll 4  // (independent gathers in flight)
     for (uint32_t k = threadIdx.x; k < b.ns; k += SB_T) {
         const T key = src[sample_pos(b, k)];
         const uint64_t g = b.soff + k;
@@ -288,11 +289,7 @@ __global__ void __launch_bounds__(SB_T) sb_hist_kernel(const T *__restrict__ src
 // exclusive scan over a SB_MAXS-thread workgroup (one value per thread); `all` = total
 __device__ __forceinline__ uint32_t scan_excl_1024(uint32_t v, uint32_t *wsum, uint32_t &all) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint32_t incl = v;
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o);
-        if (lane >= o) incl += y;
-    }
+    uint32_t incl = wave_incl_sum(v);
     __syncthreads();
     if (lane == 63) wsum[w] = incl;
     __syncthreads();
@@ -364,8 +361,10 @@ __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restric
         }
     };
     uint32_t tot = 0;
-    if (j < ns)
+    if (j < ns) {
+#pragma unroll 8  // (independent loads in flight: the loop is latency-bound)
         for (uint32_t c = b.c0; c < b.c1; ++c) tot += cnt(c);
+    }
     uint32_t all;
     const uint32_t ex = scan_excl_1024(tot, wsum, all);
     const uint32_t st = (uint32_t)b.start + ex;
@@ -555,11 +554,7 @@ __global__ void __launch_bounds__(SB_LT, 4) sb_local_kernel(T *__restrict__ buf,
         h[q] = hist[PER * tid + q];
         sum += h[q];
     }
-    uint32_t incl = sum;
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o);
-        if (lane >= o) incl += y;
-    }
+    uint32_t incl = wave_incl_sum(sum);
     if (lane == 63) wsum[w] = incl;
     __syncthreads();
     SBST(2);
@@ -671,11 +666,7 @@ __global__ void __launch_bounds__(SB_T) sb_scatter_kernel(const T *__restrict__ 
             h[q] = hist[4 * tid + q];
             sum += h[q];
         }
-        uint32_t incl = sum;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(incl, o);
-            if (lane >= o) incl += y;
-        }
+        uint32_t incl = wave_incl_sum(sum);
         if (lane == 63) wsum[w] = incl;
         __syncthreads();
         uint32_t ex = incl - sum;

@@ -90,11 +90,7 @@ __device__ uint64_t lookback(uint64_t *status, uint32_t id, uint64_t agg) {
 // Exclusive scan of one value per thread over the 256-thread workgroup; `agg` = total.
 __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t *wsum, uint32_t &agg) {
     const int lane = lane_id(), w = threadIdx.x >> 6;
-    uint32_t incl = v;
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o);
-        if (lane >= o) incl += y;
-    }
+    uint32_t incl = wave_incl_sum(v);
     if (lane == 63) wsum[w] = incl;
     __syncthreads();
     uint32_t woff = 0;

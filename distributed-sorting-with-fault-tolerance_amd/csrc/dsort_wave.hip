@@ -766,6 +766,7 @@ __device__ __forceinline__ bool bin_sort_tile(const T (&x)[R], int valid, T *s, 
         sm.mx[w] = mx;
     }
     __syncthreads();  // (also: every lane's gather is done with the piece table in cw)
+    STAMP(2);
     uint4 *c4 = reinterpret_cast<uint4 *>(cw) + tid;  // this thread's bins [8 tid, 8 tid + 8)
     *c4 = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
@@ -800,18 +801,14 @@ __device__ __forceinline__ bool bin_sort_tile(const T (&x)[R], int valid, T *s, 
         bin_count(x, mn, bm, cw);
     }
     __syncthreads();
+    STAMP(3);
     // 3. starts
     uint4 cv = *c4;
     uint32_t wd[4] = {cv.x, cv.y, cv.z, cv.w};
     uint32_t tot = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) tot += (wd[k] & 0xFFFFu) + (wd[k] >> 16);
-    uint32_t incl = tot;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o);
-        if (lane >= o) incl += y;
-    }
+    uint32_t incl = wave_incl_sum(tot);
     if (lane == 63) sm.wsum[w] = incl;
     __syncthreads();
     uint32_t run = incl - tot, M = 0;
@@ -829,6 +826,7 @@ __device__ __forceinline__ bool bin_sort_tile(const T (&x)[R], int valid, T *s, 
     }
     *c4 = make_uint4(wd[0], wd[1], wd[2], wd[3]);
     __syncthreads();  // (also: sm, in s, is dead from here)
+    STAMP(4);
     // 4. keys to their places
     // (mn through an opaque copy: the bins are recomputed here, not kept in registers across
     // the scan, where they would spill)
@@ -840,11 +838,14 @@ __device__ __forceinline__ bool bin_sort_tile(const T (&x)[R], int valid, T *s, 
         bin_place(x, mn, bm, cw, s);
     }
     __syncthreads();
+    STAMP(5);
     // 5. window passes; a descent can only be left at a boundary of the last pass's windows
     window_pass<0, false>(s, (int)M, tid);
     __syncthreads();
+    STAMP(6);
     window_pass<8, true>(s, (int)M, tid);
     __syncthreads();
+    STAMP(7);
     const int e8 = 16 * tid + 8;
     if (block_or<WAVES>(e8 < (int)M && s[bsw<T>(e8 - 1)] > s[bsw<T>(e8)], cw)) {  // (cw is dead from step 5)
         window_pass<0, true>(s, (int)M, tid);
@@ -858,8 +859,10 @@ __device__ __forceinline__ bool bin_sort_tile(const T (&x)[R], int valid, T *s, 
     // partial writes, 14 % of the written bytes)
     constexpr int LK = 128 / (int)sizeof(T);
     const int m = (int)((reinterpret_cast<uintptr_t>(out) / sizeof(T)) & (LK - 1));
+    STAMP(8);
     for (int i = tid - m; i < valid; i += THREADS)
         if (i >= 0) out[i] = (uint32_t)i < M ? s[bsw<T>(i)] : key_max<T>();
+    STAMP(9);
     return true;
 }
 
@@ -901,11 +904,7 @@ __device__ __forceinline__ void gather_tile(const sb::Gather &ga, const sb::GTil
         }
     }
     const uint32_t sum = len[0] + len[1];
-    uint32_t incl = sum;
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o);
-        if (lane >= o) incl += y;
-    }
+    uint32_t incl = wave_incl_sum(sum);
     if (lane == 63) wsum[w] = incl;
     __syncthreads();
     uint32_t ex = incl - sum;
@@ -1025,8 +1024,10 @@ __global__ void __launch_bounds__(64 * WG<T>::WAVES, WG<T>::OCC) bin_sort_kernel
     // of every chunk: run on one XCD at about the same time, such a line comes from HBM once and
     // from that XCD's L2 the second time.
     const uint32_t j = GATHER ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    STAMP(0);
     if (!load_tile<T, GATHER>(in, n, tiles, ntiles, ga, j, cw, reinterpret_cast<uint32_t *>(s), x, base, valid))
         return;
+    STAMP(1);
     if (valid == 0) return;
     // a duplicate run inside a gathered tile shows as two equal neighbouring splitters
     bool hint = false;

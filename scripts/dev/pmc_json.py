@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
-"""profiles/r2_pmc_traffic.json from the rocprofv3 databases of scripts/gpu_profile_r2.sh: per
+"""profiles/r<N>_pmc_traffic.json from the rocprofv3 databases of scripts/gpu_profile_r<N>.sh: per
 kernel and launch, HBM traffic = (2 x FETCH_SIZE + WRITE_SIZE) x 1 KiB (FETCH_SIZE doubled: the
 gfx950 correction of MI355X_MICROARCH.md § HBM), for the 2^30 int32 sort; the int64 Zipf sort's
-figures under "int64"."""
+figures under "int64".   pmc_json.py OUT.json [TAG32 TAG64]   (default tags i32_ i64_)"""
 import glob
 import json
 import sqlite3
@@ -24,16 +24,21 @@ def per_launch(tag):
             rec = {"fetch_kib": d["FETCH_SIZE"], "write_kib": d["WRITE_SIZE"],
                    "traffic_bytes_per_launch": int((2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024)}
             for extra in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_WAIT_INST_LDS",
-                          "TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum"):
+                          "SQ_LDS_IDX_ACTIVE", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY",
+                          "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_INSTS_VMEM_WR", "SQ_INSTS_VMEM_RD",
+                          "TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum", "TCC_EA0_RDREQ_sum"):
                 if extra in d:
                     rec[extra] = d[extra]
             res[k] = rec
     return res
 
 
-doc = {"source": "rocprofv3 --pmc (separate passes) over scripts/dev/ktime.py --reps 1, 2^30 keys",
-       "keys": 1 << 30, "key_bytes": 4, "kernels": per_launch("i32_"),
-       "int64": {"keys": 1 << 30, "key_bytes": 8, "dist": "zipf", "kernels": per_launch("i64_")}}
+t32 = sys.argv[2] if len(sys.argv) > 2 else "i32_"
+t64 = sys.argv[3] if len(sys.argv) > 3 else "i64_"
+doc = {"source": "rocprofv3 --pmc (separate passes, scripts/dev/pmc_sub.sh) over scripts/dev/ktime.py --reps 1, "
+                 "2^30 keys; converted by scripts/dev/pmc_json.py",
+       "keys": 1 << 30, "key_bytes": 4, "kernels": per_launch(t32),
+       "int64": {"keys": 1 << 30, "key_bytes": 8, "dist": "zipf", "kernels": per_launch(t64)}}
 json.dump(doc, open(sys.argv[1] if len(sys.argv) > 1 else "profiles/r2_pmc_traffic.json", "w"), indent=1)
 for t, ks in (("int32", doc["kernels"]), ("int64", doc["int64"]["kernels"])):
     for k, r in ks.items():

@@ -10,4 +10,5 @@ for set in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE
            "WRITE_SIZE" "FETCH_SIZE"; do
   i=$((i+1))
   timeout -s KILL 90 rocprofv3 --pmc $set -d $R/gpurun_out/${TAG}pmc$i -o run -- python3 $R/scripts/dev/ktime.py $ARGS > $R/gpurun_out/${TAG}pmc$i.log 2>&1 || exit $?
+  echo "pmc pass $i ok"
 done
