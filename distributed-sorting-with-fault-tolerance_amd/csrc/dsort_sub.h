@@ -125,11 +125,15 @@ __device__ __forceinline__ int sub_pick(const Spl<T> *spl, uint32_t r, const Spl
 template <typename T>
 __device__ __forceinline__ int sub_of(const Spl<T> *spl, const uint32_t *rng, T klo, uint32_t sh, T key,
                                       uint32_t pos) {
-    // the first two splitters of the slot without a branch (the table holds SB_MAXS + 1 entries,
-    // so the reads stay inside it), then the rare crowded slot
+    // the slot's first two splitters, read only by the lanes whose slot holds them (a slot holds
+    // none in about 60 % of the keys' cases at 2^30 uniform: fewer lanes in every random LDS read,
+    // fewer bank conflicts), then the rare crowded slot
     const uint32_t r = rng[slot_of<T>(key, klo, sh)];
-    const int lo = (int)(r & 0xFFFF);
-    return sub_pick<T>(spl, r, spl[lo], spl[lo + 1], key, pos);
+    const int lo = (int)(r & 0xFFFF), hi = (int)(r >> 16);
+    Spl<T> a{}, b{};
+    if (lo < hi) a = spl[lo];
+    if (lo + 1 < hi) b = spl[lo + 1];
+    return sub_pick<T>(spl, r, a, b, key, pos);
 }
 
 // Sample g (global index, bucket b's samples at [soff, soff + ns)) = the key at position
@@ -316,9 +320,11 @@ struct Ovf {
 // A tile of the local-partition path: sub-buckets [j0, j1) of bucket b, `valid` keys, output
 // position `base`; the tile sort gathers one piece per chunk of the bucket.
 struct GTile {
-    uint64_t base;
+    uint64_t base;         // output position
+    uint64_t src;          // first key of the bucket's first chunk (chunk c0 + k at src + k * SB_LCH)
     uint32_t valid, b, j0, j1;
-    uint64_t pad;
+    uint32_t c0, nch;      // the bucket's chunks [c0, c0 + nch)
+    uint32_t nsub, pad;    // the bucket's sub-buckets
 };
 
 // What the gathering tile sort needs (block_sort_w_kernel<T, true>): its tiles, the chunk and
@@ -330,6 +336,8 @@ struct Gather {
     const uint32_t *pref;
     int SS;
     const void *spl;  // the splitters (Spl<T>, SS per bucket): equal neighbours = a duplicate run
+    const void *bspl; // the first level's splitters (bk::Comp<T>::C, B - 1): a bucket's key bounds
+    int B;
 };
 
 // LOCAL: the chunk histograms are the prefix tables of sb_local_kernel (pref[c][j+1] -
@@ -424,7 +432,7 @@ __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restric
         const uint32_t p = ss[i0], len = ss[i1] - p;
         uint32_t k = tbase + tex;
         if constexpr (LOCAL) {
-            static_cast<GTile *>(tiles)[k] = GTile{p, len, blockIdx.x, i0, i1, 0};
+            static_cast<GTile *>(tiles)[k] = GTile{p, b.start, len, blockIdx.x, i0, i1, b.c0, b.c1 - b.c0, b.nsub, 0};
         } else {
             bk::TileRef *tt = static_cast<bk::TileRef *>(tiles);
             if (!over) {
@@ -533,8 +541,11 @@ __global__ void __launch_bounds__(SB_LT, 4) sb_local_kernel(T *__restrict__ buf,
 #pragma unroll
         for (int u = 0; u < G; ++u)
             if (g0 + u < KPT) {
-                sa[u] = spl[r[u] & 0xFFFF];
-                sb[u] = spl[(r[u] & 0xFFFF) + 1];
+                const uint32_t lo = r[u] & 0xFFFF, hi = r[u] >> 16;
+                sa[u] = Spl<T>{};
+                sb[u] = Spl<T>{};
+                if (lo < hi) sa[u] = spl[lo];
+                if (lo + 1 < hi) sb[u] = spl[lo + 1];
             }
 #pragma unroll
         for (int u = 0; u < G; ++u)

@@ -744,36 +744,39 @@ __device__ __forceinline__ void window_pass(T *s, int M, int tid) {
 // cw holds the counters (NB / 2 words); the caller has passed a barrier since its last use.
 template <typename T>
 __device__ __forceinline__ bool bin_sort_tile(const T (&x)[R], int valid, T *s, uint32_t *cw, T *out,
-                                              bool hot_hint, const int tid) {
+                                              bool hot_hint, bool known, T klo, T khi, const int tid) {
     using U = typename sb::KeyU<T>::U;
     constexpr int WAVES = WG<T>::WAVES, THREADS = 64 * WAVES, NB = BIN_NB<T>;
     constexpr int BPT = NB / THREADS;
     static_assert(BPT == 8, "one 16-byte word of counters per thread");
     BinSm<T> &sm = *reinterpret_cast<BinSm<T> *>(s);
     const int lane = tid & 63, w = tid >> 6;
-    // 1. range
-    T mn = key_max<T>(), mx = key_min<T>();
+    // 1. range: the caller's bounds, or a reduction over the keys (which waits for all of them)
+    T mn = klo, mx = khi;
+    uint4 *c4 = reinterpret_cast<uint4 *>(cw) + tid;  // this thread's bins [8 tid, 8 tid + 8) (zeroed)
+    if (!known) {
+        mn = key_max<T>();
+        mx = key_min<T>();
 #pragma unroll
-    for (int i = 0; i < R; ++i) {
-        mn = x[i] < mn ? x[i] : mn;
-        const T xm = x[i] == key_max<T>() ? key_min<T>() : x[i];
-        mx = xm > mx ? xm : mx;
+        for (int i = 0; i < R; ++i) {
+            mn = x[i] < mn ? x[i] : mn;
+            const T xm = x[i] == key_max<T>() ? key_min<T>() : x[i];
+            mx = xm > mx ? xm : mx;
+        }
+        mn = wave_min(mn);
+        mx = wave_max(mx);
+        if (lane == 0) {
+            sm.mn[w] = mn;
+            sm.mx[w] = mx;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < WAVES; ++i) {
+            mn = sm.mn[i] < mn ? sm.mn[i] : mn;
+            mx = sm.mx[i] > mx ? sm.mx[i] : mx;
+        }
     }
-    mn = wave_min(mn);
-    mx = wave_max(mx);
-    if (lane == 0) {
-        sm.mn[w] = mn;
-        sm.mx[w] = mx;
-    }
-    __syncthreads();  // (also: every lane's gather is done with the piece table in cw)
     STAMP(2);
-    uint4 *c4 = reinterpret_cast<uint4 *>(cw) + tid;  // this thread's bins [8 tid, 8 tid + 8)
-    *c4 = make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-    for (int i = 0; i < WAVES; ++i) {
-        mn = sm.mn[i] < mn ? sm.mn[i] : mn;
-        mx = sm.mx[i] > mx ? sm.mx[i] : mx;
-    }
     if (mx < mn || (mn == key_max<T>())) {  // every key is key_max
         for (int i = tid; i < valid; i += THREADS) out[i] = key_max<T>();
         return true;
@@ -789,10 +792,12 @@ __device__ __forceinline__ bool bin_sort_tile(const T (&x)[R], int valid, T *s, 
         const float f = (float)NB * 4294967296.0f * (1.0f - 0x1p-20f) * __builtin_amdgcn_rcpf(den);
         bm.scale = f >= 4294967040.0f ? 0xFFFFFFFFu : (uint32_t)f;
     }
+    // a duplicate run (8 or more of a wave's first keys in one bin): aggregated atomics, decided
+    // per wave (no barrier: the other keys may still be on their way)
     const bool act0 = x[0] != key_max<T>();
     const uint32_t bx = bm((U)x[0] - (U)mn);
     const uint32_t bf = (uint32_t)__builtin_amdgcn_readfirstlane((int)bx);
-    const bool hot = block_or<WAVES>(hot_hint || (lane == 0 && __popcll(__ballot(act0 && bx == bf)) >= 8), sm.flag);
+    const bool hot = hot_hint || __popcll(__ballot(act0 && bx == bf)) >= 8;
     // 2. counting
     if (hot || !BIN_BATCH<T>) {
 #pragma unroll
@@ -886,8 +891,9 @@ __device__ __forceinline__ void gather_tile(const sb::Gather &ga, const sb::GTil
     constexpr int WAVES = WG<T>::WAVES, THREADS = 64 * WAVES;
     static_assert(2 * THREADS >= kMaxPieces<T> + 1, "two pieces per thread");
     uint32_t *psrc = poff + kMaxPieces<T> + 1;  // kMaxPieces sources after kMaxPieces + 1 offsets
-    const sb::BInfo b = ga.bi[gt.b];
-    const int np = (int)(b.c1 - b.c0);
+    // (the GTile carries the chunk range and the bucket's start: the prefix tables are the only
+    // reads between the tile record and the keys)
+    const int np = (int)gt.nch;
     const int lane = tid & 63, w = tid >> 6;
     uint32_t len[2], src[2];
 #pragma unroll
@@ -896,11 +902,11 @@ __device__ __forceinline__ void gather_tile(const sb::Gather &ga, const sb::GTil
         len[q] = 0;
         src[q] = 0;
         if (k < np) {
-            const uint32_t c = b.c0 + (uint32_t)k;
+            const uint32_t c = gt.c0 + (uint32_t)k;
             const uint32_t *pc = ga.pref + (uint64_t)c * (ga.SS + 1);
             const uint32_t lo = pc[gt.j0];
             len[q] = pc[gt.j1] - lo;
-            src[q] = (uint32_t)ga.ch[c].start + lo;
+            src[q] = (uint32_t)gt.src + (uint32_t)k * (uint32_t)sb::SB_LCH<T> + lo;
         }
     }
     const uint32_t sum = len[0] + len[1];
@@ -1013,34 +1019,59 @@ __global__ void __launch_bounds__(64 * WG<T>::WAVES, WG<T>::OCC) bin_sort_kernel
                                                                      const uint4 *tiles, const uint32_t *ntiles,
                                                                      sb::Gather ga, uint32_t *fb, uint32_t *nfb) {
     constexpr int TILE = TILE_OF<T>;
-    static_assert(BIN_NB<T> / 2 >= 2 * kMaxPieces<T> + 1, "the piece table fits in the counters");
+    static_assert(128 + 2 * kMaxPieces<T> + 1 <= TILE * (int)sizeof(T) / 4, "the piece table fits in the tile");
     __shared__ __attribute__((aligned(16))) T s[TILE];
     __shared__ __attribute__((aligned(16))) uint32_t cw[BIN_NB<T> / 2];
+    // the counters are zeroed before the gather's barriers; the piece table of a gathered tile and
+    // its scan words live in the tile array (free until the keys are placed), past BinSm
+    reinterpret_cast<uint4 *>(cw)[threadIdx.x] = make_uint4(0u, 0u, 0u, 0u);
+    uint32_t *s32 = reinterpret_cast<uint32_t *>(s);
     T x[R];
     uint64_t base;
     int valid;
-    // Gathered tiles: each XCD takes a contiguous block of tiles (workgroups are dealt round-robin
-    // over the 8 XCDs).  Consecutive tiles of a bucket end and start inside the same 128-byte lines
-    // of every chunk: run on one XCD at about the same time, such a line comes from HBM once and
-    // from that XCD's L2 the second time.
-    const uint32_t j = GATHER ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
     STAMP(0);
-    if (!load_tile<T, GATHER>(in, n, tiles, ntiles, ga, j, cw, reinterpret_cast<uint32_t *>(s), x, base, valid))
-        return;
-    STAMP(1);
-    if (valid == 0) return;
-    // a duplicate run inside a gathered tile shows as two equal neighbouring splitters
-    bool hint = false;
+    bool hint = false, known = false;
+    T klo = T(0), khi = T(0);
+    uint32_t j;
     if constexpr (GATHER) {
+        // Gathered tiles: each XCD takes a contiguous block of tiles (workgroups are dealt
+        // round-robin over the 8 XCDs).  Consecutive tiles of a bucket end and start inside the
+        // same 128-byte lines of every chunk: run on one XCD at about the same time, such a line
+        // comes from HBM once and from that XCD's L2 the second time.
+        j = xcd_block(blockIdx.x, gridDim.x);
+        if (j >= *ntiles) return;
         const sb::GTile gt = ga.tiles[j];
+        base = gt.base;
+        valid = (int)gt.valid;
+        if (valid == 0) return;
+        // The tile's key range from the splitters around it (read with the prefix tables, before
+        // the keys): sub-buckets [j0, j1) of bucket b hold keys in [spl[j0 - 1], spl[j1 - 1]], a
+        // bucket's bounds are the first level's splitters b - 1 and b.  Known bounds let the
+        // counting start on the first keys that arrive, with no reduction and no barrier between
+        // the loads and the counting; only the first tile of bucket 0 and the last of bucket B - 1
+        // reduce over their keys.
         const sb::Spl<T> *sp = static_cast<const sb::Spl<T> *>(ga.spl) + (uint64_t)gt.b * ga.SS;
+        const auto *bs = static_cast<const typename bk::Comp<T>::C *>(ga.bspl);
+        const bool lk = gt.j0 > 0 || gt.b > 0, hk = gt.j1 < gt.nsub || (int)gt.b + 1 < ga.B;
+        known = lk && hk;
+        if (known) {
+            klo = gt.j0 > 0 ? sp[gt.j0 - 1].k : bk::Comp<T>::key_of(bs[gt.b - 1]);
+            khi = gt.j1 < gt.nsub ? sp[gt.j1 - 1].k : bk::Comp<T>::key_of(bs[gt.b]);
+        }
+        // a duplicate run inside a gathered tile shows as two equal neighbouring splitters
         const int jl = gt.j0 > 0 ? (int)gt.j0 - 1 : 0, jh = (int)gt.j1 - 1;  // splitters around the tile
-        const int nspl = (int)ga.bi[gt.b].nsub - 1;
-        const int j = jl + lane_id();
-        if (j < jh && j + 1 < nspl) hint = sp[j].k == sp[j + 1].k;
+        const int nspl = (int)gt.nsub - 1;
+        const int jj = jl + lane_id();
+        if (jj < jh && jj + 1 < nspl) hint = sp[jj].k == sp[jj + 1].k;
         hint = __ballot(hint) != 0;
+        gather_tile<T>(ga, gt, in, s32 + 128, s32 + 96, x, threadIdx.x);
+    } else {
+        j = blockIdx.x;
+        if (!load_tile<T, false>(in, n, tiles, ntiles, ga, j, nullptr, nullptr, x, base, valid)) return;
+        if (valid == 0) return;
     }
-    if (!bin_sort_tile<T>(x, valid, s, cw, out + base, hint, threadIdx.x) && threadIdx.x == 0)
+    STAMP(1);
+    if (!bin_sort_tile<T>(x, valid, s, cw, out + base, hint, known, klo, khi, threadIdx.x) && threadIdx.x == 0)
         fb[atomicAdd(nfb, 1u)] = j;
 }
 
@@ -1486,7 +1517,7 @@ static std::vector<size_t> sub_tile_runs(uint64_t p, uint64_t len, uint64_t tile
 // locally partitioned keys, if the local pass already ran: still the same buckets).
 template <typename T>
 static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_t *hb, int B, uint64_t m,
-                    hipStream_t s, bool timed, bool local, const uint8_t *pure, bool pure_done) {
+                    hipStream_t s, bool timed, bool local, const uint8_t *pure, bool pure_done, const void *bspl) {
     using namespace sb;
     constexpr int TILE = TILE_OF<T>;
     constexpr uint64_t ALIGN = KPC<T>;
@@ -1627,13 +1658,13 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         // more in empty workgroups than this wait -- measured 10.6 vs 10.1 ms)
         DSORT_HIP(ctx, hipEventSynchronize(ctx->sub_ev));
         const uint32_t ntiles = hn[0], novf = hn[1];
-        if (novf) return sub_sort<T>(ctx, src, d_keys, n, hb, B, m, s, timed, false, pure, pure_done);
+        if (novf) return sub_sort<T>(ctx, src, d_keys, n, hb, B, m, s, timed, false, pure, pure_done, bspl);
         if (ntiles > tmax) return set_err(ctx, DSORT_EHIP, "sub-bucket packing overflow");
         fault_point(ctx, s, 1);  // second-level partition done
         ctx->stats.merge_passes = 0;
         // 3. tile sort: gathered from the chunks into d_keys
         if (ntiles) {
-            const Gather ga{static_cast<const GTile *>(tt), dch, dbi, cnt, SS, spl};
+            const Gather ga{static_cast<const GTile *>(tt), dch, dbi, cnt, SS, spl, bspl, B};
             rc = tile_sort<T, true>(ctx, src, d_keys, n, nullptr, num, ga, ntiles, s, timed);
             if (rc) return rc;
         }
@@ -1828,7 +1859,7 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
         std::vector<uint8_t> pure((size_t)B, 0);
         for (int b = 1; b + 1 < B; ++b) pure[b] = Comp<T>::key_of(hspl[b - 1]) == Comp<T>::key_of(hspl[b]);
         return sub_sort<T>(ctx, part_out, d_keys, n, hb, B, m, s, timed, ctx->opt.sub_gather != 0, pure.data(),
-                           direct != nullptr);
+                           direct != nullptr, spl);
     }
     // pass plan: the runs of every bucket; the largest bucket's run count R sets the merge
     // levels L = ceil(log2 R), split into the fewest passes of <= max_logf levels (larger passes
