@@ -465,10 +465,17 @@ def run_single(args):
     if not ok:
         raise SystemExit("bench: sorted output failed verification")
     torch.cuda.synchronize()
+    # the timed steps run back to back (a sort returns while its last kernels run; nothing is read
+    # back in between), then as many steps again, each followed by a read of its HIP events, give
+    # the per-stage device times of the roofline (outside the timed region)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.sort_dev(t_in, out)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
     acc = {k: 0.0 for k in ("merge_kernel_ms", "block_sort_ms", "total_ms", "tile_sort_kernel_ms", "partition_ms",
                             "bucket_hist_ms", "bucket_scatter_ms", "sub_partition_ms")}
     npass, tkeys = 0, 0
-    t0 = time.perf_counter()
     for _ in range(args.steps):
         ctx.sort_dev(t_in, out)
         st = ctx.stats()  # reads the HIP events of this step (syncs the stream)
@@ -477,7 +484,6 @@ def run_single(args):
         npass += st["merge_passes"]
         tkeys += st["tile_sort_keys"]
     torch.cuda.synchronize()
-    t1 = time.perf_counter()
     stats = ctx.stats()
     ctx.close()
     k = {key: v / max(args.steps, 1) for key, v in acc.items()}  # per step
@@ -534,6 +540,14 @@ def run_multi(args, rank, world):
     torch.cuda.synchronize()
     dist.barrier()
     t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ptr, nout = ctx.sample_sort_dev(t_in)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t1 = time.perf_counter()
+    el = torch.tensor([t1 - t0], dtype=torch.float64)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    # per-stage device times from as many instrumented steps again (outside the timed region)
     timed = ("exchange_ms", "alltoall_ms", "final_merge_ms", "merge_kernel_ms", "tile_sort_kernel_ms",
              "bucket_hist_ms", "bucket_scatter_ms", "sub_partition_ms")
     acc = {k: 0.0 for k in timed}
@@ -549,9 +563,6 @@ def run_multi(args, rank, world):
         acc["sent"] += st["keys_sent"]
     torch.cuda.synchronize()
     dist.barrier()
-    t1 = time.perf_counter()
-    el = torch.tensor([t1 - t0], dtype=torch.float64)
-    dist.all_reduce(el, op=dist.ReduceOp.MAX)
     # per-rank figures of the roofline, gathered (rank 0 reports the slowest rank)
     steps = max(args.steps, 1)
     mine = torch.tensor([acc["tile_sort_kernel_ms"] / steps, acc["alltoall_ms"] / steps, acc["exchange_ms"] / steps,

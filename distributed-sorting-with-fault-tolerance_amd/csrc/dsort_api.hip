@@ -690,8 +690,9 @@ int dsort_finalize(dsort_ctx *ctx) {
     if (ctx->bucket_ev) (void)hipEventDestroy(ctx->bucket_ev);
     if (ctx->sub_host) (void)hipHostFree(ctx->sub_host);
     if (ctx->sub_ev) (void)hipEventDestroy(ctx->sub_ev);
-    if (ctx->tfb_host) (void)hipHostFree(ctx->tfb_host);
-    if (ctx->tfb_ev) (void)hipEventDestroy(ctx->tfb_ev);
+    if (ctx->side_ev) (void)hipEventDestroy(ctx->side_ev);
+    if (ctx->side) (void)hipStreamDestroy(ctx->side);
+    if (ctx->done_ev) (void)hipEventDestroy(ctx->done_ev);
     for (auto &e : ctx->ev)
         if (e) (void)hipEventDestroy(e);
     for (auto &e : ctx->kev)

@@ -351,10 +351,11 @@ __global__ void __launch_bounds__(BK_MAXB) pair_splitter_kernel(const int64_t *_
     }
 }
 
+// spl holds BK_MAXB + 1 entries: the BP splitters (+inf padded) and a +inf past them
 template <typename T>
 __device__ __forceinline__ void load_splitters(const typename Comp<T>::C *spl_g, int BP,
                                                typename Comp<T>::C *spl) {
-    for (int b = threadIdx.x; b < BP; b += BK_T) spl[b] = spl_g[b];
+    for (int b = threadIdx.x; b <= BP; b += BK_T) spl[b] = b < BP ? spl_g[b] : Comp<T>::inf();
 }
 
 // Keys per partition workgroup: `subs` sub-tiles of BK_T * KPT keys, 4..16 so that a large
@@ -394,7 +395,7 @@ __global__ void __launch_bounds__(BK_T, 2) bucket_hist_kernel(const T *__restric
                                                               int subs, uint32_t *__restrict__ counts) {
     using CT = Comp<T>;
     constexpr int KPT = Geo<T>::KPT, SUB = BK_T * KPT;
-    __shared__ typename CT::C spl[BK_MAXB];
+    __shared__ typename CT::C spl[BK_MAXB + 1];
     __shared__ uint32_t rng[BK_SLOTS];
     const BkMap m = *map;
     __shared__ uint32_t hist[BK_MAXB];
@@ -521,10 +522,11 @@ static __global__ void __launch_bounds__(BK_MAXB) bucket_scan_kernel(uint64_t *_
     }
     uint64_t allk, allt;
     const uint64_t sk = scan_excl_u64(tot, wsum, allk);
-    const uint64_t nt = b < B ? bucket_tiles(sk, tot, tile, align) : 0;
+    // (tile == 0: no tile table -- the second partition level makes its own tiles)
+    const uint64_t nt = b < B && tile ? bucket_tiles(sk, tot, tile, align) : 0;
     const uint64_t st = scan_excl_u64(nt, wsum, allt);
-    if (b < B) {
-        bstart[b] = sk;
+    if (b < B) bstart[b] = sk;
+    if (b < B && tile) {
         const uint64_t h = bucket_head(sk, tot, align);
         uint64_t k = st;
         if (h) tt[k++] = TileRef{sk, (uint32_t)h, 0};
@@ -596,7 +598,7 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
     constexpr int KPT = Geo<T>::KPT, SUB = G::SUB, LK = G::LK, KPL = G::KPL;
     static_assert(SUB + LK < (1 << 16) && LK <= 16, "packed fields");
     // (a non-last sub-tile writes <= (SUB + (LK-1) B) / LK lines, the last <= (SUB + 2 (LK-1) B) / LK)
-    __shared__ typename CT::C spl[BK_MAXB];
+    __shared__ typename CT::C spl[BK_MAXB + 1];
     __shared__ uint32_t rng[BK_SLOTS];
     __shared__ uint32_t hist[BK_MAXB];               // sub-tile histogram, then the LDS starts
     __shared__ uint2 st[BK_MAXB];                    // per bucket: LDS start | first line << 16, vc|ph|pure|L

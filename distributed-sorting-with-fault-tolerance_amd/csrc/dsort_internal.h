@@ -98,10 +98,15 @@ struct dsort_ctx {
     void *sub_host = nullptr;     // pinned: bucket table, chunk table, tile / merge-record counts
     size_t sub_host_bytes = 0;
     hipEvent_t sub_ev = nullptr;
-    void *tfb = nullptr;          // tiles the bin sort declined (+ their count)
+    hipStream_t side = nullptr;   // table uploads that overlap the first-level scatter
+    hipEvent_t side_ev = nullptr;
+    // End of the last sort / merge on its stream: a call on another stream waits for it, since
+    // the arenas are shared and a call returns while its last kernels still run.
+    hipEvent_t done_ev = nullptr;
+    hipStream_t done_stream = nullptr;
+    bool done_pending = false;
+    void *tfb = nullptr;          // tiles the bin sort declined (+ their count, on the device)
     size_t tfb_bytes = 0;
-    uint32_t *tfb_host = nullptr; // pinned: that count
-    hipEvent_t tfb_ev = nullptr;
     void *text_status = nullptr;  // per-tile look-back status words of the text codec
     size_t text_status_bytes = 0;
     void *red = nullptr;       // 64 B of reduction accumulators

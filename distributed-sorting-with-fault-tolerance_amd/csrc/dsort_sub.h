@@ -136,22 +136,47 @@ __device__ __forceinline__ int sub_of(const Spl<T> *spl, const uint32_t *rng, T 
     return sub_pick<T>(spl, r, a, b, key, pos);
 }
 
-// Sample g (global index, bucket b's samples at [soff, soff + ns)) = the key at position
-// start + ((2k + 1) * len) / (2 ns), k = g - soff.  Written as the key (smp) and, for int32, as
-// the composite key * 2^32 + g (cmp), whose sort orders the samples by (key, position).
+// Samples are taken in runs of SB_RUN consecutive keys (one 64-byte line, mostly, instead of one
+// line per sample: the sampling kernel went from ~80 us to ~?? us per sort at 2^30), run r of the
+// bucket's ns / SB_RUN runs centred at ((2r + 1) len) / (2 nr).  The first level's output holds a
+// bucket's keys in the order its workgroups met them, so a run samples as well as isolated keys do
+// on unstructured input, and on sorted input the bucket is sorted and every run lies at its
+// quantile.  Sample g (global index, bucket b's samples at [soff, soff + ns)) is written as the
+// key (smp) and, for int32, as the composite key * 2^32 + g (cmp), whose sort orders the samples
+// by (key, position).  A bucket whose ns is not a multiple of SB_RUN (DSORT_OPT_SUB_OVERSAMPLE
+// not a multiple of 4) samples single keys.
+constexpr uint32_t SB_RUN = 4;
+__host__ __device__ __forceinline__ uint32_t sample_run(const BInfo &b) { return b.ns % SB_RUN ? 1u : SB_RUN; }
+__host__ __device__ __forceinline__ uint64_t sample_run_pos(const BInfo &b, uint32_t run, uint64_t r) {
+    const uint64_t nr = b.ns / run;
+    const uint64_t p = ((2 * r + 1) * b.len) / (2 * nr);
+    return b.start + (p + run > b.len ? b.len - run : p);
+}
 __host__ __device__ __forceinline__ uint64_t sample_pos(const BInfo &b, uint64_t k) {
-    return b.start + ((2 * k + 1) * b.len) / (2 * (uint64_t)b.ns);
+    const uint32_t run = sample_run(b);
+    return sample_run_pos(b, run, k / run) + k % run;
 }
 template <typename T>
 __global__ void __launch_bounds__(SB_T) sb_sample_kernel(const T *__restrict__ src, const BInfo *__restrict__ bi,
                                                          T *__restrict__ smp, int64_t *__restrict__ cmp) {
     const BInfo b = bi[blockIdx.x];
-#pragma unroll 4  // (independent gathers in flight)
-    for (uint32_t k = threadIdx.x; k < b.ns; k += SB_T) {
-        const T key = src[sample_pos(b, k)];
+    auto put = [&](uint64_t k, T key) {
         const uint64_t g = b.soff + k;
         smp[g] = key;
         if constexpr (sizeof(T) == 4) cmp[g] = (int64_t)((uint64_t)(int64_t)key << 32 | (uint32_t)g);
+    };
+    if (sample_run(b) == SB_RUN) {
+#pragma unroll 2  // (independent gathers in flight)
+        for (uint32_t r = threadIdx.x; r < b.ns / SB_RUN; r += SB_T) {
+            const T *p = src + sample_run_pos(b, SB_RUN, r);
+            T key[SB_RUN];
+#pragma unroll
+            for (uint32_t i = 0; i < SB_RUN; ++i) key[i] = p[i];
+#pragma unroll
+            for (uint32_t i = 0; i < SB_RUN; ++i) put((uint64_t)r * SB_RUN + i, key[i]);
+        }
+    } else {
+        for (uint32_t k = threadIdx.x; k < b.ns; k += SB_T) put(k, src[sample_run_pos(b, 1, k)]);
     }
 }
 
@@ -522,6 +547,14 @@ __global__ void __launch_bounds__(SB_LT, 4) sb_local_kernel(T *__restrict__ buf,
     // (int32: 31 keys and their ranks are already live; batching spills and measured slower)
     constexpr int G = sizeof(T) == 4 ? 1 : 8;
     if constexpr (G == 1) {
+        if (c.len == (uint32_t)CHL) {  // a whole chunk (all but a bucket's last): no per-key branch
+#pragma unroll
+            for (int k = 0; k < KPT; ++k) {
+                const uint32_t i = tid + k * SB_LT;
+                const int j = sub_of<T>(spl, rng, f.klo, f.sh, key[k], (uint32_t)(c.start + i));
+                pk[k] = (uint32_t)j | atomicAdd(&hist[j], 1u) << 10;
+            }
+        } else
 #pragma unroll
         for (int k = 0; k < KPT; ++k) {
             const uint32_t i = tid + k * SB_LT;
@@ -582,6 +615,14 @@ __global__ void __launch_bounds__(SB_LT, 4) sb_local_kernel(T *__restrict__ buf,
     }
     __syncthreads();
     SBST(3);
+    if (c.len == (uint32_t)CHL) {  // a whole chunk: no per-key branch
+#pragma unroll
+        for (int k = 0; k < KPT; ++k) lk[hist[pk[k] & 1023] + (pk[k] >> 10)] = key[k];
+        __syncthreads();
+        SBST(4);
+#pragma unroll
+        for (int k = 0; k < KPT; ++k) src[tid + k * SB_LT] = lk[tid + k * SB_LT];
+    } else {
 #pragma unroll
     for (int k = 0; k < KPT; ++k) {
         const uint32_t i = tid + k * SB_LT;
@@ -593,6 +634,7 @@ __global__ void __launch_bounds__(SB_LT, 4) sb_local_kernel(T *__restrict__ buf,
     for (int k = 0; k < KPT; ++k) {
         const uint32_t i = tid + k * SB_LT;
         if (i < c.len) src[i] = lk[i];
+    }
     }
 #ifdef DSORT_STAMPS
     SBST(5);

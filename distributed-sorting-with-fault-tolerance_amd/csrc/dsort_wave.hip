@@ -700,27 +700,26 @@ __device__ __forceinline__ void merge_halves(T (&v)[K]) {
     }
 }
 
-// One window pass over s[0, M) (M <= TILE): thread t sorts (MERGE: merges the sorted halves of)
+// One window pass over s[0, P) (P <= TILE): thread t sorts (MERGE: merges the sorted halves of)
 // the 16 keys at 16 t + OFF.  Windows of one pass are disjoint, so each is read and written in
-// place.  A window is always moved as 16-byte vectors: slots past M read as key_max, sort to the
-// window's end and are written back past M, where nothing reads them.  (Guarding the vector path
-// with `ws + 16 <= M` let the compiler fold it into the scalar path: 16 ds_read2_b32 per window
-// at a 64-byte lane stride, 16-way bank conflicts.)  The last window at offset 8 would reach past
-// the tile; its second half is empty, so the merge is a no-op and it is skipped.
+// place.  The slots from P up to 24 past it (or the tile's end) hold key_max (bin_sort_tile), so a
+// window reaching past P needs no masking: key_max sorts to its end.  A window is always moved as
+// 16-byte vectors.  (Guarding the vector path with `ws + 16 <= M` let the compiler fold it into
+// the scalar path: 16 ds_read2_b32 per window at a 64-byte lane stride, 16-way bank conflicts.)
+// The last window at offset 8 would reach past the tile; its second half is empty, so the merge
+// is a no-op and it is skipped.
 template <int OFF, bool MERGE, typename T>
-__device__ __forceinline__ void window_pass(T *s, int M, int tid) {
+__device__ __forceinline__ void window_pass(T *s, int P, int tid) {
     using V = typename V16<T>::type;
     constexpr int N = KPC<T>;
     const int ws = 16 * tid + OFF;
-    if (ws >= M || ws + 16 > TILE_OF<T>) return;
+    if (ws >= P || ws + 16 > TILE_OF<T>) return;
     T v[16];
     V *p[16 / N];  // the window's 16-byte chunks (their physical slots: bsw)
 #pragma unroll
     for (int q = 0; q < 16 / N; ++q) p[q] = reinterpret_cast<V *>(s + bsw<T>((uint32_t)(ws + N * q)));
 #pragma unroll
     for (int q = 0; q < 16 / N; ++q) V16<T>::get(*p[q], v + N * q);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) v[k] = ws + k < M ? v[k] : key_max<T>();
     if constexpr (MERGE) merge_halves<16>(v);
     else sort_net<16>(v);
 #pragma unroll
@@ -781,6 +780,13 @@ __device__ __forceinline__ bool bin_sort_tile(const T (&x)[R], int valid, T *s, 
         for (int i = tid; i < valid; i += THREADS) out[i] = key_max<T>();
         return true;
     }
+    // The tile's LDS slots are shifted by sh = out's misalignment within a 16-byte chunk, so LDS
+    // chunk q (slots N q .. N q + N - 1) is output chunk q of out - sh, a 16-byte aligned address:
+    // step 6 moves whole chunks (ds_read_b128 -> 16-byte stores).  Slots [0, sh) hold key_min.
+    // A tile within 3 keys of TILE keeps sh = 0 (its shifted slots would not fit) and writes keys.
+    constexpr int N = KPC<T>;
+    const int sh0 = (int)((reinterpret_cast<uintptr_t>(out) / sizeof(T)) & (N - 1));
+    const int sh = valid + sh0 <= TILE_OF<T> ? sh0 : 0;
     const U range = (U)mx - (U)mn;
     BinMap<T> bm;
     bm.pre = 0;
@@ -799,7 +805,10 @@ __device__ __forceinline__ bool bin_sort_tile(const T (&x)[R], int valid, T *s, 
     const uint32_t bf = (uint32_t)__builtin_amdgcn_readfirstlane((int)bx);
     const bool hot = hot_hint || __popcll(__ballot(act0 && bx == bf)) >= 8;
     // 2. counting
-    if (hot || !BIN_BATCH<T>) {
+    if (!hot && !BIN_BATCH<T>) {  // (wave-uniform: the plain loop carries no aggregation code)
+#pragma unroll
+        for (int i = 0; i < R; ++i) bin_put<false>(x[i], mn, bm, cw, s, lane, false);
+    } else if (hot || !BIN_BATCH<T>) {
 #pragma unroll
         for (int i = 0; i < R; ++i) bin_put<false>(x[i], mn, bm, cw, s, lane, hot);
     } else {
@@ -816,7 +825,7 @@ __device__ __forceinline__ bool bin_sort_tile(const T (&x)[R], int valid, T *s, 
     uint32_t incl = wave_incl_sum(tot);
     if (lane == 63) sm.wsum[w] = incl;
     __syncthreads();
-    uint32_t run = incl - tot, M = 0;
+    uint32_t run = incl - tot + (uint32_t)sh, M = 0;
 #pragma unroll
     for (int i = 0; i < WAVES; ++i) {
         const uint32_t v = sm.wsum[i];
@@ -832,11 +841,22 @@ __device__ __forceinline__ bool bin_sort_tile(const T (&x)[R], int valid, T *s, 
     *c4 = make_uint4(wd[0], wd[1], wd[2], wd[3]);
     __syncthreads();  // (also: sm, in s, is dead from here)
     STAMP(4);
+    // Binned keys go to slots [sh, P); key_min below, key_max from P to the end of the output
+    // (E) and at least 24 slots past P (the windows reaching past P read them: no masking).
+    const int P = (int)M + sh, E = valid + sh;
+    {
+        const int F0 = E > P + 24 ? E : P + 24, F = F0 < TILE_OF<T> ? F0 : TILE_OF<T>;
+        if (tid < sh) s[bsw<T>((uint32_t)tid)] = key_min<T>();
+        for (int p = P + tid; p < F; p += THREADS) s[bsw<T>((uint32_t)p)] = key_max<T>();
+    }
     // 4. keys to their places
     // (mn through an opaque copy: the bins are recomputed here, not kept in registers across
     // the scan, where they would spill)
     asm volatile("" : "+v"(mn));
-    if (hot || !BIN_BATCH<T>) {
+    if (!hot && !BIN_BATCH<T>) {
+#pragma unroll
+        for (int i = 0; i < R; ++i) bin_put<true>(x[i], mn, bm, cw, s, lane, false);
+    } else if (hot || !BIN_BATCH<T>) {
 #pragma unroll
         for (int i = 0; i < R; ++i) bin_put<true>(x[i], mn, bm, cw, s, lane, hot);
     } else {
@@ -845,28 +865,49 @@ __device__ __forceinline__ bool bin_sort_tile(const T (&x)[R], int valid, T *s, 
     __syncthreads();
     STAMP(5);
     // 5. window passes; a descent can only be left at a boundary of the last pass's windows
-    window_pass<0, false>(s, (int)M, tid);
+    window_pass<0, false>(s, P, tid);
     __syncthreads();
     STAMP(6);
-    window_pass<8, true>(s, (int)M, tid);
+    window_pass<8, true>(s, P, tid);
     __syncthreads();
     STAMP(7);
     const int e8 = 16 * tid + 8;
-    if (block_or<WAVES>(e8 < (int)M && s[bsw<T>(e8 - 1)] > s[bsw<T>(e8)], cw)) {  // (cw is dead from step 5)
-        window_pass<0, true>(s, (int)M, tid);
+    if (block_or<WAVES>(e8 < P && s[bsw<T>(e8 - 1)] > s[bsw<T>(e8)], cw)) {  // (cw is dead from step 5)
+        window_pass<0, true>(s, P, tid);
         __syncthreads();
         const int e16 = 16 * tid + 16;
-        if (block_or<WAVES>(e16 < (int)M && s[bsw<T>(e16 - 1)] > s[bsw<T>(e16)], cw + WAVES)) return false;
+        if (block_or<WAVES>(e16 < P && s[bsw<T>(e16 - 1)] > s[bsw<T>(e16)], cw + WAVES)) return false;
     }
-    // 6. out: the binned keys in order, then key_max
-    // (indices start m keys below the tile, at the 128-byte line below out, so every wave's store
-    // covers whole lines: tiles start anywhere, and lines shared by two waves' stores came out as
-    // partial writes, 14 % of the written bytes)
-    constexpr int LK = 128 / (int)sizeof(T);
-    const int m = (int)((reinterpret_cast<uintptr_t>(out) / sizeof(T)) & (LK - 1));
+    // 6. out: slots [sh, E) -- the binned keys in order, then key_max.  Chunk q of out - sh is
+    // LDS chunk q; indices start at the 128-byte line below out - sh, so every wave's stores cover
+    // whole lines (tiles start anywhere, and lines shared by two waves' stores came out as partial
+    // writes, 14 % of the written bytes).  Round 2 moved one key per lane and instruction.
     STAMP(8);
-    for (int i = tid - m; i < valid; i += THREADS)
-        if (i >= 0) out[i] = (uint32_t)i < M ? s[bsw<T>(i)] : key_max<T>();
+    if (sh == sh0) {
+        using V = typename V16<T>::type;
+        T *ob = out - sh;  // 16-byte aligned
+        const int m8 = (int)((reinterpret_cast<uintptr_t>(ob) / 16) & 7);
+        const int nq = (E + N - 1) / N;
+        for (int q = tid - m8; q < nq; q += THREADS) {
+            if (q < 0) continue;
+            const int p0 = N * q;
+            const V v = *reinterpret_cast<const V *>(s + bsw<T>((uint32_t)p0));
+            if (p0 >= sh && p0 + N <= E) {
+                *reinterpret_cast<V *>(ob + p0) = v;
+            } else {
+                T k[N];
+                V16<T>::get(v, k);
+#pragma unroll
+                for (int e = 0; e < N; ++e)
+                    if (p0 + e >= sh && p0 + e < E) ob[p0 + e] = k[e];
+            }
+        }
+    } else {
+        constexpr int LK = 128 / (int)sizeof(T);
+        const int m = (int)((reinterpret_cast<uintptr_t>(out) / sizeof(T)) & (LK - 1));
+        for (int i = tid - m; i < valid; i += THREADS)
+            if (i >= 0) out[i] = s[bsw<T>((uint32_t)i)];
+    }
     STAMP(9);
     return true;
 }
@@ -1075,12 +1116,13 @@ __global__ void __launch_bounds__(64 * WG<T>::WAVES, WG<T>::OCC) bin_sort_kernel
         fb[atomicAdd(nfb, 1u)] = j;
 }
 
-// The bitonic tile sort: tile fb[blockIdx.x] (fb = the bin sort's declined tiles) or tile
-// blockIdx.x (fb = NULL).
+// The bitonic tile sort of the bin sort's declined tiles fb[i], i < *nfb, each workgroup taking
+// i = blockIdx.x, blockIdx.x + gridDim.x, ... (the count stays on the device: the host never
+// waits for the bin sort, and with no declined tile every workgroup exits at once).
 template <typename T, bool GATHER>
 __global__ void __launch_bounds__(64 * WG<T>::WAVES, WG<T>::OCC) block_sort_w_kernel(
     const T *in, T *out, uint64_t n, const uint4 *tiles, const uint32_t *ntiles, sb::Gather ga,
-    const uint32_t *fb) {
+    const uint32_t *fb, const uint32_t *nfb) {
     constexpr int TILE = TILE_OF<T>, N = KPC<T>;
     using V = typename V16<T>::type;
     // `in` may alias `out`: every workgroup reads its tile before it writes it
@@ -1089,10 +1131,14 @@ __global__ void __launch_bounds__(64 * WG<T>::WAVES, WG<T>::OCC) block_sort_w_ke
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
     const T c[6] = {lane_side<T>(0), lane_side<T>(1), lane_side<T>(2), lane_side<T>(3), lane_side<T>(4),
                     lane_side<T>(5)};
+    const uint32_t nj = *nfb;
+#pragma unroll 1
+    for (uint32_t i = blockIdx.x; i < nj; i += gridDim.x) {
+    if (i != blockIdx.x) __syncthreads();  // the previous tile's last reads of s are done
     T x[R];
     uint64_t base;
     int valid;
-    const uint32_t j = fb ? fb[blockIdx.x] : blockIdx.x;
+    const uint32_t j = fb[i];
     // (the piece table of a gathered tile sits in the slack, not in the runs)
     if (!load_tile<T, GATHER>(in, n, tiles, ntiles, ga, j, reinterpret_cast<uint32_t *>(s + TILE),
                               reinterpret_cast<uint32_t *>(s), x, base, valid))
@@ -1135,6 +1181,7 @@ __global__ void __launch_bounds__(64 * WG<T>::WAVES, WG<T>::OCC) block_sort_w_ke
             store_window_desc<true>(s, win, ps, lo, x);
             __syncthreads();
         }
+    }
     }
 }
 
@@ -1374,39 +1421,30 @@ static int tile_sort_event(dsort_ctx *ctx, hipStream_t s, bool timed, int which)
 }
 
 // The tile sort of `grid` tiles (an upper bound when the count lives on the device): the bin
-// sort first, then the bitonic sort of the tiles it declined (their count read back: the host
-// waits for the bin sort, which is the last work queued).  Events 7 / 8 around both.
+// sort first, then the bitonic sort of the tiles it declined.  Events 7 / 8 around both.
+constexpr uint32_t kFallbackWgs = 512;  // two workgroups per CU
 template <typename T, bool GATHER>
 static int tile_sort(dsort_ctx *ctx, const T *in, T *out, uint64_t n, const uint4 *tiles, const uint32_t *ntiles,
                      const sb::Gather &ga, uint32_t grid, hipStream_t s, bool timed) {
     const dim3 blk(64 * WG<T>::WAVES);
     int rc = tile_sort_event(ctx, s, timed, 0);
     if (rc) return rc;
-    // The library's own small sorts (timed = false: the splitter samples) take the bitonic sort
-    // alone: it needs no read-back, so the host never waits in the middle of a sort for them.
-    if (grid && timed) {
+    // (The library's own small sorts, the splitter samples, take the same path: nothing is read
+    // back, and a tile of a bucket's 2048 samples costs the bin sort a quarter of what the bitonic
+    // sort spends on the whole padded tile.)
+    if (grid) {
         rc = ensure(ctx, &ctx->tfb, &ctx->tfb_bytes, ((size_t)grid + 1) * 4, "tile fallback list");
         if (rc) return rc;
-        if (!ctx->tfb_host) DSORT_HIP(ctx, hipHostMalloc((void **)&ctx->tfb_host, 64, hipHostMallocDefault));
-        if (!ctx->tfb_ev && hipEventCreateWithFlags(&ctx->tfb_ev, hipEventDisableTiming) != hipSuccess)
-            return set_err(ctx, DSORT_EHIP, "hipEventCreate");
         uint32_t *fb = static_cast<uint32_t *>(ctx->tfb), *nfb = fb + grid;
         DSORT_HIP(ctx, hipMemsetAsync(nfb, 0, 4, s));
         hipLaunchKernelGGL((bin_sort_kernel<T, GATHER>), dim3(grid), blk, 0, s, in, out, n, tiles, ntiles, ga, fb, nfb);
         DSORT_HIP(ctx, hipGetLastError());
-        DSORT_HIP(ctx, hipMemcpyAsync(ctx->tfb_host, nfb, 4, hipMemcpyDeviceToHost, s));
-        DSORT_HIP(ctx, hipEventRecord(ctx->tfb_ev, s));
-        DSORT_HIP(ctx, hipEventSynchronize(ctx->tfb_ev));
-        const uint32_t nf = *ctx->tfb_host;
-        if (nf > grid) return set_err(ctx, DSORT_EHIP, "tile fallback overflow");
-        if (nf) {
-            hipLaunchKernelGGL((block_sort_w_kernel<T, GATHER>), dim3(nf), blk, 0, s, in, out, n, tiles, ntiles, ga,
-                               static_cast<const uint32_t *>(fb));
-            DSORT_HIP(ctx, hipGetLastError());
-        }
-    } else if (grid) {
-        hipLaunchKernelGGL((block_sort_w_kernel<T, GATHER>), dim3(grid), blk, 0, s, in, out, n, tiles, ntiles, ga,
-                           static_cast<const uint32_t *>(nullptr));
+        // the declined tiles: a grid of at most one round of workgroups over the chip walks the
+        // list, whose length stays on the device (round 2 read it back: the host waited for the
+        // bin sort, and the GPU idled about 70 us per sort until the next work arrived)
+        const uint32_t fgrid = grid < kFallbackWgs ? grid : kFallbackWgs;
+        hipLaunchKernelGGL((block_sort_w_kernel<T, GATHER>), dim3(fgrid), blk, 0, s, in, out, n, tiles, ntiles, ga,
+                           static_cast<const uint32_t *>(fb), static_cast<const uint32_t *>(nfb));
         DSORT_HIP(ctx, hipGetLastError());
     }
     return tile_sort_event(ctx, s, timed, 1);
@@ -1599,9 +1637,20 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
     for (int b = 0; b < B; ++b)
         if (bi[b].ns) hst[nst++] = bk::TileRef{bi[b].soff, bi[b].ns, 0};
     *reinterpret_cast<uint32_t *>(hst + B) = nst;
-    DSORT_HIP(ctx, hipMemcpyAsync(dbi, h, B * sizeof(BInfo), hipMemcpyHostToDevice, s));
-    if (nch) DSORT_HIP(ctx, hipMemcpyAsync(dch, h + h_ch, nch * sizeof(Chunk), hipMemcpyHostToDevice, s));
-    DSORT_HIP(ctx, hipMemcpyAsync(stl, hst, B * sizeof(bk::TileRef) + 16, hipMemcpyHostToDevice, s));
+    // The tables go up on a side stream, so the copies run while the first-level scatter (queued
+    // on s before this point) is still running; s waits for them before the first kernel that
+    // reads them.  (On s they queued behind the scatter: about 60 us of idle GPU per sort at 2^30.)
+    // Nothing still reads the arena: the host got here after waiting for the histogram of this
+    // sort, which follows every kernel of the previous sort on s.
+    if (!ctx->side && hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess)
+        return set_err(ctx, DSORT_EHIP, "hipStreamCreate");
+    if (!ctx->side_ev && hipEventCreateWithFlags(&ctx->side_ev, hipEventDisableTiming) != hipSuccess)
+        return set_err(ctx, DSORT_EHIP, "hipEventCreate");
+    DSORT_HIP(ctx, hipMemcpyAsync(dbi, h, B * sizeof(BInfo), hipMemcpyHostToDevice, ctx->side));
+    if (nch) DSORT_HIP(ctx, hipMemcpyAsync(dch, h + h_ch, nch * sizeof(Chunk), hipMemcpyHostToDevice, ctx->side));
+    DSORT_HIP(ctx, hipMemcpyAsync(stl, hst, B * sizeof(bk::TileRef) + 16, hipMemcpyHostToDevice, ctx->side));
+    DSORT_HIP(ctx, hipEventRecord(ctx->side_ev, ctx->side));
+    DSORT_HIP(ctx, hipStreamWaitEvent(s, ctx->side_ev, 0));
     DSORT_HIP(ctx, hipMemsetAsync(num, 0, 8, s));
     uint64_t npure = 0;
     for (int b = 0; b < B; ++b) npure += pure[b] ? hb[b + 1] - hb[b] : 0;
@@ -1829,7 +1878,7 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
     if ((rc = stage_event(ctx, s, timed, 10))) return rc;
     hipLaunchKernelGGL(bucket_colsum_kernel, dim3((unsigned)nchunk), dim3(BK_MAXB), 0, s, cnt, (uint32_t)G, B, part);
     hipLaunchKernelGGL(bucket_scan_kernel, dim3(1), dim3(BK_MAXB), 0, s, part, (uint32_t)nchunk, B,
-                       (uint32_t)TILE, (uint32_t)ALIGN, bst, tt, ntl);
+                       sub_keys<T>(ctx) ? 0u : (uint32_t)TILE, (uint32_t)ALIGN, bst, tt, ntl);
     hipLaunchKernelGGL(bucket_offsets_kernel<uint64_t>, dim3((unsigned)nchunk), dim3(BK_MAXB), 0, s, cnt, part, bst, (uint32_t)G, B, offs);
     DSORT_HIP(ctx, hipGetLastError());
     // bucket starts to the host (the pass plan depends on the bucket sizes); the host waits for
@@ -2202,11 +2251,31 @@ int sort_stages(const dsort_opts &opt, uint64_t n, int key_bytes) {
     return 1 + (int)passes;
 }
 
+// A top-level call first waits (on the device) for the context's previous call when that ran on
+// another stream, and marks its own end: the calls share the context's arenas and return while
+// their last kernels still run.
+static int order_begin(dsort_ctx *ctx, hipStream_t s) {
+    if (ctx->nested) return DSORT_OK;
+    if (ctx->done_pending && ctx->done_stream != s) DSORT_HIP(ctx, hipStreamWaitEvent(s, ctx->done_ev, 0));
+    return DSORT_OK;
+}
+static int order_end(dsort_ctx *ctx, hipStream_t s) {
+    if (ctx->nested) return DSORT_OK;
+    if (!ctx->done_ev && hipEventCreateWithFlags(&ctx->done_ev, hipEventDisableTiming) != hipSuccess)
+        return set_err(ctx, DSORT_EHIP, "hipEventCreate");
+    DSORT_HIP(ctx, hipEventRecord(ctx->done_ev, s));
+    ctx->done_stream = s;
+    ctx->done_pending = true;
+    return DSORT_OK;
+}
+
 template <typename T>
 int sort_device(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipStream_t s, bool timed) {
     const bool top = ctx->nested == 0;
     if (top) ctx->stages_done = 0;
-    const int rc = wv::wave_sort<T>(ctx, d_in, d_keys, n, s, timed);
+    int rc = order_begin(ctx, s);
+    if (!rc) rc = wv::wave_sort<T>(ctx, d_in, d_keys, n, s, timed);
+    if (!rc) rc = order_end(ctx, s);
     if (rc || !top || ctx->opt.kill_after_pass < 0) return rc;
     // the kill stage was never reached: a fault-injection run that would silently not fail
     return set_err(ctx, DSORT_EINVAL,
@@ -2220,7 +2289,10 @@ int sort_device(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipStream_t 
 template <typename T>
 int merge_device(dsort_ctx *ctx, const T *d_in, const size_t *lens, int k, T *d_out, hipStream_t s,
                  bool keep_stats) {
-    return wv::wave_merge<T>(ctx, d_in, lens, k, d_out, s, keep_stats);
+    int rc = order_begin(ctx, s);
+    if (!rc) rc = wv::wave_merge<T>(ctx, d_in, lens, k, d_out, s, keep_stats);
+    if (!rc) rc = order_end(ctx, s);
+    return rc;
 }
 
 template int sort_device<int32_t>(dsort_ctx *, const int32_t *, int32_t *, size_t, hipStream_t, bool);

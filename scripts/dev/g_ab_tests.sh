@@ -1,7 +1,10 @@
-cd "${GRAFT_REPO_ROOT}"
-mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests -q -x -m gpu --timeout 170 --timeout-method thread > gpurun_out/tests.log 2>&1
-st=$?; echo "tests exit $st"; tail -4 gpurun_out/tests.log
-[ $st -ne 0 ] && exit $st
-VS="csw0" bash scripts/dev/ab_multi.sh > gpurun_out/ab.log 2>&1 || exit $?
-cat gpurun_out/ab.log | grep -v amdgpu.ids
+#!/bin/bash
+# A/B of compile-time variants (ktime, 2 rounds) then the GPU suite against the variant $TESTV.
+# usage: VS="v1 v2" TESTV=v2 scripts/dev/g_ab_tests.sh [ktime args]
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+R=$PWD; mkdir -p gpurun_out
+bash scripts/dev/ab_multi.sh "$@" || exit $?
+if [ -n "$TESTV" ]; then
+  DSORT_LIB=$R/build_variants/$TESTV/libdsort.so timeout -k 10 400 python -u -m pytest tests -q -x -m gpu --timeout 170 --timeout-method thread > gpurun_out/tests_$TESTV.log 2>&1
+  st=$?; echo "tests($TESTV) exit $st"; tail -3 gpurun_out/tests_$TESTV.log; exit $st
+fi

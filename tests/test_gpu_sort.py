@@ -268,3 +268,26 @@ def test_sort_i32_pass_boundaries(gpu_ctx, n):
     out = torch.empty_like(t)
     gpu_ctx.sort_dev(t, out)
     assert np.array_equal(out.cpu().numpy(), np.sort(host))
+
+
+def test_back_to_back_sorts_on_two_streams(gpu_ctx):
+    """A sort returns while its last kernels still run, and the context's arenas are shared: a
+    following sort on another stream must wait for it on the device (order_begin/order_end in
+    dsort_wave.hip).  Two bucketed sorts issued back to back on two streams, then checked."""
+    import torch
+    n = (1 << 25) + 4097
+    a = torch.empty(n, dtype=torch.int32, device="cuda")
+    b = torch.empty(n, dtype=torch.int32, device="cuda")
+    gpu_ctx.gen_uniform(a, 11)
+    gpu_ctx.gen_uniform(b, 12)
+    torch.cuda.synchronize()
+    oa, ob = torch.empty_like(a), torch.empty_like(b)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    for _ in range(2):
+        with torch.cuda.stream(s1):
+            gpu_ctx.sort_dev(a, oa)
+        with torch.cuda.stream(s2):
+            gpu_ctx.sort_dev(b, ob)
+    torch.cuda.synchronize()
+    assert torch.equal(oa, torch.sort(a)[0])
+    assert torch.equal(ob, torch.sort(b)[0])
