@@ -193,7 +193,8 @@ __host__ __device__ __forceinline__ bool slot_first(const BkMap &m, uint32_t i, 
     return true;
 }
 
-template <typename T, int SB = BK_SLOTB>
+// PACK (int32 only): the packed entry of bucket_fast's first branch (the scatter's table)
+template <typename T, bool PACK, int SB = BK_SLOTB>
 __device__ __forceinline__ void build_slots(const typename Comp<T>::C *spl, int BP, const BkMap &m,
                                             uint32_t *rng) {
     using CT = Comp<T>;
@@ -212,9 +213,17 @@ __device__ __forceinline__ void build_slots(const typename Comp<T>::C *spl, int 
                 cnt[e] = (uint32_t)bucket_of<T>(spl, BP, c);
             }
         }
-        // a slot whose (>= 2) splitters all hold one key K: see bucket_fast
-        const bool one = CT::ADAPT && cnt[1] >= cnt[0] + 2 && CT::key_of(spl[cnt[0]]) == CT::key_of(spl[cnt[1] - 1]);
-        rng[i] = cnt[0] | (uint32_t)one << 15 | (cnt[1] << 16);
+        if constexpr (!CT::ADAPT && PACK) {
+            // int32: lo (bits 0-9), splitters in the slot (bits 10-11; 3 = three or more) and bits
+            // 20..1 of the flipped key of the slot's first splitter (bits 12-31): see bucket_fast
+            const uint32_t in = cnt[1] - cnt[0];
+            const uint32_t kb = in ? ((uint32_t)CT::key_of(spl[cnt[0]]) ^ 0x80000000u) << 11 >> 12 : 0u;
+            rng[i] = cnt[0] | (in > 3 ? 3u : in) << 10 | kb << 12;
+        } else {
+            // a slot whose (>= 2) splitters all hold one key K: see bucket_fast
+            const bool one = CT::ADAPT && cnt[1] >= cnt[0] + 2 && CT::key_of(spl[cnt[0]]) == CT::key_of(spl[cnt[1] - 1]);
+            rng[i] = cnt[0] | (uint32_t)one << 15 | (cnt[1] << 16);
+        }
     }
 }
 
@@ -228,10 +237,34 @@ __device__ __forceinline__ void build_slots(const typename Comp<T>::C *spl, int 
 // input, land together in one or two buckets).
 // Histogram and scatter use the same map and table, so they agree key for key.  (Which copy of
 // K lands where does not matter to a keys-only sort.)
-template <typename T>
+// int32: the slot entry carries the slot's first splitter's key down to bit 1 (the slot is the
+// top 11 bits), so a key in a slot of at most one splitter needs no splitter read -- the usual
+// case: uniform keys put one splitter in every other slot, about 2^22 values apart.  A key equal
+// to that splitter in bits 31..1 compares its composite; a slot of two or more splitters searches
+// them (its end from the next slot's entry).  (Round 2 read the splitter for every key of a slot
+// that had one: half of the keys, a dependent 8-byte LDS read on the way to the rank atomic.)
+template <typename T, bool PACK>
 __device__ __forceinline__ int bucket_fast(const typename Comp<T>::C *spl, const uint32_t *rng, uint32_t slot,
                                            T key, const typename Comp<T>::C &c) {
     const uint32_t r = rng[slot];
+    if constexpr (!Comp<T>::ADAPT && PACK) {
+        // branch-free on the usual path; the rare keys that search take one wave-uniform branch
+        // (per-key early returns doubled the histogram's branches and cost it 0.2 ms at 2^30)
+        int lo = (int)(r & 1023);
+        const uint32_t in = (r >> 10) & 3, sb = r >> 12;
+        const uint32_t kb = ((uint32_t)key ^ 0x80000000u) << 11 >> 12;
+        const int j = lo + (int)(in == 1 && kb > sb);
+        const bool slow = in > 1 || (in == 1 && kb == sb);
+        if (__builtin_expect(__ballot(slow) == 0, 1)) return j;
+        if (!slow) return j;
+        int hi = in == 1 ? lo + 1 : in == 2 ? lo + 2 : slot + 1 < (uint32_t)BK_SLOTS ? (int)(rng[slot + 1] & 1023) : BK_MAXB;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (Comp<T>::lt(spl[mid], c)) lo = mid + 1;
+            else hi = mid;
+        }
+        return lo;
+    }
     int lo = (int)(r & 0x7FFF), hi = (int)(r >> 16);
     if (Comp<T>::ADAPT && (r & 0x8000)) {
         const typename Comp<T>::C a = spl[lo], z = spl[hi - 1];
@@ -351,11 +384,12 @@ __global__ void __launch_bounds__(BK_MAXB) pair_splitter_kernel(const int64_t *_
     }
 }
 
-// spl holds BK_MAXB + 1 entries: the BP splitters (+inf padded) and a +inf past them
+// spl holds BK_MAXB + 1 entries: the BP splitters (+inf padded), +inf up to the end (the int32
+// lookup of the last slot searches up to BK_MAXB)
 template <typename T>
 __device__ __forceinline__ void load_splitters(const typename Comp<T>::C *spl_g, int BP,
                                                typename Comp<T>::C *spl) {
-    for (int b = threadIdx.x; b <= BP; b += BK_T) spl[b] = b < BP ? spl_g[b] : Comp<T>::inf();
+    for (int b = threadIdx.x; b <= BK_MAXB; b += BK_T) spl[b] = b < BP ? spl_g[b] : Comp<T>::inf();
 }
 
 // Keys per partition workgroup: `subs` sub-tiles of BK_T * KPT keys, 4..16 so that a large
@@ -402,7 +436,7 @@ __global__ void __launch_bounds__(BK_T, 2) bucket_hist_kernel(const T *__restric
     load_splitters<T>(spl_g, BP, spl);
     for (int b = threadIdx.x; b < B; b += BK_T) hist[b] = 0;
     __syncthreads();
-    build_slots<T>(spl, BP, m, rng);
+    build_slots<T, false>(spl, BP, m, rng);  // (the packed table measured 0.78 -> 0.93 ms here)
     __syncthreads();
     const uint64_t g0 = (uint64_t)blockIdx.x * subs * SUB;
     // the next sub-tile's keys are loaded while the current one is counted (two workgroups per CU
@@ -432,14 +466,14 @@ __global__ void __launch_bounds__(BK_T, 2) bucket_hist_kernel(const T *__restric
             for (int k = 0; k < KPT; ++k) {
                 const uint64_t i = b0 + (uint64_t)k * BK_T;
                 const uint32_t sl = slot_mode<T, BK_SLOTB, 0>(m, key[k]);
-                if (i < n) atomicAdd(&hist[bucket_fast<T>(spl, rng, sl, key[k], CT::make(key[k], i))], 1u);
+                if (i < n) atomicAdd(&hist[bucket_fast<T, false>(spl, rng, sl, key[k], CT::make(key[k], i))], 1u);
             }
         } else {
 #pragma unroll
             for (int k = 0; k < KPT; ++k) {
                 const uint64_t i = b0 + (uint64_t)k * BK_T;
                 const uint32_t sl = slot_mode<T, BK_SLOTB, 1>(m, key[k]);
-                if (i < n) atomicAdd(&hist[bucket_fast<T>(spl, rng, sl, key[k], CT::make(key[k], i))], 1u);
+                if (i < n) atomicAdd(&hist[bucket_fast<T, false>(spl, rng, sl, key[k], CT::make(key[k], i))], 1u);
             }
         }
     }
@@ -586,6 +620,21 @@ template <typename T> struct LineGeo {
     static constexpr int SUB = BK_T * Geo<T>::KPT;                  // keys per sub-tile
     static constexpr int MAPN = (SUB + 2 * (LK - 1) * BK_MAXB) / LK; // lines per sub-tile, at most
 };
+#ifdef DSORT_STAMPS
+// Diagnostic build only: per-workgroup phase cycles of the line scatter (wave 0's view), read back
+// by dsort_debug_bkstamps() (scripts/dev/bkstamps.py).
+__device__ unsigned long long g_bkstamps[8192 * 16];
+#define BKST(k)                                            \
+    do {                                                   \
+        const uint64_t t1_ = __builtin_amdgcn_s_memtime(); \
+        bk_acc[k] += t1_ - bk_t0;                          \
+        bk_t0 = t1_;                                       \
+    } while (0)
+#else
+#define BKST(k) \
+    do {        \
+    } while (0)
+#endif
 template <typename T>
 __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__restrict__ in, uint64_t n,
                                                                     const typename Comp<T>::C *__restrict__ spl_g,
@@ -624,9 +673,12 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
     load_splitters<T>(spl_g, BP, spl);
     const BkMap m = *map;
     __syncthreads();
-    build_slots<T>(spl, BP, m, rng);
+    build_slots<T, true>(spl, BP, m, rng);
     __syncthreads();
     const uint64_t g0 = (uint64_t)g * subs * SUB;
+#ifdef DSORT_STAMPS
+    uint64_t bk_acc[8] = {}, bk_t0 = __builtin_amdgcn_s_memtime();
+#endif
     T nxt[KPT];
 #pragma unroll
     for (int k = 0; k < KPT; ++k) {
@@ -656,11 +708,12 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
             const uint64_t i = s0 + tb + (uint64_t)k * BK_T;
             pk[k] = ~0u;
             if (i < n) {
-                const int b = bucket_fast<T>(spl, rng, sl[k], key[k], CT::make(key[k], i));
+                const int b = bucket_fast<T, true>(spl, rng, sl[k], key[k], CT::make(key[k], i));
                 pk[k] = atomicAdd(&hist[b], 1u) | (uint32_t)b << 16;
             }
         }
         __syncthreads();  // A
+        BKST(0);
         // owner: new keys, whole lines to write, entries carried to the next sub-tile
         const uint32_t hv = owner ? hist[tb] : 0;
         const uint32_t L = vc + hv;  // stream entries not yet written
@@ -669,6 +722,7 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
         const uint32_t incl = wave_incl_sum(pv);
         if (lane == 63) wsum[w] = incl;
         __syncthreads();  // B
+        BKST(1);
         uint32_t woff = 0, all = 0;
 #pragma unroll
         for (int i = 0; i < BK_T / 64; ++i) {
@@ -685,10 +739,12 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
             for (uint32_t i = 0; i < nl; ++i) lmap[p0 + i] = (uint16_t)tb;
         }
         __syncthreads();  // C
+        BKST(2);
 #pragma unroll
         for (int k = 0; k < KPT; ++k)
             if (pk[k] != ~0u) lk[hist[pk[k] >> 16] + (pk[k] & 0xFFFF)] = key[k];
         __syncthreads();  // D
+        BKST(3);
         if (owner) hist[tb] = 0;  // (the next sub-tile's atomics follow barrier E)
         // whole lines: 4 lanes per line, 16 bytes per lane
         for (uint32_t it = tb; it < 4 * C; it += BK_T) {
@@ -721,6 +777,7 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
         }
         if (last) break;
         __syncthreads();  // E
+        BKST(4);
         // carry the tail of every stream: entries [LK nl, L) -> carry[0, L - LK nl) (the entries
         // below vc of a stream that wrote no line are there already)
         if (owner) {
@@ -730,8 +787,15 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
             gb += nl * LK;
             vc = nv;
         }
+        BKST(5);
     }
+#ifdef DSORT_STAMPS
+    BKST(4);
+    if (tb == 0 && g < 8192)
+        for (int k = 0; k < 8; ++k) g_bkstamps[g * 16 + k] = bk_acc[k];
+#endif
 }
+#undef BKST
 
 }  // namespace bk
 }  // namespace dsort

@@ -349,7 +349,7 @@ struct GTile {
     uint64_t src;          // first key of the bucket's first chunk (chunk c0 + k at src + k * SB_LCH)
     uint32_t valid, b, j0, j1;
     uint32_t c0, nch;      // the bucket's chunks [c0, c0 + nch)
-    uint32_t nsub, pad;    // the bucket's sub-buckets
+    uint32_t nsub, flags;  // the bucket's sub-buckets; bit 0: gathered key by key (no vector room)
 };
 
 // What the gathering tile sort needs (block_sort_w_kernel<T, true>): its tiles, the chunk and
@@ -359,6 +359,8 @@ struct Gather {
     const Chunk *ch;
     const BInfo *bi;
     const uint32_t *pref;
+    const uint2 *pieces;  // tile j's pieces [lo, hi) (global key indices) at pieces[j * PS ..], one per chunk
+    uint32_t PS;          // piece-table stride: the most chunks of a bucket
     int SS;
     const void *spl;  // the splitters (Spl<T>, SS per bucket): equal neighbours = a duplicate run
     const void *bspl; // the first level's splitters (bk::Comp<T>::C, B - 1): a bucket's key bounds
@@ -370,21 +372,32 @@ struct Gather {
 // oversized sub-bucket only counts in novf (the host then takes the scatter path).
 // SCATTER: counts[c][j]; the per-chunk offsets of the scatter are written too; tiles are
 // TileRefs.
+// LOCAL: a tile's room is tile - cpad * (the bucket's chunks): the gathering tile sort reads every
+// piece as the 16-byte vectors covering it, up to cpad extra slots per piece (gather_tile).
+// LOCAL also writes every tile's piece table (pieces, PS entries per tile, tiles below tcap; lch =
+// keys per chunk): the
+// gathering tile sort then reads it together with the tile record, one round trip before its key
+// loads instead of two (record, then the prefix tables).
 template <bool LOCAL>
 __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restrict__ bi, int SS,
                                                           const uint32_t *__restrict__ counts,
                                                           uint32_t *__restrict__ offs, int tile, int align,
-                                                          uint32_t mis, void *__restrict__ tiles,
+                                                          uint32_t mis, uint32_t cpad, void *__restrict__ tiles,
                                                           uint32_t *__restrict__ ntiles, Ovf *__restrict__ ovf,
-                                                          uint32_t *__restrict__ novf) {
+                                                          uint32_t *__restrict__ novf, uint2 *__restrict__ pieces,
+                                                          uint32_t PS, uint32_t tcap, uint32_t lch) {
     __shared__ uint32_t wsum[SB_MAXS / 64];
     __shared__ uint32_t ss[SB_MAXS + 1];   // sub-bucket starts (positions)
     __shared__ uint16_t nxt[SB_MAXS];      // first sub-bucket after the tile starting at i
     __shared__ uint16_t chain[SB_MAXS];    // sub-buckets that start a tile
+    __shared__ uint16_t tix[SB_MAXS];      // LOCAL: tile of chain entry i, relative to tbase (0xFFFF: none)
     __shared__ uint32_t nchain, tbase;
     const BInfo b = bi[blockIdx.x];
     const int j = threadIdx.x;
     const int ns = (int)b.nsub;
+    const int full = tile;  // LOCAL: a lone sub-bucket above the padded room still makes a tile up to
+                            // `full` keys, gathered key by key (GTile.flags bit 0)
+    if (LOCAL) tile -= (int)(cpad * (b.c1 - b.c0));
     auto cnt = [&](uint32_t c) -> uint32_t {
         if constexpr (LOCAL) {
             const uint32_t *pc = counts + (uint64_t)c * (SS + 1);
@@ -445,7 +458,7 @@ __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restric
         i1 = nxt[i0];
         const uint32_t p = ss[i0], len = ss[i1] - p;
         room = (uint32_t)tile - ((p + mis) & (uint32_t)(align - 1));
-        over = len > room;
+        over = len > (LOCAL ? (uint32_t)full : room);
         nt = len == 0 ? 0 : over ? (LOCAL ? 0 : 1 + (len - room + tile - 1) / tile) : 1;
         if (LOCAL && over) atomicAdd(novf, 1u);
     }
@@ -453,11 +466,13 @@ __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restric
     const uint32_t tex = scan_excl_1024(nt, wsum, tall);
     if (j == 0) tbase = tall ? atomicAdd(ntiles, tall) : 0;
     __syncthreads();
+    if (LOCAL && j < nc) tix[j] = nt ? (uint16_t)tex : (uint16_t)0xFFFF;
     if (j < nc && nt) {
         const uint32_t p = ss[i0], len = ss[i1] - p;
         uint32_t k = tbase + tex;
         if constexpr (LOCAL) {
-            static_cast<GTile *>(tiles)[k] = GTile{p, b.start, len, blockIdx.x, i0, i1, b.c0, b.c1 - b.c0, b.nsub, 0};
+            static_cast<GTile *>(tiles)[k] = GTile{p, b.start, len, blockIdx.x, i0, i1, b.c0, b.c1 - b.c0, b.nsub,
+                                                   len > room ? 1u : 0u};
         } else {
             bk::TileRef *tt = static_cast<bk::TileRef *>(tiles);
             if (!over) {
@@ -468,6 +483,21 @@ __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restric
                     tt[k++] = bk::TileRef{(uint64_t)p + q, len - q < (uint32_t)tile ? len - q : (uint32_t)tile, 0};
                 ovf[atomicAdd(novf, 1u)] = Ovf{p, len};
             }
+        }
+    }
+    if constexpr (LOCAL) {
+        __syncthreads();
+        // the piece tables: (tile, chunk) pairs spread over the workgroup
+        const uint32_t nch = b.c1 - b.c0;
+        for (uint32_t q = threadIdx.x; q < (uint32_t)nc * nch; q += blockDim.x) {
+            const uint32_t t = q / nch, c = q - t * nch;
+            if (tix[t] == 0xFFFF) continue;
+            const uint32_t k = tbase + tix[t];
+            if (k >= tcap) continue;  // (the host sees ntiles > tcap and fails the sort)
+            const uint32_t a0 = chain[t], a1 = nxt[a0];
+            const uint32_t *pc = counts + (uint64_t)(b.c0 + c) * (SS + 1);
+            const uint32_t base = (uint32_t)b.start + c * lch;
+            pieces[(uint64_t)k * PS + c] = make_uint2(base + pc[a0], base + pc[a1]);
         }
     }
 }

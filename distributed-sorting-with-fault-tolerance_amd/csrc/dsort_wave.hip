@@ -917,80 +917,137 @@ __device__ __forceinline__ bool bin_sort_tile(const T (&x)[R], int valid, T *s, 
 // ------------------------------------------------------------------------------------------
 // tiles: NULL = tile j is keys [j * TILE, (j + 1) * TILE) of n; else tile j = tiles[j] (the
 // bucketed sort's tiles, which never cross a bucket), j < *ntiles.
-// Pieces of a gathered tile at most: the piece table (offsets + sources) lives in the slack.
+// Pieces of a gathered tile at most (= chunks of a bucket on the local-partition path).
 template <typename T> constexpr int kMaxPieces = WK * (int)sizeof(T) / 8 - 2;
+static_assert(64 + 3 * kMaxPieces<int32_t> + 1 <= TILE_OF<int32_t> && 64 + 3 * kMaxPieces<int64_t> + 1 <= 2 * TILE_OF<int64_t>,
+              "the piece table of a gathered tile fits in the tile's LDS");
 
 // The tile of a GTile (local-partition path, dsort_sub.h): one piece per chunk of its bucket.
-// The piece table (offsets in the tile, sources) goes to the LDS slack; then lane t of wave w
-// loads tile slots w * 1024 + 64 i + t straight into x[i] (the order before the sort does not
-// matter), walking the pieces upwards as i grows: consecutive lanes read consecutive keys of a
-// piece, and all R loads of a lane are in flight together.
-// poff: 2 kMaxPieces + 1 words of LDS for the piece table; wsum: one word per wave.
+// Keys move as aligned 16-byte vectors (N keys): piece k is read as the vectors that cover it,
+// its neighbours' keys in its first and last vector masked to key_max.  The piece table (vector
+// offsets in the tile, piece bounds) goes to LDS; lane t of wave w loads the tile's vector slots
+// w * WK / N + 64 i + t straight into x[N i .. N i + N) (the order before the sort does not
+// matter), walking the pieces upwards as i grows: consecutive lanes read consecutive vectors of a
+// piece, and all R / N loads of a lane are in flight together.  The masked keys take up to
+// 2 (N - 1) slots per piece beyond `valid`: the tile packing leaves that room (sb_scan_kernel).
+// (Round 2 moved one key per lane and load, walking the pieces key by key: 4x the loads and the
+// address arithmetic of int32.)  `in` is 16-byte aligned (the context's scratch).
+// The piece-table entries of thread t (pieces 2t, 2t + 1 of tile jt), loaded before the tile record
+// is waited for.
+__device__ __forceinline__ void gather_pieces(const sb::Gather &ga, uint32_t jt, uint2 (&pe)[2],
+                                              const int tid = threadIdx.x) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {  // (up to the stride: the reads do not wait for the record)
+        const uint32_t k = 2 * tid + q;
+        pe[q] = k < ga.PS ? ga.pieces[(uint64_t)jt * ga.PS + k] : make_uint2(0u, 0u);
+    }
+}
+// ptab: 3 kMaxPieces + 1 words of LDS for the piece table; wsum: one word per wave.
 template <typename T>
-__device__ __forceinline__ void gather_tile(const sb::Gather &ga, const sb::GTile &gt, const T *in, uint32_t *poff,
-                                            uint32_t *wsum, T (&x)[R], const int tid = threadIdx.x) {
-    constexpr int WAVES = WG<T>::WAVES, THREADS = 64 * WAVES;
-    static_assert(2 * THREADS >= kMaxPieces<T> + 1, "two pieces per thread");
-    uint32_t *psrc = poff + kMaxPieces<T> + 1;  // kMaxPieces sources after kMaxPieces + 1 offsets
-    // (the GTile carries the chunk range and the bucket's start: the prefix tables are the only
-    // reads between the tile record and the keys)
+__device__ __forceinline__ void gather_tile(const sb::Gather &ga, const uint2 (&pe)[2], const sb::GTile &gt,
+                                            const T *in, uint32_t *ptab, uint32_t *wsum, T (&x)[R],
+                                            const int tid = threadIdx.x) {
+    constexpr int WAVES = WG<T>::WAVES, THREADS = 64 * WAVES, N = KPC<T>, KP = kMaxPieces<T>;
+    using V = typename V16<T>::type;
+    static_assert(2 * THREADS >= KP + 1, "two pieces per thread");
+    uint32_t *voff = ptab, *plo = ptab + KP + 1, *phi = plo + KP;  // vector offsets, piece bounds
+    // (the piece table, written by sb_scan_kernel, is read with the tile record: one round trip
+    // before the key loads)
     const int np = (int)gt.nch;
     const int lane = tid & 63, w = tid >> 6;
-    uint32_t len[2], src[2];
+    // (flags bit 0: a lone sub-bucket above the vector room, gathered key by key; nv = keys)
+    const bool keyw = (gt.flags & 1) != 0;
+    uint32_t nv[2], lo[2], hi[2];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
         const int k = 2 * tid + q;
-        len[q] = 0;
-        src[q] = 0;
+        nv[q] = lo[q] = hi[q] = 0;
         if (k < np) {
-            const uint32_t c = gt.c0 + (uint32_t)k;
-            const uint32_t *pc = ga.pref + (uint64_t)c * (ga.SS + 1);
-            const uint32_t lo = pc[gt.j0];
-            len[q] = pc[gt.j1] - lo;
-            src[q] = (uint32_t)gt.src + (uint32_t)k * (uint32_t)sb::SB_LCH<T> + lo;
+            lo[q] = pe[q].x;
+            hi[q] = pe[q].y;
+            nv[q] = lo[q] < hi[q] ? (keyw ? hi[q] - lo[q] : (hi[q] + N - 1) / N - lo[q] / N) : 0;
         }
     }
-    const uint32_t sum = len[0] + len[1];
+    const uint32_t sum = nv[0] + nv[1];
     uint32_t incl = wave_incl_sum(sum);
     if (lane == 63) wsum[w] = incl;
     __syncthreads();
-    uint32_t ex = incl - sum;
-    for (int i = 0; i < w; ++i) ex += wsum[i];
+    uint32_t ex = incl - sum, tot = 0;
+    for (int i = 0; i < WAVES; ++i) {
+        const uint32_t v = wsum[i];
+        ex += i < w ? v : 0;
+        tot += v;
+    }
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
         const int k = 2 * tid + q;
         if (k < np) {
-            poff[k] = ex;
-            psrc[k] = src[q];
+            voff[k] = ex;
+            plo[k] = lo[q];
+            phi[k] = hi[q];
         }
-        ex += len[q];
+        ex += nv[q];
     }
-    if (tid == 0) poff[np] = gt.valid;
+    if (tid == 0) voff[np] = tot;
     __syncthreads();
-    const uint32_t valid = gt.valid, e0 = (uint32_t)(w * WK + lane);
-    // piece of slot e0: the last k with poff[k] <= e0
-    int lo = 0, hi = np;
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (poff[mid] <= e0) lo = mid;
-        else hi = mid;
-    }
-    int k = lo;
-    uint32_t pend = poff[k + 1], pbase = psrc[k] - poff[k];
+    if (keyw) {
+        // slot e = w WK + 64 i + t of key offsets; piece of the first: the last k with voff[k] <= e
+        const uint32_t e0 = (uint32_t)(w * WK + lane);
+        int a = 0, b = np;
+        while (b - a > 1) {
+            const int mid = (a + b) >> 1;
+            if (voff[mid] <= e0) a = mid;
+            else b = mid;
+        }
+        int k = a;
+        uint32_t pend = voff[k + 1], pbase = plo[k] - voff[k];
 #pragma unroll
-    for (int i = 0; i < R; ++i) {
-        const uint32_t e = e0 + 64 * i;
-        if (e < valid) {
-            while (e >= pend) {
-                ++k;
-                pend = poff[k + 1];
-                pbase = psrc[k] - poff[k];
-            }
-            x[i] = in[pbase + e];
-        } else {
+        for (int i = 0; i < R; ++i) {
+            const uint32_t e = e0 + 64 * i;
             x[i] = key_max<T>();
+            if (e < tot) {
+                while (e >= pend) {
+                    ++k;
+                    pend = voff[k + 1];
+                    pbase = plo[k] - voff[k];
+                }
+                x[i] = in[pbase + e];
+            }
+        }
+        return;
+    }
+    const uint32_t e0 = (uint32_t)(w * (WK / N) + lane);
+    // piece of vector slot e0: the last k with voff[k] <= e0
+    int a = 0, b = np;
+    while (b - a > 1) {
+        const int mid = (a + b) >> 1;
+        if (voff[mid] <= e0) a = mid;
+        else b = mid;
+    }
+    int k = a;
+    uint32_t vend = voff[k + 1], pl = plo[k], ph = phi[k], vb = pl / N - voff[k];
+    uint32_t keep = 0;  // bit N i + j: key j of vector i belongs to the tile
+    // all loads first, the masks applied once they are in flight (a select right after its load
+    // would wait for that load before the next one issues)
+#pragma unroll
+    for (int i = 0; i < R / N; ++i) {
+        const uint32_t e = e0 + 64 * i;
+        if (e < tot) {
+            while (e >= vend) {
+                ++k;
+                vend = voff[k + 1];
+                pl = plo[k];
+                ph = phi[k];
+                vb = pl / N - voff[k];
+            }
+            const uint32_t g = (vb + e) * N;  // first key of the vector
+            V16<T>::get(*reinterpret_cast<const V *>(in + g), x + N * i);
+#pragma unroll
+            for (int j = 0; j < N; ++j) keep |= (uint32_t)(g + j >= pl && g + j < ph) << (N * i + j);
         }
     }
+#pragma unroll
+    for (int i = 0; i < R; ++i) x[i] = (keep >> i) & 1 ? x[i] : key_max<T>();
 }
 
 // Tile j's keys into x (any order; slots past `valid` are key_max).  Returns false when j is
@@ -1008,7 +1065,9 @@ __device__ __forceinline__ bool load_tile(const T *in, uint64_t n, const uint4 *
         const sb::GTile gt = ga.tiles[j];
         base = gt.base;
         valid = (int)gt.valid;
-        gather_tile<T>(ga, gt, in, poff, wsum, x, tid);
+        uint2 pe[2];
+        gather_pieces(ga, j, pe, tid);
+        gather_tile<T>(ga, pe, gt, in, poff, wsum, x, tid);
         return true;
     } else if (tiles) {
         if (j >= *ntiles) return false;
@@ -1060,7 +1119,7 @@ __global__ void __launch_bounds__(64 * WG<T>::WAVES, WG<T>::OCC) bin_sort_kernel
                                                                      const uint4 *tiles, const uint32_t *ntiles,
                                                                      sb::Gather ga, uint32_t *fb, uint32_t *nfb) {
     constexpr int TILE = TILE_OF<T>;
-    static_assert(128 + 2 * kMaxPieces<T> + 1 <= TILE * (int)sizeof(T) / 4, "the piece table fits in the tile");
+    static_assert(128 + 3 * kMaxPieces<T> + 1 <= TILE * (int)sizeof(T) / 4, "the piece table fits in the tile");
     __shared__ __attribute__((aligned(16))) T s[TILE];
     __shared__ __attribute__((aligned(16))) uint32_t cw[BIN_NB<T> / 2];
     // the counters are zeroed before the gather's barriers; the piece table of a gathered tile and
@@ -1081,6 +1140,8 @@ __global__ void __launch_bounds__(64 * WG<T>::WAVES, WG<T>::OCC) bin_sort_kernel
         // comes from HBM once and from that XCD's L2 the second time.
         j = xcd_block(blockIdx.x, gridDim.x);
         if (j >= *ntiles) return;
+        uint2 pe[2];
+        gather_pieces(ga, j, pe);
         const sb::GTile gt = ga.tiles[j];
         base = gt.base;
         valid = (int)gt.valid;
@@ -1105,7 +1166,7 @@ __global__ void __launch_bounds__(64 * WG<T>::WAVES, WG<T>::OCC) bin_sort_kernel
         const int jj = jl + lane_id();
         if (jj < jh && jj + 1 < nspl) hint = sp[jj].k == sp[jj + 1].k;
         hint = __ballot(hint) != 0;
-        gather_tile<T>(ga, gt, in, s32 + 128, s32 + 96, x, threadIdx.x);
+        gather_tile<T>(ga, pe, gt, in, s32 + 128, s32 + 96, x, threadIdx.x);
     } else {
         j = blockIdx.x;
         if (!load_tile<T, false>(in, n, tiles, ntiles, ga, j, nullptr, nullptr, x, base, valid)) return;
@@ -1139,10 +1200,11 @@ __global__ void __launch_bounds__(64 * WG<T>::WAVES, WG<T>::OCC) block_sort_w_ke
     uint64_t base;
     int valid;
     const uint32_t j = fb[i];
-    // (the piece table of a gathered tile sits in the slack, not in the runs)
-    if (!load_tile<T, GATHER>(in, n, tiles, ntiles, ga, j, reinterpret_cast<uint32_t *>(s + TILE),
+    // (the piece table of a gathered tile sits in the runs' space: a barrier before they are written)
+    if (!load_tile<T, GATHER>(in, n, tiles, ntiles, ga, j, reinterpret_cast<uint32_t *>(s) + 64,
                               reinterpret_cast<uint32_t *>(s), x, base, valid))
         return;
+    if (GATHER) __syncthreads();
     sort_wave(x, c);
     // lane-major run of the wave -> LDS; odd waves' runs (the B runs of the first level) are
     // stored descending
@@ -1561,6 +1623,7 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
     constexpr uint64_t ALIGN = KPC<T>;
     for (int b = 0; b < B && local; ++b)
         if (!pure[b] && ceil_div(hb[b + 1] - hb[b], (uint64_t)SB_LCH<T>) > (uint64_t)kMaxPieces<T>) local = false;
+    if (reinterpret_cast<uintptr_t>(src) % 16) local = false;  // (the gather reads aligned 16-byte vectors)
     const uint64_t CH = local ? SB_LCH<T> : SB_CH<T>;
     // samples per sub-bucket; a bucket's samples (<= SB_MAXS * 8) fit one int64 tile
     constexpr int kMaxOs = TILE_OF<int64_t> / SB_MAXS;
@@ -1574,11 +1637,20 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
     std::vector<BInfo> bi((size_t)B);
     uint64_t nsmp = 0, nch = 0, nsubs = 0;
     int SS = 1;
+    // local path: the piece tables' stride (most chunks of a bucket) and a bound on the tiles -- a
+    // greedy packing's consecutive tiles hold more than a tile's room together, so a bucket of len
+    // keys takes at most 2 len / room + 1 tiles
+    uint32_t PS = 1;
+    uint64_t tcap = 0;
     for (int b = 0; b < B; ++b) {
         const uint64_t len = pure[b] ? 0 : hb[b + 1] - hb[b];  // (a pure bucket: no chunks, no tiles)
         uint64_t ns = len <= (uint64_t)TILE ? 1 : ceil_div(len, m);
         ns = ns > (uint64_t)SB_MAXS ? SB_MAXS : ns;
         const uint64_t nc = ceil_div(len, CH);
+        if (local && len) {
+            PS = nc > PS ? (uint32_t)nc : PS;
+            tcap += 2 * len / ((uint64_t)TILE - 2 * (ALIGN - 1) * nc) + 1;
+        }
         bi[b] = BInfo{hb[b], nsmp, (uint32_t)len, (uint32_t)ns, ns > 1 ? (uint32_t)(ns * os) : 0u, (uint32_t)nch,
                       (uint32_t)(nch + nc), 0};
         nsmp += bi[b].ns;
@@ -1596,7 +1668,8 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
                  o_rng = take((size_t)B * SB_SLOTS * 4), o_sfn = take(B * sizeof(SlotFn<T>)),
                  o_cnt = take(nch * (SS + 1) * 4), o_offs = take(local ? 0 : nch * SS * 4),
                  o_tt = take(tmax * sizeof(GTile)),
-                 o_ovf = take(nsubs * sizeof(Ovf)), o_num = take(8), o_stl = take(B * sizeof(bk::TileRef) + 16);
+                 o_ovf = take(nsubs * sizeof(Ovf)), o_num = take(8), o_stl = take(B * sizeof(bk::TileRef) + 16),
+                 o_pcs = take(local ? tcap * PS * sizeof(uint2) : 0);
     int rc = ensure(ctx, &ctx->sub, &ctx->sub_bytes, off, "sub-bucket partition");
     if (rc) return rc;
     char *a = static_cast<char *>(ctx->sub);
@@ -1612,6 +1685,7 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
     Ovf *ovf = reinterpret_cast<Ovf *>(a + o_ovf);
     uint32_t *num = reinterpret_cast<uint32_t *>(a + o_num);  // tiles, merge records
     bk::TileRef *stl = reinterpret_cast<bk::TileRef *>(a + o_stl);  // sample tiles, then their count
+    uint2 *pcs = reinterpret_cast<uint2 *>(a + o_pcs);                // local path: piece tables
     // pinned staging: the two tables, the sample tiles + count, then the two counters read back
     const size_t h_ch = (B * sizeof(BInfo) + 15) & ~(size_t)15, h_stl = h_ch + nch * sizeof(Chunk);
     const size_t h_num = h_stl + B * sizeof(bk::TileRef) + 16;
@@ -1699,7 +1773,8 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
             if ((rc = stage_event(ctx, s, timed, 14))) return rc;
         }
         hipLaunchKernelGGL(sb_scan_kernel<true>, dim3((unsigned)B), dim3(SB_MAXS), 0, s, dbi, SS, cnt, nullptr, TILE, 1,
-                           0u, tt, num, nullptr, num + 1);
+                           0u, (uint32_t)(2 * (ALIGN - 1)), tt, num, nullptr, num + 1, pcs, PS, (uint32_t)tcap,
+                           (uint32_t)SB_LCH<T>);
         DSORT_HIP(ctx, hipGetLastError());
         DSORT_HIP(ctx, hipMemcpyAsync(hn, num, 8, hipMemcpyDeviceToHost, s));
         DSORT_HIP(ctx, hipEventRecord(ctx->sub_ev, s));
@@ -1708,12 +1783,12 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         DSORT_HIP(ctx, hipEventSynchronize(ctx->sub_ev));
         const uint32_t ntiles = hn[0], novf = hn[1];
         if (novf) return sub_sort<T>(ctx, src, d_keys, n, hb, B, m, s, timed, false, pure, pure_done, bspl);
-        if (ntiles > tmax) return set_err(ctx, DSORT_EHIP, "sub-bucket packing overflow");
+        if (ntiles > tmax || ntiles > tcap) return set_err(ctx, DSORT_EHIP, "sub-bucket packing overflow");
         fault_point(ctx, s, 1);  // second-level partition done
         ctx->stats.merge_passes = 0;
         // 3. tile sort: gathered from the chunks into d_keys
         if (ntiles) {
-            const Gather ga{static_cast<const GTile *>(tt), dch, dbi, cnt, SS, spl, bspl, B};
+            const Gather ga{static_cast<const GTile *>(tt), dch, dbi, cnt, pcs, PS, SS, spl, bspl, B};
             rc = tile_sort<T, true>(ctx, src, d_keys, n, nullptr, num, ga, ntiles, s, timed);
             if (rc) return rc;
         }
@@ -1733,7 +1808,7 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         DSORT_HIP(ctx, hipGetLastError());
     }
     hipLaunchKernelGGL(sb_scan_kernel<false>, dim3((unsigned)B), dim3(SB_MAXS), 0, s, dbi, SS, cnt, offs, TILE,
-                       (int)ALIGN, mis, tt, num, ovf, num + 1);
+                       (int)ALIGN, mis, 0u, tt, num, ovf, num + 1, nullptr, 0u, 0u, 0u);
     DSORT_HIP(ctx, hipGetLastError());
     DSORT_HIP(ctx, hipMemcpyAsync(hn, num, 8, hipMemcpyDeviceToHost, s));
     DSORT_HIP(ctx, hipEventRecord(ctx->sub_ev, s));
@@ -1818,7 +1893,8 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
     TileRef *tt = reinterpret_cast<TileRef *>(a + o_tt);
     uint32_t *ntl = reinterpret_cast<uint32_t *>(a + o_nt);
     BkMap *map = reinterpret_cast<BkMap *>(a + o_map);
-    rc = ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, n * sizeof(T), "sort scratch");
+    // (+ 16 bytes: the gathering tile sort reads the 16-byte vector that holds the last key)
+    rc = ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, n * sizeof(T) + 16, "sort scratch");
     if (rc) return rc;
     T *scratch = static_cast<T *>(ctx->scratch);
     const size_t hbytes = (size_t)(BK_MAXB + 1) * 8 + (size_t)BK_MAXB * 16;  // starts, then the splitters
@@ -2210,6 +2286,9 @@ static int wave_merge(dsort_ctx *ctx, const T *d_in, const size_t *lens, int k, 
 #ifdef DSORT_STAMPS
 extern "C" int dsort_debug_stamps(void *host, size_t bytes) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(wv::g_stamps), bytes) == hipSuccess ? 0 : -1;
+}
+extern "C" int dsort_debug_bkstamps(void *host, size_t bytes) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(bk::g_bkstamps), bytes) == hipSuccess ? 0 : -1;
 }
 extern "C" int dsort_debug_sbstamps(void *host, size_t bytes) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(sb::g_sbstamps), bytes) == hipSuccess ? 0 : -1;

@@ -25,10 +25,10 @@ fn = ctx.lib.dsort_debug_bkstamps
 fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
 assert fn(buf.ctypes.data, buf.nbytes) == 0
 S = buf.reshape(-1, 16).astype(np.float64)
-S = S[S[:, :9].sum(axis=1) > 0]
-names = ["zero+loads+lookup+atomics", "scan", "st+map clear", "lk writes", "max-scan", "map write",
-         "lines", "barrier", "carry"]
-tot = S[:, :9].sum(axis=1)
+S = S[S[:, :6].sum(axis=1) > 0]
+names = ["loads wait + classify + rank | A", "scan | B", "owner starts, line map | C", "keys to LDS | D",
+         "lines (HBM writes) | E (+ the last sub-tile's tail)", "carry"]
+tot = S[:, :6].sum(axis=1)
 print(f"workgroups {len(S)}  cycles per workgroup: mean {tot.mean():.0f}")
 for k, nm in enumerate(names):
-    print(f"  {nm:28s} {S[:, k].mean():12.0f}  {100 * S[:, k].mean() / tot.mean():5.1f} %")
+    print(f"  {nm:48s} {S[:, k].mean():12.0f}  {100 * S[:, k].mean() / tot.mean():5.1f} %")
