@@ -513,25 +513,28 @@ __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restric
 // dsort_debug_sbstamps().
 __device__ unsigned long long g_sbstamps[(1u << 18) * 8];
 #endif
-constexpr int SB_LT = 512;
-// keys per thread: the chunk (int32 62 KiB, int64 52 KiB) + tables fit two workgroups per CU
-template <typename T> constexpr int SB_LKPT = sizeof(T) == 4 ? 31 : 13;
+// int32: 1024 threads of 15 keys, 8 waves per SIMD at two workgroups per CU: twice the waves of
+// round 2's 512 threads of 31 keys to hide the lookups' LDS round trips (2.33 -> 2.02 ms at 2^30).
+// (int64 at 1024 threads of 6 keys: C4 -0.24 ms, 2^30 uniform int64 +0.4 ms; kept at 512 x 13)
+template <typename T> constexpr int SB_LT = sizeof(T) == 4 ? 1024 : 512;
+// keys per thread: the chunk (int32 60 KiB, int64 52 KiB) + tables fit two workgroups per CU
+template <typename T> constexpr int SB_LKPT = sizeof(T) == 4 ? 15 : 13;
 
-template <typename T> constexpr int SB_LCH = SB_LT * SB_LKPT<T>;
+template <typename T> constexpr int SB_LCH = SB_LT<T> * SB_LKPT<T>;
 
 template <typename T>
-__global__ void __launch_bounds__(SB_LT, 4) sb_local_kernel(T *__restrict__ buf, const Chunk *__restrict__ ch,
+__global__ void __launch_bounds__(SB_LT<T>, SB_LT<T> / 128) sb_local_kernel(T *__restrict__ buf, const Chunk *__restrict__ ch,
                                                          const BInfo *__restrict__ bi, int SS,
                                                          const Spl<T> *__restrict__ spl_g,
                                                          const uint32_t *__restrict__ rng_g,
                                                          const SlotFn<T> *__restrict__ sfn,
                                                          uint32_t *__restrict__ pref) {
-    constexpr int KPT = SB_LKPT<T>, CHL = SB_LCH<T>, PER = SB_MAXS / SB_LT;
-    static_assert(SB_MAXS % SB_LT == 0, "sub-buckets per thread");
+    constexpr int LT = SB_LT<T>, KPT = SB_LKPT<T>, CHL = SB_LCH<T>, PER = SB_MAXS / LT;
+    static_assert(SB_MAXS % LT == 0, "sub-buckets per thread");
     __shared__ Spl<T> spl[SB_MAXS + 1];
     __shared__ uint32_t rng[SB_SLOTS];
     __shared__ uint32_t hist[SB_MAXS];   // chunk histogram, then the LDS starts
-    __shared__ uint32_t wsum[SB_LT / 64];
+    __shared__ uint32_t wsum[LT / 64];
     __shared__ T lk[CHL];
 #ifdef DSORT_STAMPS
     uint64_t st_acc[6] = {}, st_t0 = __builtin_amdgcn_s_memtime();
@@ -562,7 +565,7 @@ __global__ void __launch_bounds__(SB_LT, 4) sb_local_kernel(T *__restrict__ buf,
     T key[KPT];
 #pragma unroll
     for (int k = 0; k < KPT; ++k) {
-        const uint32_t i = tid + k * SB_LT;
+        const uint32_t i = tid + k * LT;
         key[k] = i < c.len ? src[i] : T(0);
     }
     load_sub_tables<T>(b, c.b, SS, spl_g, rng_g, spl, rng);
@@ -580,14 +583,14 @@ __global__ void __launch_bounds__(SB_LT, 4) sb_local_kernel(T *__restrict__ buf,
         if (c.len == (uint32_t)CHL) {  // a whole chunk (all but a bucket's last): no per-key branch
 #pragma unroll
             for (int k = 0; k < KPT; ++k) {
-                const uint32_t i = tid + k * SB_LT;
+                const uint32_t i = tid + k * LT;
                 const int j = sub_of<T>(spl, rng, f.klo, f.sh, key[k], (uint32_t)(c.start + i));
                 pk[k] = (uint32_t)j | atomicAdd(&hist[j], 1u) << 10;
             }
         } else
 #pragma unroll
         for (int k = 0; k < KPT; ++k) {
-            const uint32_t i = tid + k * SB_LT;
+            const uint32_t i = tid + k * LT;
             if (i < c.len) {
                 const int j = sub_of<T>(spl, rng, f.klo, f.sh, key[k], (uint32_t)(c.start + i));
                 pk[k] = (uint32_t)j | atomicAdd(&hist[j], 1u) << 10;
@@ -613,7 +616,7 @@ __global__ void __launch_bounds__(SB_LT, 4) sb_local_kernel(T *__restrict__ buf,
 #pragma unroll
         for (int u = 0; u < G; ++u)
             if (g0 + u < KPT) {
-                const uint32_t i = tid + (g0 + u) * SB_LT;
+                const uint32_t i = tid + (g0 + u) * LT;
                 const int j = sub_pick<T>(spl, r[u], sa[u], sb[u], key[g0 + u], (uint32_t)(c.start + i));
                 // (a key past the chunk adds 0 to a lane-spread counter, not all to one)
                 pk[g0 + u] = (uint32_t)j | atomicAdd(&hist[i < c.len ? j : lane], i < c.len ? 1u : 0u) << 10;
@@ -634,7 +637,7 @@ __global__ void __launch_bounds__(SB_LT, 4) sb_local_kernel(T *__restrict__ buf,
     SBST(2);
     uint32_t ex = incl - sum;
 #pragma unroll
-    for (int i = 0; i < SB_LT / 64; ++i) ex += i < w ? wsum[i] : 0u;
+    for (int i = 0; i < LT / 64; ++i) ex += i < w ? wsum[i] : 0u;
     if (tid == 0) pc[ns] = c.len;
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
@@ -651,18 +654,18 @@ __global__ void __launch_bounds__(SB_LT, 4) sb_local_kernel(T *__restrict__ buf,
         __syncthreads();
         SBST(4);
 #pragma unroll
-        for (int k = 0; k < KPT; ++k) src[tid + k * SB_LT] = lk[tid + k * SB_LT];
+        for (int k = 0; k < KPT; ++k) src[tid + k * LT] = lk[tid + k * LT];
     } else {
 #pragma unroll
     for (int k = 0; k < KPT; ++k) {
-        const uint32_t i = tid + k * SB_LT;
+        const uint32_t i = tid + k * LT;
         if (i < c.len) lk[hist[pk[k] & 1023] + (pk[k] >> 10)] = key[k];
     }
     __syncthreads();
     SBST(4);
 #pragma unroll
     for (int k = 0; k < KPT; ++k) {
-        const uint32_t i = tid + k * SB_LT;
+        const uint32_t i = tid + k * LT;
         if (i < c.len) src[i] = lk[i];
     }
     }

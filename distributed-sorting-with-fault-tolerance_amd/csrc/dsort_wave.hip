@@ -1767,7 +1767,7 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         // 2. every chunk partitioned in place (cnt = the prefix tables), sub-bucket starts, tiles
         if (nch) {
             if ((rc = stage_event(ctx, s, timed, 13))) return rc;
-            hipLaunchKernelGGL(sb_local_kernel<T>, dim3((unsigned)nch), dim3(SB_LT), 0, s, src, dch, dbi, SS, spl, rng,
+            hipLaunchKernelGGL(sb_local_kernel<T>, dim3((unsigned)nch), dim3(SB_LT<T>), 0, s, src, dch, dbi, SS, spl, rng,
                                sfn, cnt);
             DSORT_HIP(ctx, hipGetLastError());
             if ((rc = stage_event(ctx, s, timed, 14))) return rc;
