@@ -508,6 +508,14 @@ __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restric
 // [j0, j1) of a bucket) is then one contiguous piece of every chunk of the bucket,
 // [pref[c][j0], pref[c][j1]), gathered by the tile sort (about 1 KiB per piece) -- no
 // element-granular scatter to HBM.
+// Workgroup -> chunk: every XCD takes a contiguous block of chunks, i.e. of buckets, so the
+// workgroups that write pieces of the same sub-buckets share an L2 (a bijection on [0, G)).
+__device__ __forceinline__ uint32_t sb_chunk_order(uint32_t bid, uint32_t G) {
+    constexpr uint32_t NX = 8;
+    const uint32_t q = G / NX, r = G % NX, x = bid % NX, i = bid / NX;
+    return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
+}
+
 #ifdef DSORT_STAMPS
 // Diagnostic build only: per-workgroup phase cycles of sb_local_kernel, read back by
 // dsort_debug_sbstamps().
@@ -549,9 +557,12 @@ __global__ void __launch_bounds__(SB_LT<T>, SB_LT<T> / 128) sb_local_kernel(T *_
     do {        \
     } while (0)
 #endif
-    const Chunk c = ch[blockIdx.x];
+    // (every XCD takes a contiguous block of chunks, i.e. of buckets: a bucket's tables and the
+    // lines its neighbouring chunks share stay in one L2; measured neutral to -0.05 ms)
+    const uint32_t cid = sb_chunk_order(blockIdx.x, gridDim.x);
+    const Chunk c = ch[cid];
     const BInfo b = bi[c.b];
-    uint32_t *pc = pref + (uint64_t)blockIdx.x * (SS + 1);
+    uint32_t *pc = pref + (uint64_t)cid * (SS + 1);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int ns = (int)b.nsub;
     if (ns == 1) {
@@ -677,13 +688,6 @@ __global__ void __launch_bounds__(SB_LT<T>, SB_LT<T> / 128) sb_local_kernel(T *_
 #undef SBST
 }
 
-// Workgroup -> chunk: every XCD takes a contiguous block of chunks, i.e. of buckets, so the
-// workgroups that write pieces of the same sub-buckets share an L2 (a bijection on [0, G)).
-__device__ __forceinline__ uint32_t sb_chunk_order(uint32_t bid, uint32_t G) {
-    constexpr uint32_t NX = 8;
-    const uint32_t q = G / NX, r = G % NX, x = bid % NX, i = bid / NX;
-    return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
-}
 
 // Per sub-tile (SB_SUB keys): sub-bucket and slot of every key (LDS atomic), scan, keys grouped
 // by sub-bucket in LDS, then consecutive threads write consecutive keys of a sub-bucket to

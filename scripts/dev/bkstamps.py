@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""Phase cycle sums of the int32 line scatter from a DSORT_STAMPS build (DSORT_LIB=...): per
-workgroup (wave 0's view), averaged over workgroups; dev tool."""
+"""Phase cycle sums of the line scatter from a DSORT_STAMPS build (DSORT_LIB=...): per workgroup
+(wave 0's view), averaged over workgroups; dev tool.   bkstamps.py [i32|i64z]"""
 import ctypes
 import os
 import sys
@@ -14,8 +14,12 @@ import dsort  # noqa: E402
 
 n = 1 << 30
 ctx = dsort.Context(0)
-t = torch.empty(n, dtype=torch.int32, device="cuda")
-ctx.gen_uniform(t, 0x5EED2026)
+if len(sys.argv) > 1 and sys.argv[1] == "i64z":
+    t = torch.empty(n, dtype=torch.int64, device="cuda")
+    ctx.gen_zipf_i64(t, 0x5EED2026)
+else:
+    t = torch.empty(n, dtype=torch.int32, device="cuda")
+    ctx.gen_uniform(t, 0x5EED2026)
 o = torch.empty_like(t)
 ctx.sort_dev(t, o)
 ctx.sort_dev(t, o)
