@@ -691,6 +691,7 @@ int dsort_finalize(dsort_ctx *ctx) {
     if (ctx->sub_host) (void)hipHostFree(ctx->sub_host);
     if (ctx->sub_ev) (void)hipEventDestroy(ctx->sub_ev);
     if (ctx->side_ev) (void)hipEventDestroy(ctx->side_ev);
+    if (ctx->ready_ev) (void)hipEventDestroy(ctx->ready_ev);
     if (ctx->side) (void)hipStreamDestroy(ctx->side);
     if (ctx->done_ev) (void)hipEventDestroy(ctx->done_ev);
     for (auto &e : ctx->ev)

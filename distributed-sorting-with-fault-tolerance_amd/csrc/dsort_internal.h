@@ -98,8 +98,9 @@ struct dsort_ctx {
     void *sub_host = nullptr;     // pinned: bucket table, chunk table, tile / merge-record counts
     size_t sub_host_bytes = 0;
     hipEvent_t sub_ev = nullptr;
-    hipStream_t side = nullptr;   // table uploads that overlap the first-level scatter
-    hipEvent_t side_ev = nullptr;
+    hipStream_t side = nullptr;   // copies that overlap the first-level scatter (both directions)
+    hipEvent_t side_ev = nullptr;  // side -> sort stream
+    hipEvent_t ready_ev = nullptr; // sort stream -> side
     // End of the last sort / merge on its stream: a call on another stream waits for it, since
     // the arenas are shared and a call returns while its last kernels still run.
     hipEvent_t done_ev = nullptr;

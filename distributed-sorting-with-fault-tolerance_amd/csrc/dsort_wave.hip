@@ -1615,6 +1615,17 @@ static std::vector<size_t> sub_tile_runs(uint64_t p, uint64_t len, uint64_t tile
 // d_keys (sb_scatter_kernel) and the tile sort reads contiguous tiles.  Local needs no oversized
 // sub-bucket and at most kMaxPieces chunks per bucket; otherwise the scatter path runs (on the
 // locally partitioned keys, if the local pass already ran: still the same buckets).
+// The context's side stream and its two events (created on first use).
+static int side_stream(dsort_ctx *ctx) {
+    if (!ctx->side && hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess)
+        return set_err(ctx, DSORT_EHIP, "hipStreamCreate");
+    if (!ctx->side_ev && hipEventCreateWithFlags(&ctx->side_ev, hipEventDisableTiming) != hipSuccess)
+        return set_err(ctx, DSORT_EHIP, "hipEventCreate");
+    if (!ctx->ready_ev && hipEventCreateWithFlags(&ctx->ready_ev, hipEventDisableTiming) != hipSuccess)
+        return set_err(ctx, DSORT_EHIP, "hipEventCreate");
+    return DSORT_OK;
+}
+
 template <typename T>
 static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_t *hb, int B, uint64_t m,
                     hipStream_t s, bool timed, bool local, const uint8_t *pure, bool pure_done, const void *bspl) {
@@ -1716,16 +1727,13 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
     // reads them.  (On s they queued behind the scatter: about 60 us of idle GPU per sort at 2^30.)
     // Nothing still reads the arena: the host got here after waiting for the histogram of this
     // sort, which follows every kernel of the previous sort on s.
-    if (!ctx->side && hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess)
-        return set_err(ctx, DSORT_EHIP, "hipStreamCreate");
-    if (!ctx->side_ev && hipEventCreateWithFlags(&ctx->side_ev, hipEventDisableTiming) != hipSuccess)
-        return set_err(ctx, DSORT_EHIP, "hipEventCreate");
+    if ((rc = side_stream(ctx))) return rc;
     DSORT_HIP(ctx, hipMemcpyAsync(dbi, h, B * sizeof(BInfo), hipMemcpyHostToDevice, ctx->side));
     if (nch) DSORT_HIP(ctx, hipMemcpyAsync(dch, h + h_ch, nch * sizeof(Chunk), hipMemcpyHostToDevice, ctx->side));
     DSORT_HIP(ctx, hipMemcpyAsync(stl, hst, B * sizeof(bk::TileRef) + 16, hipMemcpyHostToDevice, ctx->side));
+    DSORT_HIP(ctx, hipMemsetAsync(num, 0, 8, ctx->side));
     DSORT_HIP(ctx, hipEventRecord(ctx->side_ev, ctx->side));
     DSORT_HIP(ctx, hipStreamWaitEvent(s, ctx->side_ev, 0));
-    DSORT_HIP(ctx, hipMemsetAsync(num, 0, 8, s));
     uint64_t npure = 0;
     for (int b = 0; b < B; ++b) npure += pure[b] ? hb[b + 1] - hb[b] : 0;
     ctx->stats.tile_sort_keys = n - npure;
@@ -1961,10 +1969,15 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
     // them while the scatter runs.  The scatter always writes the scratch buffer (never the
     // input: the context owns it); the tile sort then writes whichever buffer makes the last
     // pass land in d_keys.
-    DSORT_HIP(ctx, hipMemcpyAsync(hb, bst, (size_t)(B + 1) * 8, hipMemcpyDeviceToHost, s));
+    // (the copies run on the side stream once the offsets are written, so the scatter does not
+    // queue behind them: ~10 us of idle GPU per sort)
+    if ((rc = side_stream(ctx))) return rc;
+    DSORT_HIP(ctx, hipEventRecord(ctx->ready_ev, s));
+    DSORT_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->ready_ev, 0));
+    DSORT_HIP(ctx, hipMemcpyAsync(hb, bst, (size_t)(B + 1) * 8, hipMemcpyDeviceToHost, ctx->side));
     C *hspl = reinterpret_cast<C *>(hb + BK_MAXB + 1);
-    DSORT_HIP(ctx, hipMemcpyAsync(hspl, spl, (size_t)(B - 1) * sizeof(C), hipMemcpyDeviceToHost, s));
-    DSORT_HIP(ctx, hipEventRecord(ctx->bucket_ev, s));
+    DSORT_HIP(ctx, hipMemcpyAsync(hspl, spl, (size_t)(B - 1) * sizeof(C), hipMemcpyDeviceToHost, ctx->side));
+    DSORT_HIP(ctx, hipEventRecord(ctx->bucket_ev, ctx->side));
     T *part_out = scratch;
     // Pure buckets (one key, see below) go straight to d_keys, in their final places, when the
     // second level runs (it skips them) and d_keys is not the input the scatter still reads.
