@@ -39,7 +39,11 @@ constexpr int BK_CHUNK = 64;             // workgroups per column-sum chunk
 // Scatter sub-tile per key width: KPT keys per thread, SUB = BK_T * KPT keys staged in LDS
 // (int32: 56 KiB next to the 64 KiB line carry of the line scatter; 12 and 13 measured slower).
 template <typename T> struct Geo;
+#ifdef DSORT_BK_K16
+template <> struct Geo<int32_t> { static constexpr int KPT = 16; };
+#else
 template <> struct Geo<int32_t> { static constexpr int KPT = 14; };
+#endif
 template <> struct Geo<int64_t> { static constexpr int KPT = 6; };  // 48 KiB next to the 64 KiB carry
 
 struct TileRef {
@@ -214,11 +218,12 @@ __device__ __forceinline__ void build_slots(const typename Comp<T>::C *spl, int 
             }
         }
         if constexpr (!CT::ADAPT && PACK) {
-            // int32: lo (bits 0-9), splitters in the slot (bits 10-11; 3 = three or more) and bits
-            // 20..1 of the flipped key of the slot's first splitter (bits 12-31): see bucket_fast
+            // int32: lo (bits 0-9), splitters in the slot (bits 10-11: 0, 1, 2 = two or more) and
+            // bits 20..1 of the flipped key of the slot's one splitter, or the number of splitters
+            // of a crowded slot (bits 12-31): see bucket_fast
             const uint32_t in = cnt[1] - cnt[0];
-            const uint32_t kb = in ? ((uint32_t)CT::key_of(spl[cnt[0]]) ^ 0x80000000u) << 11 >> 12 : 0u;
-            rng[i] = cnt[0] | (in > 3 ? 3u : in) << 10 | kb << 12;
+            const uint32_t kb = in == 1 ? ((uint32_t)CT::key_of(spl[cnt[0]]) ^ 0x80000000u) << 11 >> 12 : in;
+            rng[i] = cnt[0] | (in > 2 ? 2u : in) << 10 | kb << 12;
         } else {
             // a slot whose (>= 2) splitters all hold one key K: see bucket_fast
             const bool one = CT::ADAPT && cnt[1] >= cnt[0] + 2 && CT::key_of(spl[cnt[0]]) == CT::key_of(spl[cnt[1] - 1]);
@@ -241,7 +246,7 @@ __device__ __forceinline__ void build_slots(const typename Comp<T>::C *spl, int 
 // top 11 bits), so a key in a slot of at most one splitter needs no splitter read -- the usual
 // case: uniform keys put one splitter in every other slot, about 2^22 values apart.  A key equal
 // to that splitter in bits 31..1 compares its composite; a slot of two or more splitters searches
-// them (its end from the next slot's entry).  (Round 2 read the splitter for every key of a slot
+// them (their number is in the entry).  (Round 2 read the splitter for every key of a slot
 // that had one: half of the keys, a dependent 8-byte LDS read on the way to the rank atomic.)
 template <typename T, bool PACK>
 __device__ __forceinline__ int bucket_fast(const typename Comp<T>::C *spl, const uint32_t *rng, uint32_t slot,
@@ -257,7 +262,7 @@ __device__ __forceinline__ int bucket_fast(const typename Comp<T>::C *spl, const
         const bool slow = in > 1 || (in == 1 && kb == sb);
         if (__builtin_expect(__ballot(slow) == 0, 1)) return j;
         if (!slow) return j;
-        int hi = in == 1 ? lo + 1 : in == 2 ? lo + 2 : slot + 1 < (uint32_t)BK_SLOTS ? (int)(rng[slot + 1] & 1023) : BK_MAXB;
+        int hi = lo + (in == 1 ? 1 : (int)sb);  // (the splitters searched: those of the slot)
         while (lo < hi) {
             const int mid = (lo + hi) >> 1;
             if (Comp<T>::lt(spl[mid], c)) lo = mid + 1;
@@ -647,7 +652,14 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
     constexpr int KPT = Geo<T>::KPT, SUB = G::SUB, LK = G::LK, KPL = G::KPL;
     static_assert(SUB + LK < (1 << 16) && LK <= 16, "packed fields");
     // (a non-last sub-tile writes <= (SUB + (LK-1) B) / LK lines, the last <= (SUB + 2 (LK-1) B) / LK)
-    __shared__ typename CT::C spl[BK_MAXB + 1];
+#ifdef DSORT_BK_K16
+    // int32: the splitters are staged in lk for the slot table only (the packed lookup reads them
+    // from global memory on its rare slow path), which leaves lk room for 16 keys per thread
+    constexpr bool SPL_LK = !CT::ADAPT;
+#else
+    constexpr bool SPL_LK = false;
+#endif
+    __shared__ typename CT::C spl_own[SPL_LK ? 1 : BK_MAXB + 1];
     __shared__ uint32_t rng[BK_SLOTS];
     __shared__ uint32_t hist[BK_MAXB];               // sub-tile histogram, then the LDS starts
     __shared__ uint2 st[BK_MAXB];                    // per bucket: LDS start | first line << 16, vc|ph|pure|L
@@ -656,6 +668,9 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
     __shared__ uint32_t wsum[BK_T / 64];
     __shared__ T lk[SUB];                            // the sub-tile's new keys grouped by bucket
     __shared__ T carry[BK_MAXB * LK];                // per bucket: stream entries not yet written (< LK)
+    static_assert(!SPL_LK || sizeof(lk) >= (BK_MAXB + 1) * sizeof(typename CT::C), "splitters staged in lk");
+    typename CT::C *spl = SPL_LK ? reinterpret_cast<typename CT::C *>(lk) : spl_own;
+    const typename CT::C *spl_look = SPL_LK ? spl_g : spl;  // (global: only BP entries, searched within a slot)
     const int tb = threadIdx.x, lane = tb & 63, w = tb >> 6;
     const uint32_t g = blockIdx.x;
     const bool owner = tb < B;  // thread b owns bucket b's line stream
@@ -708,7 +723,7 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
             const uint64_t i = s0 + tb + (uint64_t)k * BK_T;
             pk[k] = ~0u;
             if (i < n) {
-                const int b = bucket_fast<T, true>(spl, rng, sl[k], key[k], CT::make(key[k], i));
+                const int b = bucket_fast<T, true>(spl_look, rng, sl[k], key[k], CT::make(key[k], i));
                 pk[k] = atomicAdd(&hist[b], 1u) | (uint32_t)b << 16;
             }
         }

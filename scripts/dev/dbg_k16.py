@@ -1,0 +1,25 @@
+#!/usr/bin/env python3
+"""dev: the B=2, 200-tile case of test_bucketed_sort_multi_pass_buckets with the stats printed."""
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(REPO, "distributed-sorting-with-fault-tolerance_amd"))
+import torch  # noqa: E402
+import dsort  # noqa: E402
+
+ctx = dsort.Context(0)
+for tiles in (200, 300):
+    rng = np.random.default_rng(tiles)
+    n = 2 * tiles * 16384 + 777
+    a = rng.integers(-(2**31), 2**31 - 1, n, endpoint=True).astype(np.int32)
+    t = torch.from_numpy(a).cuda()
+    o = torch.empty_like(t)
+    with ctx.options(buckets=2):
+        ctx.sort_dev(t, o)
+        torch.cuda.synchronize()
+        st = ctx.stats()
+    ok = np.array_equal(o.cpu().numpy(), np.sort(a))
+    print(tiles, "ok", ok, {k: st[k] for k in ("merge_passes", "tile_sort_keys", "bucket_scatter_ms", "sub_partition_ms")})
