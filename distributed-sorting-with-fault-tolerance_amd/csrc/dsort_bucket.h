@@ -37,13 +37,9 @@ constexpr int BK_OS = 32;                // samples per bucket
 constexpr int BK_CHUNK = 64;             // workgroups per column-sum chunk
 
 // Scatter sub-tile per key width: KPT keys per thread, SUB = BK_T * KPT keys staged in LDS
-// (int32: 56 KiB next to the 64 KiB line carry of the line scatter; 12 and 13 measured slower).
+// (int32: 64 KiB next to the 64 KiB line carry of the line scatter).
 template <typename T> struct Geo;
-#ifdef DSORT_BK_K16
-template <> struct Geo<int32_t> { static constexpr int KPT = 16; };
-#else
-template <> struct Geo<int32_t> { static constexpr int KPT = 14; };
-#endif
+template <> struct Geo<int32_t> { static constexpr int KPT = 16; };  // (14: +0.09 ms; 12, 13 slower still)
 template <> struct Geo<int64_t> { static constexpr int KPT = 6; };  // 48 KiB next to the 64 KiB carry
 
 struct TileRef {
@@ -652,13 +648,9 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
     constexpr int KPT = Geo<T>::KPT, SUB = G::SUB, LK = G::LK, KPL = G::KPL;
     static_assert(SUB + LK < (1 << 16) && LK <= 16, "packed fields");
     // (a non-last sub-tile writes <= (SUB + (LK-1) B) / LK lines, the last <= (SUB + 2 (LK-1) B) / LK)
-#ifdef DSORT_BK_K16
     // int32: the splitters are staged in lk for the slot table only (the packed lookup reads them
     // from global memory on its rare slow path), which leaves lk room for 16 keys per thread
     constexpr bool SPL_LK = !CT::ADAPT;
-#else
-    constexpr bool SPL_LK = false;
-#endif
     __shared__ typename CT::C spl_own[SPL_LK ? 1 : BK_MAXB + 1];
     __shared__ uint32_t rng[BK_SLOTS];
     __shared__ uint32_t hist[BK_MAXB];               // sub-tile histogram, then the LDS starts

@@ -1639,11 +1639,13 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
     // samples per sub-bucket; a bucket's samples (<= SB_MAXS * 8) fit one int64 tile
     constexpr int kMaxOs = TILE_OF<int64_t> / SB_MAXS;
     int os = ctx->opt.sub_os > 0 ? (ctx->opt.sub_os < kMaxOs ? (int)ctx->opt.sub_os : kMaxOs) : 4;
-    // buckets so large that even SB_MAXS sub-buckets average above a quarter tile: sample at the
-    // maximum rate, so the size spread (about 1/sqrt(os)) keeps every sub-bucket below a tile
+    // buckets so large that even SB_MAXS sub-buckets average above an eighth of a tile: sample at
+    // the maximum rate, so the size spread (about 1/sqrt(os)) keeps every sub-bucket below a tile
+    // (at a quarter tile and os = 4, about one sort in 30 of two 3.3M-key buckets met a sub-bucket
+    // above a tile and took the scatter path)
     if (ctx->opt.sub_os <= 0)
         for (int b = 0; b < B; ++b)
-            if (!pure[b] && hb[b + 1] - hb[b] > (uint64_t)SB_MAXS * TILE / 4) os = kMaxOs;
+            if (!pure[b] && hb[b + 1] - hb[b] > (uint64_t)SB_MAXS * TILE / 8) os = kMaxOs;
     // bucket and chunk tables
     std::vector<BInfo> bi((size_t)B);
     uint64_t nsmp = 0, nch = 0, nsubs = 0;
