@@ -40,11 +40,9 @@ constexpr int BK_CHUNK = 64;             // workgroups per column-sum chunk
 // (int32: 64 KiB next to the 64 KiB line carry of the line scatter).
 template <typename T> struct Geo;
 template <> struct Geo<int32_t> { static constexpr int KPT = 16; };  // (14: +0.09 ms; 12, 13 slower still)
-#ifdef DSORT_BK_K8
-template <> struct Geo<int64_t> { static constexpr int KPT = 8; };
-#else
-template <> struct Geo<int64_t> { static constexpr int KPT = 6; };  // 48 KiB next to the 64 KiB carry
-#endif
+// int64: 48 KiB next to the 64 KiB carry (8 keys with the splitters read from global memory on
+// the lookups: C4 scatter 6.47 -> 7.09 ms)
+template <> struct Geo<int64_t> { static constexpr int KPT = 6; };
 
 struct TileRef {
     uint64_t base;   // first key of the tile
@@ -654,11 +652,7 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
     // (a non-last sub-tile writes <= (SUB + (LK-1) B) / LK lines, the last <= (SUB + 2 (LK-1) B) / LK)
     // int32: the splitters are staged in lk for the slot table only (the packed lookup reads them
     // from global memory on its rare slow path), which leaves lk room for 16 keys per thread
-#ifdef DSORT_BK_K8
-    constexpr bool SPL_LK = true;
-#else
     constexpr bool SPL_LK = !CT::ADAPT;
-#endif
     __shared__ typename CT::C spl_own[SPL_LK ? 1 : BK_MAXB + 1];
     __shared__ uint32_t rng[BK_SLOTS];
     __shared__ uint32_t hist[BK_MAXB];               // sub-tile histogram, then the LDS starts
