@@ -642,7 +642,7 @@ template <typename T>
 __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__restrict__ in, uint64_t n,
                                                                     const typename Comp<T>::C *__restrict__ spl_g,
                                                                     const BkMap *__restrict__ map, int B, int BP, int subs,
-                                                                    const uint64_t *__restrict__ offs,
+                                                                    const uint32_t *__restrict__ offs,
                                                                     T *__restrict__ out, T *__restrict__ out2) {
     using CT = Comp<T>;
     using G = LineGeo<T>;
@@ -672,7 +672,7 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
     // front (the stream's first line not written yet), gb = global index of stream entry 0 (mod 2^32)
     uint32_t vc = 0, ph = 0, gb = 0, pure = 0;
     if (owner) {
-        const uint32_t o = (uint32_t)offs[(uint64_t)g * B + tb];
+        const uint32_t o = offs[(uint64_t)g * B + tb];
         pure = out2 && tb > 0 && tb + 1 < B && CT::key_of(spl_g[tb - 1]) == CT::key_of(spl_g[tb]);
         ph = (uint32_t)(((uintptr_t)((pure ? out2 : out) + o) / sizeof(T)) & (LK - 1));
         vc = ph;

@@ -487,17 +487,18 @@ __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restric
     }
     if constexpr (LOCAL) {
         __syncthreads();
-        // the piece tables: (tile, chunk) pairs spread over the workgroup
-        const uint32_t nch = b.c1 - b.c0;
-        for (uint32_t q = threadIdx.x; q < (uint32_t)nc * nch; q += blockDim.x) {
-            const uint32_t t = q / nch, c = q - t * nch;
+        // the piece tables: a wave per tile, a lane per chunk (no division per entry)
+        const uint32_t nch = b.c1 - b.c0, lane = threadIdx.x & 63;
+        for (uint32_t t = threadIdx.x >> 6; t < (uint32_t)nc; t += blockDim.x >> 6) {
             if (tix[t] == 0xFFFF) continue;
             const uint32_t k = tbase + tix[t];
             if (k >= tcap) continue;  // (the host sees ntiles > tcap and fails the sort)
             const uint32_t a0 = chain[t], a1 = nxt[a0];
-            const uint32_t *pc = counts + (uint64_t)(b.c0 + c) * (SS + 1);
-            const uint32_t base = (uint32_t)b.start + c * lch;
-            pieces[(uint64_t)k * PS + c] = make_uint2(base + pc[a0], base + pc[a1]);
+            for (uint32_t c = lane; c < nch; c += 64) {
+                const uint32_t *pc = counts + (uint64_t)(b.c0 + c) * (SS + 1);
+                const uint32_t base = (uint32_t)b.start + c * lch;
+                pieces[(uint64_t)k * PS + c] = make_uint2(base + pc[a0], base + pc[a1]);
+            }
         }
     }
 }

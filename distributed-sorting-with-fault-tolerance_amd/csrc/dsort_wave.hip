@@ -1889,7 +1889,7 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
     // samples: int32 composites; int64 keys, sorted keys and composites (3 x 8 bytes)
     const size_t o_smp = take((size_t)S * (sizeof(T) == 8 ? 24 : sizeof(C))), o_spl = take((size_t)BP * sizeof(C)),
                  o_cnt = take((size_t)G * B * 4), o_part = take((size_t)nchunk * B * 8),
-                 o_offs = take((size_t)G * B * 8), o_bst = take((size_t)(B + 1) * 8),
+                 o_offs = take((size_t)G * B * 4), o_bst = take((size_t)(B + 1) * 8),
                  o_tt = take((size_t)tmax * sizeof(TileRef)), o_nt = take(4), o_map = take(sizeof(BkMap));
     int rc = ensure(ctx, &ctx->bucket, &ctx->bucket_bytes, off, "bucket partition");
     if (rc) return rc;
@@ -1898,7 +1898,7 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
     C *spl = reinterpret_cast<C *>(a + o_spl);
     uint32_t *cnt = reinterpret_cast<uint32_t *>(a + o_cnt);
     uint64_t *part = reinterpret_cast<uint64_t *>(a + o_part);
-    uint64_t *offs = reinterpret_cast<uint64_t *>(a + o_offs);
+    uint32_t *offs = reinterpret_cast<uint32_t *>(a + o_offs);  // (positions mod 2^32: the scatter's index width)
     uint64_t *bst = reinterpret_cast<uint64_t *>(a + o_bst);
     TileRef *tt = reinterpret_cast<TileRef *>(a + o_tt);
     uint32_t *ntl = reinterpret_cast<uint32_t *>(a + o_nt);
@@ -1965,7 +1965,7 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
     hipLaunchKernelGGL(bucket_colsum_kernel, dim3((unsigned)nchunk), dim3(BK_MAXB), 0, s, cnt, (uint32_t)G, B, part);
     hipLaunchKernelGGL(bucket_scan_kernel, dim3(1), dim3(BK_MAXB), 0, s, part, (uint32_t)nchunk, B,
                        sub_keys<T>(ctx) ? 0u : (uint32_t)TILE, (uint32_t)ALIGN, bst, tt, ntl);
-    hipLaunchKernelGGL(bucket_offsets_kernel<uint64_t>, dim3((unsigned)nchunk), dim3(BK_MAXB), 0, s, cnt, part, bst, (uint32_t)G, B, offs);
+    hipLaunchKernelGGL(bucket_offsets_kernel<uint32_t>, dim3((unsigned)nchunk), dim3(BK_MAXB), 0, s, cnt, part, bst, (uint32_t)G, B, offs);
     DSORT_HIP(ctx, hipGetLastError());
     // bucket starts to the host (the pass plan depends on the bucket sizes); the host waits for
     // them while the scatter runs.  The scatter always writes the scratch buffer (never the
