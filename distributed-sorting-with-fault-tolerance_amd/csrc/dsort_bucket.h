@@ -663,6 +663,10 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
     __shared__ T lk[SUB];                            // the sub-tile's new keys grouped by bucket
     __shared__ T carry[BK_MAXB * LK];                // per bucket: stream entries not yet written (< LK)
     static_assert(!SPL_LK || sizeof(lk) >= (BK_MAXB + 1) * sizeof(typename CT::C), "splitters staged in lk");
+    // carry entry e of bucket b at b LK + (e ^ ((b >> 1) & (LK - 1))): the owners' copy (lane b
+    // writes entry e2 of its bucket) and the line phase's reads hit distinct banks instead of the
+    // two (int32) that the LK-word row stride leaves them (scatter 2.72 -> 2.62 ms at 2^30 int32)
+    const auto cswz = [](uint32_t b, uint32_t e) { return e ^ ((b >> 1) & (uint32_t)(LK - 1)); };
     typename CT::C *spl = SPL_LK ? reinterpret_cast<typename CT::C *>(lk) : spl_own;
     const typename CT::C *spl_look = SPL_LK ? spl_g : spl;  // (global: only BP entries, searched within a slot)
     const int tb = threadIdx.x, lane = tb & 63, w = tb >> 6;
@@ -770,7 +774,7 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
                 const uint32_t e = e0 + t;
                 ok[t] = e >= cp && e < cL;
                 full = full && ok[t];
-                v[t] = e < cv ? carry[b * LK + e] : lk[lb + e - cv];
+                v[t] = e < cv ? carry[b * LK + cswz(b, e)] : lk[lb + e - cv];
             }
             const uint32_t gi = sgb[b] + e0;  // mod 2^32
             T *tgt = (sb.y >> 10) & 1 ? out2 : out;
@@ -791,7 +795,7 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
         // below vc of a stream that wrote no line are there already)
         if (owner) {
             const uint32_t nv = L - nl * LK;
-            for (uint32_t e2 = nl ? 0 : vc; e2 < nv; ++e2) carry[tb * LK + e2] = lk[lks + nl * LK + e2 - vc];
+            for (uint32_t e2 = nl ? 0 : vc; e2 < nv; ++e2) carry[tb * LK + cswz((uint32_t)tb, e2)] = lk[lks + nl * LK + e2 - vc];
             if (nl) ph = 0;
             gb += nl * LK;
             vc = nv;
