@@ -407,8 +407,19 @@ __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restric
         }
     };
     uint32_t tot = 0;
-    if (j < ns) {
+    if constexpr (LOCAL) {
+        // sub-bucket j's total = A_j - A_{j-1}, A_j = the sum over the chunks of pref[c][j + 1]
+        // (pref[c][0] = 0): one load per chunk instead of two
+        uint32_t a = 0;
+        if (j < ns) {
 #pragma unroll 8  // (independent loads in flight: the loop is latency-bound)
+            for (uint32_t c = b.c0; c < b.c1; ++c) a += counts[(uint64_t)c * (SS + 1) + j + 1];
+            ss[j + 1] = a;
+        }
+        __syncthreads();
+        if (j < ns) tot = a - (j ? ss[j] : 0u);
+    } else if (j < ns) {
+#pragma unroll 8
         for (uint32_t c = b.c0; c < b.c1; ++c) tot += cnt(c);
     }
     uint32_t all;
