@@ -48,7 +48,8 @@ struct BInfo {       // one first-level bucket (host-built)
     uint32_t nsub;   // sub-buckets, 1..SB_MAXS
     uint32_t ns;     // samples (0 when nsub == 1)
     uint32_t c0, c1; // chunks [c0, c1)
-    uint32_t pad;
+    uint32_t single; // sample single keys (the retry after the local partition: its chunks are
+                     // partitioned, so adjacent keys lie in one old sub-bucket)
 };
 
 struct Chunk {
@@ -146,7 +147,7 @@ __device__ __forceinline__ int sub_of(const Spl<T> *spl, const uint32_t *rng, T 
 // by (key, position).  A bucket whose ns is not a multiple of SB_RUN (DSORT_OPT_SUB_OVERSAMPLE
 // not a multiple of 4) samples single keys.
 constexpr uint32_t SB_RUN = 4;
-__host__ __device__ __forceinline__ uint32_t sample_run(const BInfo &b) { return b.ns % SB_RUN ? 1u : SB_RUN; }
+__host__ __device__ __forceinline__ uint32_t sample_run(const BInfo &b) { return b.single || b.ns % SB_RUN ? 1u : SB_RUN; }
 __host__ __device__ __forceinline__ uint64_t sample_run_pos(const BInfo &b, uint32_t run, uint64_t r) {
     const uint64_t nr = b.ns / run;
     const uint64_t p = ((2 * r + 1) * b.len) / (2 * nr);

@@ -1628,7 +1628,8 @@ static int side_stream(dsort_ctx *ctx) {
 
 template <typename T>
 static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_t *hb, int B, uint64_t m,
-                    hipStream_t s, bool timed, bool local, const uint8_t *pure, bool pure_done, const void *bspl) {
+                    hipStream_t s, bool timed, bool local, const uint8_t *pure, bool pure_done, const void *bspl,
+                    bool retry = false) {
     using namespace sb;
     constexpr int TILE = TILE_OF<T>;
     constexpr uint64_t ALIGN = KPC<T>;
@@ -1665,7 +1666,7 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
             tcap += 2 * len / ((uint64_t)TILE - 2 * (ALIGN - 1) * nc) + 1;
         }
         bi[b] = BInfo{hb[b], nsmp, (uint32_t)len, (uint32_t)ns, ns > 1 ? (uint32_t)(ns * os) : 0u, (uint32_t)nch,
-                      (uint32_t)(nch + nc), 0};
+                      (uint32_t)(nch + nc), retry ? 1u : 0u};
         nsmp += bi[b].ns;
         nch += nc;
         nsubs += ns;
@@ -1792,7 +1793,9 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         // more in empty workgroups than this wait -- measured 10.6 vs 10.1 ms)
         DSORT_HIP(ctx, hipEventSynchronize(ctx->sub_ev));
         const uint32_t ntiles = hn[0], novf = hn[1];
-        if (novf) return sub_sort<T>(ctx, src, d_keys, n, hb, B, m, s, timed, false, pure, pure_done, bspl);
+        // (the scatter path over the partitioned chunks: its sample takes single keys, since a run
+        // of adjacent keys now lies in one sub-bucket of this attempt)
+        if (novf) return sub_sort<T>(ctx, src, d_keys, n, hb, B, m, s, timed, false, pure, pure_done, bspl, true);
         if (ntiles > tmax || ntiles > tcap) return set_err(ctx, DSORT_EHIP, "sub-bucket packing overflow");
         fault_point(ctx, s, 1);  // second-level partition done
         ctx->stats.merge_passes = 0;

@@ -70,28 +70,38 @@ class Session:
     def __init__(self, workdir, workers=4, master="ours", worker_kinds=None, worker_args=None,
                  master_args=(), lib_dir=None, proto="v0", bin_dir=BIN, env=None):
         self.dir = str(workdir)
-        self.port = free_port()
         self.n = workers
         self.env = dict(os.environ if env is None else env)
         if lib_dir:
             self.env["LD_LIBRARY_PATH"] = lib_dir + ":" + self.env.get("LD_LIBRARY_PATH", "")
-        with open(os.path.join(self.dir, "server.conf"), "w") as f:
-            f.write(f"SERVER_PORT={self.port}\n")
-        with open(os.path.join(self.dir, "client.conf"), "w") as f:
-            f.write(f"SERVER_IP=127.0.0.1\nSERVER_PORT={self.port}\n")
-        self.mlog = open(os.path.join(self.dir, "master.log"), "w")
         if master == "ours":
             cmd = [os.path.join(bin_dir, "dsort_master"), "--workers", str(workers), "--proto", proto,
                    *master_args, "server.conf"]
         else:
             cmd = [os.path.join(REF_BUILD, "server"), "server.conf"]
-        self.master = subprocess.Popen(cmd, cwd=self.dir, stdin=subprocess.PIPE, stdout=self.mlog,
-                                       stderr=subprocess.STDOUT, env=self.env)
-        t0 = time.time()
-        while not listening(self.port):
-            if self.master.poll() is not None or time.time() - t0 > 30:
-                raise RuntimeError("master did not start: " + self.master_log())
-            time.sleep(0.02)
+        # free_port() can lose its port to another process before the master binds it (seen on a
+        # shared GPU box): a master that exits with "Address already in use" is restarted on a
+        # fresh port, up to 5 times
+        for attempt in range(5):
+            self.port = free_port()
+            with open(os.path.join(self.dir, "server.conf"), "w") as f:
+                f.write(f"SERVER_PORT={self.port}\n")
+            with open(os.path.join(self.dir, "client.conf"), "w") as f:
+                f.write(f"SERVER_IP=127.0.0.1\nSERVER_PORT={self.port}\n")
+            self.mlog = open(os.path.join(self.dir, "master.log"), "w")
+            self.master = subprocess.Popen(cmd, cwd=self.dir, stdin=subprocess.PIPE, stdout=self.mlog,
+                                           stderr=subprocess.STDOUT, env=self.env)
+            t0 = time.time()
+            while not listening(self.port):
+                if self.master.poll() is not None or time.time() - t0 > 30:
+                    break
+                time.sleep(0.02)
+            else:
+                break
+            log = self.master_log()
+            if self.master.poll() is None or "Address already in use" not in log or attempt == 4:
+                raise RuntimeError("master did not start: " + log)
+            self.mlog.close()
         kinds = worker_kinds or ["ours"] * workers
         wargs = worker_args or [[] for _ in range(workers)]
         self.workers = []
