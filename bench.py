@@ -68,7 +68,7 @@ def parse(argv=None):
     ap.add_argument("--kill-rank", type=int, default=None,
                     help="BASELINE config C5: fault-tolerance run (launch WITHOUT torchrun: the master "
                          "spawns one worker per GPU); this worker dies mid-sort")
-    ap.add_argument("--kill-after-stage", "--kill-after-pass", dest="kill_after_stage", type=int, default=0,
+    ap.add_argument("--kill-after-stage", dest="kill_after_stage", type=int, default=0,
                     help="the dying worker SIGKILLs itself after this stage of its local sort "
                          "(DSORT_OPT_KILL_AFTER_STAGE; >= 2^25 keys per worker: 0 first-level partition, "
                          "1 second-level partition, 2 tile sort); an unreachable stage is an error")

@@ -362,9 +362,13 @@ static void abort_comm_locked(dsort_ctx *ctx) {
 // Every wait of an exchange: polls the stream, RCCL's asynchronous error (non-blocking
 // communicator), the abort flag and the deadline, and aborts the communicator on a failure,
 // instead of a hipStreamSynchronize that a dead peer would block forever.
-static int exch_wait(dsort_ctx *ctx, hipStream_t s, bool with_stream, double deadline, const char *what) {
+// hold (DSORT_OPT_TEST_HOLD_EXCHANGE): the wait reports "not done" as if a peer never sent, until
+// the abort flag or the deadline ends it.
+static int exch_wait(dsort_ctx *ctx, hipStream_t s, bool with_stream, double deadline, const char *what,
+                     bool hold = false) {
     for (;;) {
-        const hipError_t q = with_stream ? hipStreamQuery(s) : hipSuccess;
+        const hipError_t q0 = with_stream ? hipStreamQuery(s) : hipSuccess;
+        const hipError_t q = hold && q0 == hipSuccess ? hipErrorNotReady : q0;
         ncclResult_t ae = ncclSuccess;
         if (ctx->comm) ncclCommGetAsyncError(ctx->comm, &ae);
         if (q == hipSuccess && ae != ncclInProgress && (ae == ncclSuccess || !ctx->comm)) return DSORT_OK;
@@ -611,7 +615,7 @@ static int sample_sort(dsort_ctx *ctx, const T *d_in, size_t n_local, T **d_out,
     rc = merge_device<T>(ctx, rb, rlen.data(), P, outp, s, true);
     if (rc) return rc;
     if (!host_tx) {  // the receives must have landed before the caller reads the slice
-        rc = exch_wait(ctx, s, true, deadline, "key all-to-all");
+        rc = exch_wait(ctx, s, true, deadline, "key all-to-all", ctx->opt.test_hold_exchange != 0);
         if (rc) return rc;
     }
     if (ctx->ev_ok) {
@@ -725,7 +729,7 @@ int dsort_set_option(dsort_ctx *ctx, int option, int64_t v) {
             if (v != -1 && (v < 1 || v > kMaxLogF)) return set_err(ctx, DSORT_EINVAL, "DSORT_OPT_MAX_FANIN_LOG2: -1 or 1..5");
             o.max_logf = v;
             return DSORT_OK;
-        case DSORT_OPT_KILL_AFTER_PASS:
+        case DSORT_OPT_KILL_AFTER_STAGE:
             if (v < -1) return set_err(ctx, DSORT_EINVAL, "DSORT_OPT_KILL_AFTER_STAGE: -1 or a stage index");
             o.kill_after_pass = v;
             return DSORT_OK;
@@ -749,6 +753,10 @@ int dsort_set_option(dsort_ctx *ctx, int option, int64_t v) {
             if (v < 0) return set_err(ctx, DSORT_EINVAL, "DSORT_OPT_COMM_TIMEOUT_MS: >= 0");
             o.comm_timeout_ms = v;
             return DSORT_OK;
+        case DSORT_OPT_TEST_HOLD_EXCHANGE:
+            if (v != 0 && v != 1) return set_err(ctx, DSORT_EINVAL, "DSORT_OPT_TEST_HOLD_EXCHANGE: 0 or 1");
+            o.test_hold_exchange = v;
+            return DSORT_OK;
         default:
             return set_err(ctx, DSORT_EINVAL, "unknown option " + std::to_string(option));
     }
@@ -762,9 +770,10 @@ int dsort_get_option(const dsort_ctx *ctx, int option, int64_t *v) {
         case DSORT_OPT_BUCKET_KEYS: *v = o.bucket_keys; return DSORT_OK;
         case DSORT_OPT_BUCKET_OVERSAMPLE: *v = o.bucket_os; return DSORT_OK;
         case DSORT_OPT_MAX_FANIN_LOG2: *v = o.max_logf; return DSORT_OK;
-        case DSORT_OPT_KILL_AFTER_PASS: *v = o.kill_after_pass; return DSORT_OK;
+        case DSORT_OPT_KILL_AFTER_STAGE: *v = o.kill_after_pass; return DSORT_OK;
         case DSORT_OPT_KILL_IN_EXCHANGE: *v = o.kill_in_exchange; return DSORT_OK;
         case DSORT_OPT_COMM_TIMEOUT_MS: *v = o.comm_timeout_ms; return DSORT_OK;
+        case DSORT_OPT_TEST_HOLD_EXCHANGE: *v = o.test_hold_exchange; return DSORT_OK;
         case DSORT_OPT_SUB_KEYS: *v = o.sub_keys; return DSORT_OK;
         case DSORT_OPT_SUB_OVERSAMPLE: *v = o.sub_os; return DSORT_OK;
         case DSORT_OPT_SUB_GATHER: *v = o.sub_gather; return DSORT_OK;

@@ -52,9 +52,10 @@ struct dsort_opts {
     int64_t bucket_keys = 1 << 20;  // DSORT_OPT_BUCKET_KEYS
     int64_t bucket_os = 256;        // DSORT_OPT_BUCKET_OVERSAMPLE
     int64_t max_logf = -1;          // DSORT_OPT_MAX_FANIN_LOG2: -1 = per key type default
-    int64_t kill_after_pass = -1;   // DSORT_OPT_KILL_AFTER_STAGE (= DSORT_OPT_KILL_AFTER_PASS)
+    int64_t kill_after_pass = -1;   // DSORT_OPT_KILL_AFTER_STAGE
     int64_t kill_in_exchange = -1;  // DSORT_OPT_KILL_IN_EXCHANGE
     int64_t comm_timeout_ms = 0;    // DSORT_OPT_COMM_TIMEOUT_MS
+    int64_t test_hold_exchange = 0; // DSORT_OPT_TEST_HOLD_EXCHANGE
     int64_t sub_keys = -1;          // DSORT_OPT_SUB_KEYS: -1 = TILE / 8, 0 = no second level
     int64_t sub_os = -1;            // DSORT_OPT_SUB_OVERSAMPLE: -1 = 4
     int64_t sub_gather = 1;         // DSORT_OPT_SUB_GATHER

@@ -338,9 +338,13 @@ __device__ __forceinline__ uint32_t scan_excl_1024(uint32_t v, uint32_t *wsum, u
 // sort loads 16-byte-aligned vectors from p - off(p)).  Tiles are greedy: a tile starting with
 // sub-bucket i takes i, i+1, .. while they fit.  A sub-bucket that alone exceeds its tile's room
 // becomes pieces: TILE - off(p) keys, then TILE-key pieces, merged afterwards (merge record).
+// LOCAL: such a sub-bucket is cut by chunks instead -- tiles [tile0, tile0 + nt) each gather the
+// sub-bucket's pieces of a run of consecutive chunks -- and those tiles' outputs are merged
+// afterwards (the host reads their sizes from the tile records).
 struct Ovf {
     uint64_t start;
     uint64_t len;
+    uint32_t tile0, nt;  // LOCAL: the tiles the sub-bucket was cut into
 };
 
 // A tile of the local-partition path: sub-buckets [j0, j1) of bucket b, `valid` keys, output
@@ -369,16 +373,45 @@ struct Gather {
 };
 
 // LOCAL: the chunk histograms are the prefix tables of sb_local_kernel (pref[c][j+1] -
-// pref[c][j]); tiles are GTiles and a tile has no alignment constraint (room = tile); an
-// oversized sub-bucket only counts in novf (the host then takes the scatter path).
+// pref[c][j]); tiles are GTiles and a tile has no alignment constraint (room = tile); a sub-bucket
+// above a tile is cut by chunks into several tiles (split_tiles) and recorded in ovf: the host
+// merges those tiles' outputs after the tile sort (rare: a sampling outlier).
 // SCATTER: counts[c][j]; the per-chunk offsets of the scatter are written too; tiles are
 // TileRefs.
 // LOCAL: a tile's room is tile - cpad * (the bucket's chunks): the gathering tile sort reads every
 // piece as the 16-byte vectors covering it, up to cpad extra slots per piece (gather_tile).
-// LOCAL also writes every tile's piece table (pieces, PS entries per tile, tiles below tcap; lch =
-// keys per chunk): the
-// gathering tile sort then reads it together with the tile record, one round trip before its key
-// loads instead of two (record, then the prefix tables).
+// LOCAL also writes every tile's piece table (pieces, PS entries per tile, tiles below tcap;
+// chunk c's keys start at ch[c].start): the gathering tile sort then reads it together with the
+// tile record, one round trip before its key loads instead of two (record, then the prefix
+// tables).  Tile records past trec (the record array's size) are not written: the host sees
+// *ntiles > trec and takes the scatter path.
+//
+// Split of sub-bucket j (LOCAL, above a tile): greedy over the bucket's chunks, a tile taking
+// consecutive chunks' pieces while its keys plus cpad per piece fit `full`.  Calls f(ca, cb, valid)
+// per tile in order; returns the tile count.  Any one chunk's piece fits (a chunk holds fewer keys
+// than a tile).
+template <typename F>
+__device__ __forceinline__ uint32_t split_tiles(const uint32_t *counts, int SS, uint32_t c0, uint32_t c1, int j,
+                                                uint32_t full, uint32_t cpad, F &&f) {
+    uint32_t nt = 0, ca = c0, v = 0;
+    for (uint32_t c = c0; c < c1; ++c) {
+        const uint32_t *pc = counts + (uint64_t)c * (SS + 1);
+        const uint32_t piece = pc[j + 1] - pc[j];
+        if (c > ca && v + piece + cpad * (c - ca + 1) > full) {
+            f(ca, c, v);
+            ++nt;
+            ca = c;
+            v = 0;
+        }
+        v += piece;
+    }
+    if (c1 > ca) {
+        f(ca, c1, v);
+        ++nt;
+    }
+    return nt;
+}
+
 template <bool LOCAL>
 __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restrict__ bi, int SS,
                                                           const uint32_t *__restrict__ counts,
@@ -386,7 +419,8 @@ __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restric
                                                           uint32_t mis, uint32_t cpad, void *__restrict__ tiles,
                                                           uint32_t *__restrict__ ntiles, Ovf *__restrict__ ovf,
                                                           uint32_t *__restrict__ novf, uint2 *__restrict__ pieces,
-                                                          uint32_t PS, uint32_t tcap, uint32_t lch) {
+                                                          uint32_t PS, uint32_t tcap, const Chunk *__restrict__ ch,
+                                                          uint32_t trec) {
     __shared__ uint32_t wsum[SB_MAXS / 64];
     __shared__ uint32_t ss[SB_MAXS + 1];   // sub-bucket starts (positions)
     __shared__ uint16_t nxt[SB_MAXS];      // first sub-bucket after the tile starting at i
@@ -471,20 +505,41 @@ __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restric
         const uint32_t p = ss[i0], len = ss[i1] - p;
         room = (uint32_t)tile - ((p + mis) & (uint32_t)(align - 1));
         over = len > (LOCAL ? (uint32_t)full : room);
-        nt = len == 0 ? 0 : over ? (LOCAL ? 0 : 1 + (len - room + tile - 1) / tile) : 1;
-        if (LOCAL && over) atomicAdd(novf, 1u);
+        if (LOCAL && over)  // (i1 == i0 + 1: a lone sub-bucket) cut by chunks
+            nt = split_tiles(counts, SS, b.c0, b.c1, (int)i0, (uint32_t)full, cpad, [](uint32_t, uint32_t, uint32_t) {});
+        else
+            nt = len == 0 ? 0 : over ? 1 + (len - room + tile - 1) / tile : 1;
     }
     uint32_t tall;
     const uint32_t tex = scan_excl_1024(nt, wsum, tall);
     if (j == 0) tbase = tall ? atomicAdd(ntiles, tall) : 0;
     __syncthreads();
-    if (LOCAL && j < nc) tix[j] = nt ? (uint16_t)tex : (uint16_t)0xFFFF;
+    if (LOCAL && j < nc) tix[j] = nt && !over ? (uint16_t)tex : (uint16_t)0xFFFF;
     if (j < nc && nt) {
         const uint32_t p = ss[i0], len = ss[i1] - p;
         uint32_t k = tbase + tex;
         if constexpr (LOCAL) {
-            static_cast<GTile *>(tiles)[k] = GTile{p, b.start, len, blockIdx.x, i0, i1, b.c0, b.c1 - b.c0, b.nsub,
-                                                   len > room ? 1u : 0u};
+            GTile *gt = static_cast<GTile *>(tiles);
+            if (!over) {
+                if (k < trec)
+                    gt[k] = GTile{p, b.start, len, blockIdx.x, i0, i1, b.c0, b.c1 - b.c0, b.nsub, len > room ? 1u : 0u};
+            } else {
+                // the split tiles and their piece tables (this thread alone: a rare path)
+                uint32_t q = p;
+                split_tiles(counts, SS, b.c0, b.c1, (int)i0, (uint32_t)full, cpad,
+                            [&](uint32_t ca, uint32_t cb, uint32_t v) {
+                                if (k < trec)
+                                    gt[k] = GTile{q, b.start, v, blockIdx.x, i0, i1, ca, cb - ca, b.nsub, 0u};
+                                for (uint32_t c = ca; c < cb && k < tcap; ++c) {
+                                    const uint32_t *pc = counts + (uint64_t)c * (SS + 1);
+                                    const uint32_t base = (uint32_t)ch[c].start;
+                                    pieces[(uint64_t)k * PS + (c - ca)] = make_uint2(base + pc[i0], base + pc[i1]);
+                                }
+                                q += v;
+                                ++k;
+                            });
+                ovf[atomicAdd(novf, 1u)] = Ovf{p, len, tbase + tex, nt};
+            }
         } else {
             bk::TileRef *tt = static_cast<bk::TileRef *>(tiles);
             if (!over) {
@@ -493,7 +548,7 @@ __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restric
                 tt[k++] = bk::TileRef{p, room, 0};
                 for (uint32_t q = room; q < len; q += (uint32_t)tile)
                     tt[k++] = bk::TileRef{(uint64_t)p + q, len - q < (uint32_t)tile ? len - q : (uint32_t)tile, 0};
-                ovf[atomicAdd(novf, 1u)] = Ovf{p, len};
+                ovf[atomicAdd(novf, 1u)] = Ovf{p, len, 0u, 0u};
             }
         }
     }
@@ -508,7 +563,7 @@ __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restric
             const uint32_t a0 = chain[t], a1 = nxt[a0];
             for (uint32_t c = lane; c < nch; c += 64) {
                 const uint32_t *pc = counts + (uint64_t)(b.c0 + c) * (SS + 1);
-                const uint32_t base = (uint32_t)b.start + c * lch;
+                const uint32_t base = (uint32_t)ch[b.c0 + c].start;
                 pieces[(uint64_t)k * PS + c] = make_uint2(base + pc[a0], base + pc[a1]);
             }
         }

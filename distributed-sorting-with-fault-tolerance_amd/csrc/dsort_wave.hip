@@ -1626,6 +1626,42 @@ static int side_stream(dsort_ctx *ctx) {
     return DSORT_OK;
 }
 
+// The local path's sub-buckets above a tile (sb_scan_kernel<true>: each cut by chunks into the
+// tiles [tile0, tile0 + nt), sorted by the tile sort into consecutive output ranges): every one's
+// runs merged by the k-way pass kernels into tmp, then copied back.  Sets merge_passes to the
+// deepest such merge and sub_split_subbuckets to their number.
+template <typename T>
+static int merge_split_subbuckets(dsort_ctx *ctx, const sb::Ovf *d_ovf, uint32_t novf, const sb::GTile *d_tiles,
+                                  T *d_keys, T *tmp, hipStream_t s) {
+    using namespace sb;
+    std::vector<Ovf> ov(novf);
+    DSORT_HIP(ctx, hipMemcpyAsync(ov.data(), d_ovf, novf * sizeof(Ovf), hipMemcpyDeviceToHost, s));
+    DSORT_HIP(ctx, hipStreamSynchronize(s));
+    int lv = 0;
+    for (const Ovf &o : ov) {
+        std::vector<GTile> gt(o.nt);
+        DSORT_HIP(ctx, hipMemcpyAsync(gt.data(), d_tiles + o.tile0, o.nt * sizeof(GTile), hipMemcpyDeviceToHost, s));
+        DSORT_HIP(ctx, hipStreamSynchronize(s));
+        std::vector<size_t> runs(o.nt);
+        uint64_t tot = 0;
+        for (uint32_t i = 0; i < o.nt; ++i) {
+            runs[i] = gt[i].valid;
+            tot += gt[i].valid;
+        }
+        if (tot != o.len || (o.nt && gt[0].base != o.start))
+            return set_err(ctx, DSORT_EHIP, "split sub-bucket: tile records do not cover it");
+        int rc = wave_merge<T>(ctx, d_keys + o.start, runs.data(), (int)runs.size(), tmp + o.start, s, true);
+        if (rc) return rc;
+        DSORT_HIP(ctx, hipMemcpyAsync(d_keys + o.start, tmp + o.start, o.len * sizeof(T), hipMemcpyDeviceToDevice, s));
+        int l = 0;
+        for (uint64_t r = runs.size(); r > 1; r = ceil_div(r, (uint64_t)1 << WG<T>::MAXLOGF)) ++l;
+        lv = l > lv ? l : lv;
+    }
+    ctx->stats.merge_passes = lv;
+    ctx->stats.sub_split_subbuckets = (int)novf;
+    return DSORT_OK;
+}
+
 template <typename T>
 static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_t *hb, int B, uint64_t m,
                     hipStream_t s, bool timed, bool local, const uint8_t *pure, bool pure_done, const void *bspl,
@@ -1633,9 +1669,11 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
     using namespace sb;
     constexpr int TILE = TILE_OF<T>;
     constexpr uint64_t ALIGN = KPC<T>;
+    const bool asked_local = local;
     for (int b = 0; b < B && local; ++b)
         if (!pure[b] && ceil_div(hb[b + 1] - hb[b], (uint64_t)SB_LCH<T>) > (uint64_t)kMaxPieces<T>) local = false;
     if (reinterpret_cast<uintptr_t>(src) % 16) local = false;  // (the gather reads aligned 16-byte vectors)
+    if (asked_local && !local) ctx->stats.sub_scatter_fallback = 1;
     const uint64_t CH = local ? SB_LCH<T> : SB_CH<T>;
     // samples per sub-bucket; a bucket's samples (<= SB_MAXS * 8) fit one int64 tile
     constexpr int kMaxOs = TILE_OF<int64_t> / SB_MAXS;
@@ -1663,7 +1701,9 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         const uint64_t nc = ceil_div(len, CH);
         if (local && len) {
             PS = nc > PS ? (uint32_t)nc : PS;
-            tcap += 2 * len / ((uint64_t)TILE - 2 * (ALIGN - 1) * nc) + 1;
+            // (+ 8: the split tiles of a rare sub-bucket above a tile; beyond the bound the sort
+            // takes the scatter path)
+            tcap += 2 * len / ((uint64_t)TILE - 2 * (ALIGN - 1) * nc) + 1 + 8;
         }
         bi[b] = BInfo{hb[b], nsmp, (uint32_t)len, (uint32_t)ns, ns > 1 ? (uint32_t)(ns * os) : 0u, (uint32_t)nch,
                       (uint32_t)(nch + nc), retry ? 1u : 0u};
@@ -1784,8 +1824,8 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
             if ((rc = stage_event(ctx, s, timed, 14))) return rc;
         }
         hipLaunchKernelGGL(sb_scan_kernel<true>, dim3((unsigned)B), dim3(SB_MAXS), 0, s, dbi, SS, cnt, nullptr, TILE, 1,
-                           0u, (uint32_t)(2 * (ALIGN - 1)), tt, num, nullptr, num + 1, pcs, PS, (uint32_t)tcap,
-                           (uint32_t)SB_LCH<T>);
+                           0u, (uint32_t)(2 * (ALIGN - 1)), tt, num, ovf, num + 1, pcs, PS, (uint32_t)tcap,
+                           static_cast<const Chunk *>(dch), (uint32_t)tmax);
         DSORT_HIP(ctx, hipGetLastError());
         DSORT_HIP(ctx, hipMemcpyAsync(hn, num, 8, hipMemcpyDeviceToHost, s));
         DSORT_HIP(ctx, hipEventRecord(ctx->sub_ev, s));
@@ -1793,10 +1833,13 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         // more in empty workgroups than this wait -- measured 10.6 vs 10.1 ms)
         DSORT_HIP(ctx, hipEventSynchronize(ctx->sub_ev));
         const uint32_t ntiles = hn[0], novf = hn[1];
-        // (the scatter path over the partitioned chunks: its sample takes single keys, since a run
-        // of adjacent keys now lies in one sub-bucket of this attempt)
-        if (novf) return sub_sort<T>(ctx, src, d_keys, n, hb, B, m, s, timed, false, pure, pure_done, bspl, true);
-        if (ntiles > tmax || ntiles > tcap) return set_err(ctx, DSORT_EHIP, "sub-bucket packing overflow");
+        // Beyond the tile tables (only when many sub-buckets were split): the scatter path over the
+        // partitioned chunks -- its sample takes single keys, since a run of adjacent keys now lies
+        // in one sub-bucket of this attempt.
+        if (ntiles > tmax || ntiles > tcap) {
+            ctx->stats.sub_scatter_fallback = 1;
+            return sub_sort<T>(ctx, src, d_keys, n, hb, B, m, s, timed, false, pure, pure_done, bspl, true);
+        }
         fault_point(ctx, s, 1);  // second-level partition done
         ctx->stats.merge_passes = 0;
         // 3. tile sort: gathered from the chunks into d_keys
@@ -1807,10 +1850,19 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         }
         if (timed && ctx->ev_ok) {
             DSORT_HIP(ctx, hipEventRecord(ctx->ev[1], s));
-            DSORT_HIP(ctx, hipEventRecord(ctx->ev[2], s));
-            ctx->ev_mask |= 6u;
+            ctx->ev_mask |= 2u;
         }
-        fault_point(ctx, s, 2);  // tile sort done
+        fault_point(ctx, s, 2);  // tile sort done (a split sub-bucket's merge follows)
+        // sub-buckets above a tile (a sampling outlier): their split tiles' outputs merged (src,
+        // read by the tile sort, is free scratch now)
+        if (novf) {
+            rc = merge_split_subbuckets<T>(ctx, ovf, novf, static_cast<const GTile *>(tt), d_keys, src, s);
+            if (rc) return rc;
+        }
+        if (timed && ctx->ev_ok) {
+            DSORT_HIP(ctx, hipEventRecord(ctx->ev[2], s));
+            ctx->ev_mask |= 4u;
+        }
         return DSORT_OK;
     }
     // 2. histograms, sub-bucket starts, tiles
@@ -1821,7 +1873,7 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         DSORT_HIP(ctx, hipGetLastError());
     }
     hipLaunchKernelGGL(sb_scan_kernel<false>, dim3((unsigned)B), dim3(SB_MAXS), 0, s, dbi, SS, cnt, offs, TILE,
-                       (int)ALIGN, mis, 0u, tt, num, ovf, num + 1, nullptr, 0u, 0u, 0u);
+                       (int)ALIGN, mis, 0u, tt, num, ovf, num + 1, nullptr, 0u, 0u, nullptr, (uint32_t)tmax);
     DSORT_HIP(ctx, hipGetLastError());
     DSORT_HIP(ctx, hipMemcpyAsync(hn, num, 8, hipMemcpyDeviceToHost, s));
     DSORT_HIP(ctx, hipEventRecord(ctx->sub_ev, s));
@@ -1865,6 +1917,7 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
             lv = l > lv ? l : lv;
         }
         ctx->stats.merge_passes = lv;
+        ctx->stats.sub_split_subbuckets = (int)novf;
     }
     if (timed && ctx->ev_ok) {
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[2], s));
@@ -2290,7 +2343,8 @@ static int wave_merge(dsort_ctx *ctx, const T *d_in, const size_t *lens, int k, 
         ctx->groups_ev_pending = true;
         PassDesc pd{n, 0, 1 << logf, ng, static_cast<const GroupK *>(ctx->groups)};
         T *dst = dsts[which];
-        rc = launch_pass_w<T, false>(ctx, src, dst, pd, logf, tiles, s, false);
+        // a top-level merge times its merge kernels (dsort_stats.merge_kernel_ms)
+        rc = launch_pass_w<T, false>(ctx, src, dst, pd, logf, tiles, s, !keep_stats);
         if (rc) return rc;
         rl.swap(next);
         src = dst;
@@ -2375,7 +2429,7 @@ int sort_device(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipStream_t 
     if (!rc) rc = order_end(ctx, s);
     if (rc || !top || ctx->opt.kill_after_pass < 0) return rc;
     // the kill stage was never reached: a fault-injection run that would silently not fail
-    return set_err(ctx, DSORT_EINVAL,
+    return set_err(ctx, DSORT_ESTAGE,
                    "DSORT_OPT_KILL_AFTER_STAGE = " + std::to_string(ctx->opt.kill_after_pass) + ": this sort of " +
                        std::to_string(n) + " keys has " + std::to_string(ctx->stages_done) +
                        " stages (kill points 0.." + std::to_string(ctx->stages_done - 1) + ")");

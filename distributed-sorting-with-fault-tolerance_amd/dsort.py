@@ -22,7 +22,7 @@ except Exception:  # pragma: no cover
     torch = None
 
 DSORT_OK = 0
-ERRORS = {-1: "EINVAL", -2: "ENOMEM", -3: "EHIP", -4: "ECOMM", -5: "ENODEV", -6: "ETIMEOUT"}
+ERRORS = {-1: "EINVAL", -2: "ENOMEM", -3: "EHIP", -4: "ECOMM", -5: "ENODEV", -6: "ETIMEOUT", -7: "ESTAGE"}
 
 # every symbol include/dsort.h declares (checked by tests/test_abi.py)
 EXPORTS = [
@@ -46,9 +46,9 @@ EXPORTS = [
 
 # dsort_set_option / dsort_get_option (include/dsort.h)
 OPTIONS = {"buckets": 1, "bucket_keys": 2, "bucket_oversample": 3,
-           "max_fanin_log2": 5, "kill_after_stage": 6, "kill_after_pass": 6, "kill_in_exchange": 7,
+           "max_fanin_log2": 5, "kill_after_stage": 6, "kill_in_exchange": 7,
            "comm_timeout_ms": 8,
-           "sub_keys": 9, "sub_oversample": 10, "sub_gather": 11}
+           "sub_keys": 9, "sub_oversample": 10, "sub_gather": 11, "test_hold_exchange": 12}
 
 
 class DsortError(RuntimeError):
@@ -65,7 +65,8 @@ class Stats(ctypes.Structure):
                 ("keys_sent", ctypes.c_size_t), ("tile_sort_kernel_ms", ctypes.c_double),
                 ("partition_ms", ctypes.c_double), ("tile_sort_keys", ctypes.c_size_t),
                 ("bucket_hist_ms", ctypes.c_double), ("bucket_scatter_ms", ctypes.c_double),
-                ("sub_partition_ms", ctypes.c_double)]
+                ("sub_partition_ms", ctypes.c_double), ("sub_split_subbuckets", ctypes.c_int),
+                ("sub_scatter_fallback", ctypes.c_int)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

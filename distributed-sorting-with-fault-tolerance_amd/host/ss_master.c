@@ -172,7 +172,7 @@ int samplesort_master(int argc, char **argv, const char *argv0) {
         } else if (!strcmp(a, "--worker")) o.worker = NEXT();
         else if (!strcmp(a, "--kill-rank")) o.kill_rank = atoi(NEXT());
         else if (!strcmp(a, "--kill-stage")) kill_stage_exchange = !strcmp(NEXT(), "exchange");
-        else if (!strcmp(a, "--kill-after-stage") || !strcmp(a, "--kill-after-pass")) o.kill_after_pass = atoi(NEXT());
+        else if (!strcmp(a, "--kill-after-stage")) o.kill_after_pass = atoi(NEXT());
         else if (!strcmp(a, "--kill-in-recovery")) o.kill_in_recovery = atoi(NEXT());
         else if (!strcmp(a, "--kill-exchange-stage")) o.kill_exchange_stage = atoi(NEXT());
         else if (!strcmp(a, "--reassign")) o.next_live = !strcmp(NEXT(), "next-live");

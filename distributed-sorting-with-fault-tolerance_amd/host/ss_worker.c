@@ -349,11 +349,11 @@ int samplesort_worker(const char *host, int port, int device, int verbose) {
         const double t_go = now_ms();
         /* the local sort: the worker's merge_sort (client.c:117); the fault injection of config C5
          * strikes inside it, after merge pass k */
-        CHECK(dsort_set_option(ctx, DSORT_OPT_KILL_AFTER_PASS, job.kill_after_pass));
+        CHECK(dsort_set_option(ctx, DSORT_OPT_KILL_AFTER_STAGE, job.kill_after_pass));
         if (i64) CHECK(dsort_sort_dev_copy_i64(ctx, (const int64_t *)d_chunk, (int64_t *)d_run, n0, NULL));
         else CHECK(dsort_sort_dev_copy_i32(ctx, (const int32_t *)d_chunk, (int32_t *)d_run, n0, NULL));
         CHECK(dsort_synchronize(ctx));
-        CHECK(dsort_set_option(ctx, DSORT_OPT_KILL_AFTER_PASS, -1));
+        CHECK(dsort_set_option(ctx, DSORT_OPT_KILL_AFTER_STAGE, -1));
         const double t_sorted = now_ms() - t_go;
         uint64_t run_len = n0;
         uint32_t owned[SS_MAX_CHUNKS];

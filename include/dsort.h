@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define DSORT_ABI_VERSION 3
+#define DSORT_ABI_VERSION 4
 
 #define DSORT_OK 0
 #define DSORT_EINVAL (-1)   /* bad argument */
@@ -43,6 +43,8 @@ extern "C" {
 #define DSORT_ECOMM (-4)    /* RCCL error or communicator not initialised */
 #define DSORT_ENODEV (-5)   /* no gfx950 device / device index out of range */
 #define DSORT_ETIMEOUT (-6) /* a peer did not answer in time (fault path) */
+#define DSORT_ESTAGE (-7)   /* ABI 4: DSORT_OPT_KILL_AFTER_STAGE names a stage this sort never
+                               reached (the sort itself finished: its output is valid)        */
 
 typedef struct dsort_ctx dsort_ctx;
 
@@ -74,6 +76,12 @@ typedef struct dsort_stats {
     double bucket_hist_ms;    /* first-level histogram                                      */
     double bucket_scatter_ms; /* first-level scatter                                        */
     double sub_partition_ms;  /* second-level partition (local partition, or hist + scatter) */
+    /* ABI 4: the second level's rare paths */
+    int sub_split_subbuckets; /* sub-buckets above a tile (a sampling outlier): tile-sorted in
+                                 pieces and merged (merge_passes counts that merge)            */
+    int sub_scatter_fallback; /* 1 when the sort left the default local partition for the
+                                 scatter path on its own (a bucket of too many chunks, or more
+                                 split tiles than the tile tables hold)                         */
 } dsort_stats;
 
 /* ---------------------------------------------------------------- lifecycle ---------- */
@@ -100,8 +108,11 @@ int dsort_synchronize(dsort_ctx *ctx);
                                          off (default).  Stages: bucketed sort (>= 2^25 keys) 0 first-
                                          level partition, 1 second-level partition, 2 tile sort; below
                                          2^25 keys 0 tile sort, 1 + p merge pass p (dsort_sort_stages).
-                                         A stage the sort never reaches makes it return DSORT_EINVAL */
-#define DSORT_OPT_KILL_AFTER_PASS DSORT_OPT_KILL_AFTER_STAGE /* ABI 2 name                        */
+                                         A stage the sort never reaches makes it return DSORT_ESTAGE
+                                         (ABI 3: DSORT_EINVAL) */
+/* ABI 2's DSORT_OPT_KILL_AFTER_PASS (option 6) counted merge passes; ABI 3 renumbered option 6 as
+ * stages (merge path: ABI 2's pass p is stage 1 + p; the bucketed path's stages did not exist),
+ * and ABI 4 retires the old name: callers must say DSORT_OPT_KILL_AFTER_STAGE. */
 #define DSORT_OPT_KILL_IN_EXCHANGE 7  /* fault injection: SIGKILL inside the sample-sort exchange, at
                                          stage 1 (samples all-gathered) or 2 (counts exchanged, keys
                                          about to move); -1 = off (default)                            */
@@ -115,6 +126,11 @@ int dsort_synchronize(dsort_ctx *ctx);
 #define DSORT_OPT_SUB_OVERSAMPLE 10   /* splitter samples per sub-bucket, 1..64; -1 = 4 (default)       */
 #define DSORT_OPT_SUB_GATHER 11       /* second level: 1 = chunks partitioned in place and gathered by
                                          the tile sort (default), 0 = keys scattered to sub-buckets  */
+#define DSORT_OPT_TEST_HOLD_EXCHANGE 12 /* test only: 1 = the sample sort's last exchange wait (keys
+                                         in flight) reports "not done" until the communicator is
+                                         aborted (dsort_comm_abort from another thread) or the deadline
+                                         passes -- the survivor's blocked wait of a peer failure, made
+                                         deterministic.  0 = off (default)                          */
 int dsort_set_option(dsort_ctx *ctx, int option, int64_t value);
 int dsort_get_option(const dsort_ctx *ctx, int option, int64_t *value);
 

@@ -94,14 +94,14 @@ static void *g_out = NULL;
 
 int dsort_set_option(dsort_ctx *ctx, int option, int64_t v) {
     (void)ctx;
-    if (option == DSORT_OPT_KILL_AFTER_PASS) g_kill_after_pass = (int)v;
+    if (option == DSORT_OPT_KILL_AFTER_STAGE) g_kill_after_pass = (int)v;
     else if (option == DSORT_OPT_KILL_IN_EXCHANGE) g_kill_in_exchange = (int)v;
-    else if (option < 1 || option > 8) return DSORT_EINVAL;
+    else if (option < 1 || option > 12) return DSORT_EINVAL;
     return DSORT_OK;
 }
 int dsort_get_option(const dsort_ctx *ctx, int option, int64_t *v) {
     (void)ctx;
-    *v = option == DSORT_OPT_KILL_AFTER_PASS ? g_kill_after_pass : option == DSORT_OPT_KILL_IN_EXCHANGE ? g_kill_in_exchange : 0;
+    *v = option == DSORT_OPT_KILL_AFTER_STAGE ? g_kill_after_pass : option == DSORT_OPT_KILL_IN_EXCHANGE ? g_kill_in_exchange : 0;
     return DSORT_OK;
 }
 int dsort_synchronize(dsort_ctx *ctx) { (void)ctx; return DSORT_OK; }
@@ -149,7 +149,7 @@ int dsort_sort_stages(const dsort_ctx *ctx, size_t n, int key_bytes, int *stages
     int dsort_sort_dev_copy_##SFX(dsort_ctx *ctx, const T *in, T *out, size_t n, void *s) {            \
         (void)ctx; (void)s;                                                                          \
         if (n && in != out) memmove(out, in, n * sizeof(T));                                        \
-        if (n < 2) return g_kill_after_pass >= 0 ? DSORT_EINVAL : DSORT_OK;                          \
+        if (n < 2) return g_kill_after_pass >= 0 ? DSORT_ESTAGE : DSORT_OK;                          \
         const size_t h = n / 2;                                                                      \
         if (oracle_merge_sort_##SFX(out, h)) return DSORT_ENOMEM;                                    \
         if (g_kill_after_pass == 0) raise(SIGKILL);                                                  \
@@ -163,7 +163,7 @@ int dsort_sort_stages(const dsort_ctx *ctx, size_t n, int key_bytes, int *stages
         memcpy(out, tmp, n * sizeof(T));                                                             \
         free(tmp);                                                                                   \
         if (g_kill_after_pass == 2) raise(SIGKILL);                                                  \
-        return g_kill_after_pass >= 0 ? DSORT_EINVAL : DSORT_OK;                                     \
+        return g_kill_after_pass >= 0 ? DSORT_ESTAGE : DSORT_OK;                                     \
     }                                                                                                \
     int dsort_merge_dev_##SFX(dsort_ctx *ctx, const T *in, const size_t lens[], int k, T *out, void *s) { \
         (void)ctx; (void)s;                                                                          \

@@ -3,7 +3,7 @@
   * the kill points of a local sort (DSORT_OPT_KILL_AFTER_STAGE, dsort.h): every stage of the
     bucketed path (>= 2^25 keys: first-level partition, second-level partition, tile sort) and of
     the merge path really SIGKILLs the process after that stage, and a stage the sort never reaches
-    is an error (DSORT_EINVAL), not a silent fault-free run -- the reference's fault moment is "any
+    is an error (DSORT_ESTAGE), not a silent fault-free run -- the reference's fault moment is "any
     time the socket fails" (server.c:358-395, 421-449);
   * the RCCL communicator's abort and rebuild (the survivor path of server.c:421-449 in the
     multi-GPU design): a non-blocking communicator is built, sorts, is aborted from a second thread
@@ -64,7 +64,7 @@ def test_kill_point_fires(n, w, stage):
 @pytest.mark.parametrize("n,w,stage", [(1 << 25, 4, 3), (1 << 20, 4, 3), (1, 4, 0)])
 def test_unreachable_kill_point_is_an_error(n, w, stage):
     p = _kill_child(n, w, stage)
-    assert p.returncode == 3 and "EINVAL" in p.stdout and "stages" in p.stdout, p.stdout + p.stderr
+    assert p.returncode == 3 and "ESTAGE" in p.stdout and "stages" in p.stdout, p.stdout + p.stderr
 
 
 def _sorted_slice_ok(ctx, ptr, nout, fp_in):
@@ -126,6 +126,73 @@ def test_rccl_abort_and_rebuild_one_rank(gpu_ctx):
     ctx.comm_destroy()
     del t
     torch.cuda.empty_cache()
+
+
+def test_rccl_abort_frees_a_survivor_blocked_in_the_exchange(gpu_ctx):
+    """The survivor side of server.c:421-449 in the multi-GPU design, deterministic: with
+    DSORT_OPT_TEST_HOLD_EXCHANGE the sample sort's wait for the key all-to-all reports "not done"
+    (as when a peer died before sending), so the call is parked inside exch_wait's poll loop.
+    dsort_comm_abort from another thread must free it: the call returns DSORT_ECOMM (never "ok"),
+    ncclCommAbort has run under the communicator lock, and a fresh communicator sorts again."""
+    import torch
+
+    import dsort
+    ctx = gpu_ctx
+    n = (1 << 25) + 333
+    t = torch.empty(n, dtype=torch.int32, device="cuda")
+    ctx.gen_uniform(t, SEED, 7)
+    fp_in = ctx.fingerprint(t)
+    ctx.comm_init(1, 0, dsort.Context.unique_id())
+    res = {}
+
+    def run():
+        try:
+            res["ok"] = ctx.sample_sort_dev(t)
+            ctx.synchronize()
+        except dsort.DsortError as e:
+            res["err"] = str(e)
+
+    with ctx.options(test_hold_exchange=1, comm_timeout_ms=60000):
+        th = threading.Thread(target=run)
+        th.start()
+        time.sleep(0.5)
+        assert th.is_alive(), res  # parked in the exchange, not finished
+        t0 = time.perf_counter()
+        ctx.comm_abort()
+        th.join(30)
+        freed_ms = 1e3 * (time.perf_counter() - t0)
+    assert not th.is_alive()
+    assert "err" in res and "ECOMM" in res["err"] and "dsort_comm_abort" in res["err"], res
+    assert freed_ms < 1000, freed_ms
+    with pytest.raises(dsort.DsortError, match="ECOMM"):  # the communicator is gone
+        ctx.sample_sort_dev(t)
+    ctx.comm_init(1, 0, dsort.Context.unique_id())
+    ptr, nout = ctx.sample_sort_dev(t)
+    ctx.synchronize()
+    assert nout == n and _sorted_slice_ok(ctx, ptr, nout, fp_in)
+    ctx.comm_destroy()
+    del t
+    torch.cuda.empty_cache()
+
+
+def test_held_exchange_times_out_at_the_deadline(gpu_ctx):
+    """The same parked wait with nobody aborting: DSORT_OPT_COMM_TIMEOUT_MS ends it with
+    DSORT_ETIMEOUT and aborts the communicator (a hung peer, not a dead one)."""
+    import torch
+
+    import dsort
+    ctx = gpu_ctx
+    t = torch.empty(1 << 20, dtype=torch.int32, device="cuda")
+    ctx.gen_uniform(t, SEED, 0)
+    ctx.comm_init(1, 0, dsort.Context.unique_id())
+    with ctx.options(test_hold_exchange=1, comm_timeout_ms=300):
+        t0 = time.perf_counter()
+        with pytest.raises(dsort.DsortError, match="ETIMEOUT"):
+            ctx.sample_sort_dev(t)
+        assert time.perf_counter() - t0 < 10
+    with pytest.raises(dsort.DsortError, match="ECOMM"):
+        ctx.sample_sort_dev(t)
+    ctx.comm_destroy()
 
 
 def test_c_master_rccl_one_gpu_with_comm_deadline():

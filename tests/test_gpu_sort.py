@@ -291,3 +291,26 @@ def test_back_to_back_sorts_on_two_streams(gpu_ctx):
     torch.cuda.synchronize()
     assert torch.equal(oa, torch.sort(a)[0])
     assert torch.equal(ob, torch.sort(b)[0])
+
+
+def test_c3_receive_merge_8_runs_bit_exact(gpu_ctx):
+    """Config C3's per-rank receive merge (dsort_api.hip sample_sort step 8: the gather + merge of
+    server.c:414-415 / 500-515): 8 sorted runs of 2^26 int32 keys inside one rank's key range
+    (1/8 of the int32 range, as uniform input gives every rank) merged by dsort_merge_dev_i32,
+    compared element for element with torch.sort."""
+    import torch
+    P, m = 8, 1 << 26
+    recv = torch.empty(P * m, dtype=torch.int32, device="cuda")
+    gpu_ctx.gen_uniform(recv, 0x5EED2026 ^ 0xC3, 0)
+    span = (1 << 32) // P
+    r64 = recv.to(torch.int64) & (span - 1)
+    recv.copy_((r64 - (1 << 31) + 3 * span).to(torch.int32))
+    del r64
+    for s in range(P):
+        gpu_ctx.sort_dev(recv[s * m:(s + 1) * m])
+    out = torch.empty_like(recv)
+    gpu_ctx.merge_dev(recv, [m] * P, out)
+    torch.cuda.synchronize()
+    assert torch.equal(out, torch.sort(recv).values)
+    del recv, out
+    torch.cuda.empty_cache()
