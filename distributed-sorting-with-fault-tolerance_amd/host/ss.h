@@ -62,6 +62,9 @@ typedef struct ss_job {
     uint32_t heartbeat_ms;
     int32_t kill_in_recovery;               /* fault injection: 1 = die on the first recovery PLAN
                                                (a second failure while the survivors rebuild)   */
+    int32_t hang_before_exchange;           /* fault injection: 1 = SIGSTOP itself after the local
+                                               sort (a hung, not dead, worker: only silence and
+                                               the peers' failed exchanges show it)            */
     char shm_name[64];
     char uid[128];                          /* RCCL unique id of this epoch                   */
 } ss_job;

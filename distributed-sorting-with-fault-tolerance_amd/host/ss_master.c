@@ -74,7 +74,7 @@ typedef struct mopt {
     int share;      /* all workers on GPU 0 */
     int devices[SS_MAX_WORKERS];
     const char *worker;
-    int kill_rank, kill_after_pass, kill_exchange_stage, kill_in_recovery;
+    int kill_rank, kill_after_pass, kill_exchange_stage, kill_in_recovery, hang_rank;
     int next_live;
     int hb_ms, timeout_ms;
     int64_t comm_timeout_ms;
@@ -85,6 +85,7 @@ typedef struct mopt {
 /* A DONE with an error status waits this long for a peer's death that would explain it (the
  * master sees a death within milliseconds: socket EOF, process exit) before the worker is fenced. */
 #define SS_FAIL_GRACE_MS 1000.0
+#define SS_SILENT_MIN_MS 500.0  /* a peer unheard for this long (or 20 heartbeats) counts as hung */
 
 static double now_ms(void) {
     struct timespec ts;
@@ -102,7 +103,7 @@ static void usage_ss(void) {
             "usage: dsort_master --mode samplesort --gpus N [--keys K] [--dtype i32|i64] [--dist uniform|zipf]\n"
             "       [--input FILE] [--transport rccl|relay] [--devices 0,1,..|share] [--worker PATH]\n"
             "       [--kill-rank R [--kill-stage sort|exchange] [--kill-after-stage K] [--kill-exchange-stage 1|2]]\n"
-            "       [--kill-in-recovery R2]\n"
+            "       [--kill-in-recovery R2] [--hang-rank R3]\n"
             "       [--reassign first-live|next-live] [--heartbeat-ms MS] [--timeout-ms MS]\n"
             "       [--comm-timeout-ms MS] [--seed S] [--output FILE]\n");
     exit(2);
@@ -141,6 +142,7 @@ int samplesort_master(int argc, char **argv, const char *argv0) {
     o.kill_after_pass = -1;
     o.kill_exchange_stage = -1;
     o.kill_in_recovery = -1;
+    o.hang_rank = -1;
     o.hb_ms = 50;
     o.timeout_ms = 5000;
     o.seed = 0x5EED2026ull;
@@ -174,6 +176,7 @@ int samplesort_master(int argc, char **argv, const char *argv0) {
         else if (!strcmp(a, "--kill-stage")) kill_stage_exchange = !strcmp(NEXT(), "exchange");
         else if (!strcmp(a, "--kill-after-stage")) o.kill_after_pass = atoi(NEXT());
         else if (!strcmp(a, "--kill-in-recovery")) o.kill_in_recovery = atoi(NEXT());
+        else if (!strcmp(a, "--hang-rank")) o.hang_rank = atoi(NEXT());
         else if (!strcmp(a, "--kill-exchange-stage")) o.kill_exchange_stage = atoi(NEXT());
         else if (!strcmp(a, "--reassign")) o.next_live = !strcmp(NEXT(), "next-live");
         else if (!strcmp(a, "--heartbeat-ms")) o.hb_ms = atoi(NEXT());
@@ -195,6 +198,7 @@ int samplesort_master(int argc, char **argv, const char *argv0) {
         if (kill_stage_exchange) o.kill_after_pass = -1;
         else o.kill_exchange_stage = -1;
     }
+    if (o.hang_rank >= o.n) usage_ss();
     if (o.kill_rank >= o.n || o.kill_in_recovery >= o.n || (o.kill_in_recovery >= 0 && o.kill_in_recovery == o.kill_rank)) {
         fprintf(stderr, "master: --kill-rank / --kill-in-recovery must name two different workers of %d\n", o.n);
         return 2;
@@ -361,6 +365,7 @@ int samplesort_master(int argc, char **argv, const char *argv0) {
             j.kill_after_pass = r == o.kill_rank ? o.kill_after_pass : -1;
             j.kill_in_exchange = r == o.kill_rank ? o.kill_exchange_stage : -1;
             j.kill_in_recovery = r == o.kill_in_recovery ? 1 : 0;
+            j.hang_before_exchange = r == o.hang_rank ? 1 : 0;
             j.comm_timeout_ms = o.comm_timeout_ms;
             j.heartbeat_ms = (uint32_t)o.hb_ms;
             snprintf(j.shm_name, sizeof j.shm_name, "%s", shm_name);
@@ -449,14 +454,37 @@ int samplesort_master(int argc, char **argv, const char *argv0) {
                     kill(W[r].pid, SIGKILL);
                     W[r].alive = 0;
                     newly = 1;
-                } else if (W[r].fail_at > 0 && now - W[r].fail_at > SS_FAIL_GRACE_MS) {
-                    /* its exchange failed (DSORT_ECOMM / DSORT_ETIMEOUT) and no peer died that
-                     * would explain it: fence the worker (kill) and reassign its chunks */
-                    fprintf(stderr, "master: worker %d reported status %d for epoch %u; fenced\n", r + 1,
-                            W[r].dn.status, epoch);
-                    kill(W[r].pid, SIGKILL);
-                    W[r].alive = 0;
-                    newly = 1;
+                }
+            }
+            /* A failed exchange (DONE with DSORT_ECOMM / DSORT_ETIMEOUT) that no peer's death has
+             * explained within the grace period.  A hung peer (stopped, or stuck so that even its
+             * heartbeat thread is silent) makes every survivor's exchange time out: fence the
+             * peers that have been silent for `silent` first and keep the reporters (they get the
+             * next epoch's plan).  Only when every peer is heard from is the reporter itself the
+             * suspect: fence it. */
+            if (go_sent) {
+                int due = 0;
+                for (int r = 0; r < o.n; ++r)
+                    if (W[r].alive && W[r].fail_at > 0 && now - W[r].fail_at > SS_FAIL_GRACE_MS) due = 1;
+                if (due) {
+                    const double silent = 20.0 * o.hb_ms > SS_SILENT_MIN_MS ? 20.0 * o.hb_ms : SS_SILENT_MIN_MS;
+                    int fenced_silent = 0;
+                    for (int r = 0; r < o.n; ++r)
+                        if (W[r].alive && W[r].fail_at <= 0 && now - W[r].last_seen > silent) {
+                            fprintf(stderr, "master: worker %d silent for %.0f ms while peers' exchanges failed; "
+                                            "fenced\n", r + 1, now - W[r].last_seen);
+                            kill(W[r].pid, SIGKILL);
+                            W[r].alive = 0;
+                            newly = fenced_silent = 1;
+                        }
+                    for (int r = 0; r < o.n && !fenced_silent; ++r)
+                        if (W[r].alive && W[r].fail_at > 0 && now - W[r].fail_at > SS_FAIL_GRACE_MS) {
+                            fprintf(stderr, "master: worker %d reported status %d for epoch %u; fenced\n", r + 1,
+                                    W[r].dn.status, epoch);
+                            kill(W[r].pid, SIGKILL);
+                            W[r].alive = 0;
+                            newly = 1;
+                        }
                 }
             }
             if (newly) {

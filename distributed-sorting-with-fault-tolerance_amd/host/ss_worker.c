@@ -48,6 +48,7 @@ typedef struct wk {
     char *resp;
     size_t resp_len;
     uint32_t hb_ms;
+    int64_t comm_timeout_ms; /* deadline of one relay exchange (the RCCL path's exchange deadline) */
 } wk;
 
 static double now_ms(void) {
@@ -136,9 +137,11 @@ static void *heartbeat_main(void *arg) {
         /* a PLAN for a newer epoch while the communicator of this one is being built: the
          * reader's abort may have come before dsort_comm_init took the communicator lock and been
          * lost; repeat it until the set-up returns (an init waiting for a dead peer never would) */
-        const int stuck = w->initing && w->plan_pending && w->plan.epoch > w->epoch;
+        /* (under w->mu, like the reader's abort: a late abort outside the lock could land after
+         * the main thread moved on to the newer epoch and cancel that epoch's set-up; the call
+         * only try-locks the communicator, so it never blocks here) */
+        if (w->initing && w->plan_pending && w->plan.epoch > w->epoch) dsort_comm_abort(w->ctx);
         pthread_mutex_unlock(&w->mu);
-        if (stuck) dsort_comm_abort(w->ctx);
         if (done || send_frame(w, SS_HB, NULL, 0)) return NULL;
     }
 }
@@ -158,7 +161,19 @@ static int relay(wk *w, uint16_t type, const void *a, size_t na, const void *b, 
     pthread_mutex_unlock(&w->mu);
     if (send_frame2(w, type, tag, a, na, b, nb)) return -1;
     pthread_mutex_lock(&w->mu);
-    while (!(w->resp_ready && w->resp_tag == tag) && !superseded(w)) pthread_cond_wait(&w->cv, &w->mu);
+    /* a deadline like the RCCL exchange's (DSORT_OPT_COMM_TIMEOUT_MS): a hung peer never posts its
+     * part, and the master answers only when every live rank has */
+    struct timespec dl;
+    clock_gettime(CLOCK_REALTIME, &dl);
+    dl.tv_sec += (time_t)(w->comm_timeout_ms / 1000);
+    dl.tv_nsec += (long)(w->comm_timeout_ms % 1000) * 1000000L;
+    dl.tv_sec += dl.tv_nsec / 1000000000L;
+    dl.tv_nsec %= 1000000000L;
+    int timed_out = 0;
+    while (!(w->resp_ready && w->resp_tag == tag) && !superseded(w) && !timed_out) {
+        if (w->comm_timeout_ms > 0) timed_out = pthread_cond_timedwait(&w->cv, &w->mu, &dl) == ETIMEDOUT;
+        else pthread_cond_wait(&w->cv, &w->mu);
+    }
     const int ok = w->resp_ready && w->resp_tag == tag;
     if (ok) {
         *resp = w->resp;
@@ -299,6 +314,7 @@ int samplesort_worker(const char *host, int port, int device, int verbose) {
     }
     const double t_setup0 = now_ms();
     w.hb_ms = job.heartbeat_ms ? job.heartbeat_ms : 50;
+    w.comm_timeout_ms = job.comm_timeout_ms;
     const size_t kb = job.key_bytes;
     const int i64 = kb == 8;
     /* the master's chunk replicas: shared memory, pinned here for DMA */
@@ -355,6 +371,7 @@ int samplesort_worker(const char *host, int port, int device, int verbose) {
         CHECK(dsort_synchronize(ctx));
         CHECK(dsort_set_option(ctx, DSORT_OPT_KILL_AFTER_STAGE, -1));
         const double t_sorted = now_ms() - t_go;
+        if (job.hang_before_exchange) raise(SIGSTOP); /* fault injection: hung, not dead */
         uint64_t run_len = n0;
         uint32_t owned[SS_MAX_CHUNKS];
         uint32_t nowned = 1;

@@ -126,3 +126,19 @@ def test_input_file_kat(libdir, tmp_path):
 def test_all_workers_dead_fails_cleanly(libdir, tmp_path):
     r, p = run_master(libdir, tmp_path, "--gpus", "1", "--keys", "1000", "--kill-rank", "0")
     assert not r["ok"] and p.returncode != 0
+
+
+def test_hung_worker_is_fenced_not_its_peers(libdir, tmp_path, oracle):
+    """A worker that hangs (SIGSTOP after its local sort: its heartbeat stops, its socket stays
+    open) with an exchange deadline and a long heartbeat timeout: every peer's exchange times out
+    and reports a failed DONE.  The master must fence the silent worker, not the peers that
+    reported (the 1 s fencing of failed reporters used to kill every survivor), then
+    finish over the survivors."""
+    n = 30_011
+    out = tmp_path / "out.txt"
+    r, p = run_master(libdir, tmp_path, "--gpus", "3", "--keys", str(n), "--hang-rank", "1",
+                      "--comm-timeout-ms", "1500", "--timeout-ms", "60000", "--output", str(out), timeout=90)
+    assert r["ok"], p.stdout + p.stderr
+    assert r["dead"] == [1] and r["survivors"] == 2 and r["epochs"] == 2, r
+    assert "silent" in p.stderr and "fenced" in p.stderr
+    assert out.read_bytes() == b"".join(b"%d\n" % int(k) for k in expected(oracle, n))
