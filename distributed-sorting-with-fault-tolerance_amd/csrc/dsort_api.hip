@@ -406,6 +406,164 @@ static void exchange_fault_point(dsort_ctx *ctx, int stage) {
     if (ctx->opt.kill_in_exchange == stage) raise(SIGKILL);
 }
 
+// All-gather of `count` uint64 per rank (RCCL through the context's small device buffer, or the
+// host transport): out[r * count + i] = rank r's src[i].
+static int allgather_u64(dsort_ctx *ctx, const uint64_t *src, size_t count, uint64_t *out, hipStream_t s,
+                         double deadline, const char *what) {
+    const int P = ctx->nranks;
+    if (ctx->has_transport) {
+        if (ctx->transport.allgather(ctx->transport.user, src, out, count * 8))
+            return set_err(ctx, DSORT_ECOMM, std::string("host transport allgather (") + what + ") failed");
+        return DSORT_OK;
+    }
+    const size_t bytes = count * 8 * (size_t)(P + 1);
+    int rc = ensure(ctx, &ctx->small, &ctx->small_bytes, bytes, "sample-sort small buffers");
+    if (rc) return rc;
+    if (ctx->small_host_bytes < bytes) {
+        if (ctx->small_host) (void)hipHostFree(ctx->small_host);
+        ctx->small_host = nullptr;
+        ctx->small_host_bytes = 0;
+        DSORT_HIP(ctx, hipHostMalloc(&ctx->small_host, bytes, hipHostMallocDefault));
+        ctx->small_host_bytes = bytes;
+    }
+    uint64_t *d = static_cast<uint64_t *>(ctx->small), *h = static_cast<uint64_t *>(ctx->small_host);
+    memcpy(h, src, count * 8);
+    DSORT_HIP(ctx, hipMemcpyAsync(d, h, count * 8, hipMemcpyHostToDevice, s));
+    DSORT_NCCLNB(ctx, ncclAllGather(d, d + count, count, ncclUint64, ctx->comm, s));
+    rc = exch_wait(ctx, s, false, deadline, what);
+    if (rc) return rc;
+    DSORT_HIP(ctx, hipMemcpyAsync(h + count, d + count, count * 8 * (size_t)P, hipMemcpyDeviceToHost, s));
+    rc = exch_wait(ctx, s, true, deadline, what);
+    if (rc) return rc;
+    memcpy(out, h + count, count * 8 * (size_t)P);
+    return DSORT_OK;
+}
+
+// The bucket exchange (dsort_internal.h): samples of the unsorted keys from every
+// rank -> the same Btot global splitters everywhere -> this rank's keys partitioned into the Btot
+// buckets (the first level of the one-GPU sort) -> buckets [q Bl, (q+1) Bl) to rank q (RCCL
+// grouped send/recv over xGMI) -> the received pieces of this rank's Bl buckets finished by the
+// second level and the tile sort.  Replaces the gather + merge_chunks of server.c:414-415 and
+// 500-515: nothing is merged.
+template <typename T>
+static int sample_sort_bx(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, T **d_out, size_t *n_out, hipStream_t s,
+                          double deadline) {
+    const int P = pl.P, me = pl.me, Bl = pl.Bl, Bt = pl.Btot;
+    const bool host_tx = ctx->has_transport;
+    const size_t rec = (size_t)pl.s_max * sizeof(BxSample);
+    int rc = ensure(ctx, &ctx->bxs, &ctx->bxs_bytes, rec * (size_t)(P + 1), "bucket-exchange samples");
+    if (rc) return rc;
+    BxSample *mine = static_cast<BxSample *>(ctx->bxs), *all = mine + pl.s_max;
+    // 1. samples, all-gathered
+    if ((rc = bx_sample<T>(ctx, d_in, pl, mine, s))) return rc;
+    if (!host_tx) {
+        DSORT_NCCLNB(ctx, ncclAllGather(mine, all, (size_t)pl.s_max * 2, ncclInt64, ctx->comm, s));
+        rc = exch_wait(ctx, s, false, deadline, "sample all-gather (enqueue)");
+        if (rc) return rc;
+    } else {
+        rc = ensure_host(ctx, &ctx->xfer, &ctx->xfer_bytes, rec * (size_t)(P + 1));
+        if (rc) return rc;
+        char *hm = static_cast<char *>(ctx->xfer), *ha = hm + rec;
+        DSORT_HIP(ctx, hipMemcpyAsync(hm, mine, rec, hipMemcpyDeviceToHost, s));
+        rc = exch_wait(ctx, s, true, deadline, "samples");
+        if (rc) return rc;
+        if (ctx->transport.allgather(ctx->transport.user, hm, ha, rec))
+            return set_err(ctx, DSORT_ECOMM, "host transport allgather (samples) failed");
+        DSORT_HIP(ctx, hipMemcpyAsync(all, ha, rec * (size_t)P, hipMemcpyHostToDevice, s));
+    }
+    exchange_fault_point(ctx, 1);
+    // 2. global splitters and this rank's first partition level (the host waits for the bucket
+    //    starts while the scatter runs); kill stage 0
+    const uint64_t *hb;
+    T *part;
+    rc = bx_partition<T>(ctx, d_in, pl, all, s, true, &hb, &part);
+    if (rc) return rc;
+    // 3. every rank's bucket starts
+    std::vector<uint64_t> hb_all((size_t)P * (Bt + 1));
+    {
+        const std::vector<uint64_t> mine_hb(hb, hb + Bt + 1);
+        rc = allgather_u64(ctx, mine_hb.data(), (size_t)Bt + 1, hb_all.data(), s, deadline, "bucket starts all-gather");
+        if (rc) return rc;
+    }
+    std::vector<size_t> scnt(P), sdsp(P), rlen(P);
+    std::vector<uint64_t> roff(P + 1, 0);
+    uint64_t sent = 0;
+    for (int q = 0; q < P; ++q) {
+        sdsp[q] = hb_all[(size_t)me * (Bt + 1) + (size_t)q * Bl];
+        scnt[q] = hb_all[(size_t)me * (Bt + 1) + (size_t)(q + 1) * Bl] - sdsp[q];
+        if (q != me) sent += scnt[q];
+        const uint64_t *h = hb_all.data() + (size_t)q * (Bt + 1);
+        rlen[q] = h[(size_t)(me + 1) * Bl] - h[(size_t)me * Bl];
+        roff[q + 1] = roff[q] + rlen[q];
+    }
+    const uint64_t nrecv = roff[P];
+    rc = ensure(ctx, &ctx->recv, &ctx->recv_bytes, (nrecv ? nrecv : 1) * sizeof(T) + 16, "receive buffer");
+    if (rc) return rc;
+    rc = ensure(ctx, &ctx->recv2, &ctx->recv2_bytes, (nrecv ? nrecv : 1) * sizeof(T), "sorted slice");
+    if (rc) return rc;
+    T *rb = static_cast<T *>(ctx->recv);
+    exchange_fault_point(ctx, 2);
+    // 4. the buckets to their ranks: one send and one receive per peer (all-to-all-v over xGMI)
+    if (ctx->ev_ok) {
+        DSORT_HIP(ctx, hipEventRecord(ctx->ev[5], s));
+        ctx->ev_mask |= 32u;
+    }
+    if (!host_tx) {
+        DSORT_NCCLNB(ctx, ncclGroupStart());
+        for (int q = 0; q < P; ++q) {
+            if (q == me) continue;
+            if (scnt[q]) DSORT_NCCLNB(ctx, ncclSend(part + sdsp[q], scnt[q], nccl_type<T>(), q, ctx->comm, s));
+            if (rlen[q]) DSORT_NCCLNB(ctx, ncclRecv(rb + roff[q], rlen[q], nccl_type<T>(), q, ctx->comm, s));
+        }
+        DSORT_NCCLNB(ctx, ncclGroupEnd());
+        rc = exch_wait(ctx, s, false, deadline, "key all-to-all (enqueue)");
+        if (rc) return rc;
+        if (scnt[me])
+            DSORT_HIP(ctx, hipMemcpyAsync(rb + roff[me], part + sdsp[me], scnt[me] * sizeof(T), hipMemcpyDeviceToDevice, s));
+    } else {
+        rc = ensure_host(ctx, &ctx->xfer, &ctx->xfer_bytes, (pl.n_local ? pl.n_local : 1) * sizeof(T));
+        if (rc) return rc;
+        rc = ensure_host(ctx, &ctx->xfer2, &ctx->xfer2_bytes, (nrecv ? nrecv : 1) * sizeof(T));
+        if (rc) return rc;
+        if (pl.n_local)
+            DSORT_HIP(ctx, hipMemcpyAsync(ctx->xfer, part, pl.n_local * sizeof(T), hipMemcpyDeviceToHost, s));
+        rc = exch_wait(ctx, s, true, deadline, "key staging");
+        if (rc) return rc;
+        std::vector<size_t> sc(P), sd(P), rcn(P), rd(P);
+        for (int q = 0; q < P; ++q) {
+            sc[q] = scnt[q] * sizeof(T);
+            sd[q] = sdsp[q] * sizeof(T);
+            rcn[q] = rlen[q] * sizeof(T);
+            rd[q] = roff[q] * sizeof(T);
+        }
+        if (ctx->transport.alltoallv(ctx->transport.user, ctx->xfer, sc.data(), sd.data(), ctx->xfer2, rcn.data(),
+                                     rd.data()))
+            return set_err(ctx, DSORT_ECOMM, "host transport alltoallv (keys) failed");
+        if (nrecv) DSORT_HIP(ctx, hipMemcpyAsync(rb, ctx->xfer2, nrecv * sizeof(T), hipMemcpyHostToDevice, s));
+    }
+    if (ctx->ev_ok) {
+        DSORT_HIP(ctx, hipEventRecord(ctx->ev[6], s));
+        DSORT_HIP(ctx, hipEventRecord(ctx->ev[3], s));
+        ctx->ev_mask |= 64u | 8u;
+    }
+    // the receives must have landed before the second level: its host waits (the tile count) would
+    // block on a stream a dead peer never completes -- this wait polls the abort flag and deadline
+    rc = exch_wait(ctx, s, true, deadline, "key all-to-all", ctx->opt.test_hold_exchange != 0);
+    if (rc) return rc;
+    // 5. the second level and the tile sort of this rank's buckets; kill stages 1 and 2
+    T *outp = static_cast<T *>(ctx->recv2);
+    rc = bx_local_sort<T>(ctx, rb, outp, pl, hb_all.data(), roff.data(), s, true);
+    if (rc) return rc;
+    ctx->last_stream = s;
+    ctx->stats.keys_in = pl.n_local;
+    ctx->stats.keys_out = nrecv;
+    ctx->stats.keys_sent = sent;
+    ctx->stats.exchange_path = 1;
+    *d_out = outp;
+    *n_out = nrecv;
+    return DSORT_OK;
+}
+
 template <typename T>
 static int sample_sort(dsort_ctx *ctx, const T *d_in, size_t n_local, T **d_out, size_t *n_out,
                        void *stream, bool presorted) {
@@ -422,6 +580,19 @@ static int sample_sort(dsort_ctx *ctx, const T *d_in, size_t n_local, T **d_out,
     const int P = ctx->nranks, me = ctx->rank, S = kSamplesPerRank;
     const bool host_tx = ctx->has_transport;
     int rc;
+    if (!presorted) {
+        // every rank's key count decides the path, the same on every rank: the bucket exchange, or
+        // (small inputs, partition switched off) sort locally and merge the received runs
+        std::vector<uint64_t> n_of(P);
+        const uint64_t nl = n_local;
+        rc = allgather_u64(ctx, &nl, 1, n_of.data(), s, deadline, "key count all-gather");
+        if (rc) return rc;
+        BxPlan pl;
+        if (bx_make_plan(ctx->opt, P, me, n_of.data(), (int)sizeof(T), pl)) {
+            ctx->stats = dsort_stats{};
+            return sample_sort_bx<T>(ctx, d_in, pl, d_out, n_out, s, deadline);
+        }
+    }
     const T *d_keys;
     dsort_stats st{};
     if (presorted) {
@@ -625,6 +796,7 @@ static int sample_sort(dsort_ctx *ctx, const T *d_in, size_t n_local, T **d_out,
     ctx->last_stream = s;
     st.keys_out = nrecv;
     st.keys_sent = sent;
+    st.exchange_path = 2;
     ctx->stats = st;
     *d_out = outp;
     *n_out = nrecv;

@@ -424,12 +424,14 @@ __host__ __forceinline__ int bucket_wg_subs(uint64_t n) {
 }
 
 // counts[g * B + b] = keys of workgroup g's subs sub-tiles in bucket b.  (The same slot table as
-// the scatter's: the one-key slots must agree.)
+// the scatter's: the one-key slots must agree.)  ioff: the composite index of in[0] (the multi-GPU
+// path: this rank's first key in the global order; 0 on one GPU).
 template <typename T>
 __global__ void __launch_bounds__(BK_T, 2) bucket_hist_kernel(const T *__restrict__ in, uint64_t n,
                                                               const typename Comp<T>::C *__restrict__ spl_g,
                                                               const BkMap *__restrict__ map, int B, int BP,
-                                                              int subs, uint32_t *__restrict__ counts) {
+                                                              int subs, uint32_t *__restrict__ counts,
+                                                              uint64_t ioff) {
     using CT = Comp<T>;
     constexpr int KPT = Geo<T>::KPT, SUB = BK_T * KPT;
     __shared__ typename CT::C spl[BK_MAXB + 1];
@@ -469,14 +471,14 @@ __global__ void __launch_bounds__(BK_T, 2) bucket_hist_kernel(const T *__restric
             for (int k = 0; k < KPT; ++k) {
                 const uint64_t i = b0 + (uint64_t)k * BK_T;
                 const uint32_t sl = slot_mode<T, BK_SLOTB, 0>(m, key[k]);
-                if (i < n) atomicAdd(&hist[bucket_fast<T, false>(spl, rng, sl, key[k], CT::make(key[k], i))], 1u);
+                if (i < n) atomicAdd(&hist[bucket_fast<T, false>(spl, rng, sl, key[k], CT::make(key[k], i + ioff))], 1u);
             }
         } else {
 #pragma unroll
             for (int k = 0; k < KPT; ++k) {
                 const uint64_t i = b0 + (uint64_t)k * BK_T;
                 const uint32_t sl = slot_mode<T, BK_SLOTB, 1>(m, key[k]);
-                if (i < n) atomicAdd(&hist[bucket_fast<T, false>(spl, rng, sl, key[k], CT::make(key[k], i))], 1u);
+                if (i < n) atomicAdd(&hist[bucket_fast<T, false>(spl, rng, sl, key[k], CT::make(key[k], i + ioff))], 1u);
             }
         }
     }
@@ -643,7 +645,8 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
                                                                     const typename Comp<T>::C *__restrict__ spl_g,
                                                                     const BkMap *__restrict__ map, int B, int BP, int subs,
                                                                     const uint32_t *__restrict__ offs,
-                                                                    T *__restrict__ out, T *__restrict__ out2) {
+                                                                    T *__restrict__ out, T *__restrict__ out2,
+                                                                    uint64_t ioff) {
     using CT = Comp<T>;
     using G = LineGeo<T>;
     using V = typename std::conditional<sizeof(T) == 4, int4, longlong2>::type;
@@ -721,7 +724,7 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
             const uint64_t i = s0 + tb + (uint64_t)k * BK_T;
             pk[k] = ~0u;
             if (i < n) {
-                const int b = bucket_fast<T, true>(spl_look, rng, sl[k], key[k], CT::make(key[k], i));
+                const int b = bucket_fast<T, true>(spl_look, rng, sl[k], key[k], CT::make(key[k], i + ioff));
                 pk[k] = atomicAdd(&hist[b], 1u) | (uint32_t)b << 16;
             }
         }

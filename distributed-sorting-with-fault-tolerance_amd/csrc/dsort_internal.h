@@ -9,6 +9,7 @@
 #include <atomic>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "dsort.h"
 
@@ -133,6 +134,10 @@ struct dsort_ctx {
     size_t small_bytes = 0;
     void *small_host = nullptr;  // pinned
     size_t small_host_bytes = 0;
+    void *bxs = nullptr;    // bucket exchange: this rank's and every rank's splitter samples
+    size_t bxs_bytes = 0;
+    int ev_done = 2;        // the stage event a sort's second level records at its end (the bucket
+                            // exchange records its own end as event 4)
     // stage timing
     hipEvent_t ev[15] = {};  // 0 start, 1 tile sort done, 2 local sort done, 3 exchange done,
                              // 4 final merge done, 5/6 around the key all-to-all, 7/8 around the
@@ -190,6 +195,44 @@ void fault_point(dsort_ctx *ctx, hipStream_t s, int stage);
 int sort_stages(const dsort_opts &opt, uint64_t n, int key_bytes);
 // Largest log2 fan-in of one merge pass: the option, else the key type's default.
 int max_logf(const dsort_opts &opt, int type_default, int type_cap);
+
+// ----------------------------------------------------------------------------------------
+// Bucket exchange (the multi-GPU sample sort): every rank cuts its UNSORTED keys
+// into Btot = P * Bl global buckets by splitters taken from every rank's samples (the first
+// partition level of the one-GPU sort, with global splitters), ships buckets [q Bl, (q+1) Bl) to
+// rank q, and finishes its own Bl buckets with the second level and the tile sort -- the received
+// pieces of a bucket are its chunks.  No sorted runs are merged anywhere.
+// ----------------------------------------------------------------------------------------
+struct BxSample {  // a splitter sample: key (sign-extended) and position in its rank's keys
+    int64_t k;
+    uint64_t i;
+};
+struct BxPlan {
+    int P, me, Bl, Btot;
+    uint64_t n_local, n_total;
+    uint32_t s_max;                 // sample records per rank (the all-gather's unit)
+    std::vector<uint64_t> n_of;     // keys of every rank
+    std::vector<uint64_t> ioff;     // composite index of every rank's first key (prefix of n_of)
+    std::vector<uint32_t> s_of;     // real samples of every rank (the rest of its s_max: padding)
+};
+// The plan from every rank's key count; false when the bucket exchange does not apply (too few
+// keys, the second level or the partition switched off): the caller takes the sort-then-merge path.
+bool bx_make_plan(const dsort_opts &opt, int P, int me, const uint64_t *n_of, int key_bytes, BxPlan &plan);
+// 1. this rank's s_of[me] regular samples of d_in into d_smp (s_max records, the rest padded)
+template <typename T>
+int bx_sample(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, BxSample *d_smp, hipStream_t s);
+// 2. the global splitters from every rank's records (d_all: P * s_max), then the first partition
+//    level of d_in into ctx->scratch (bucket-major, Btot buckets).  *hb = this rank's bucket starts
+//    (host, Btot + 1), *part = the partitioned keys.  Kill stage 0 fires here.
+template <typename T>
+int bx_partition(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, const BxSample *d_all, hipStream_t s, bool timed,
+                 const uint64_t **hb, T **part);
+// 3. after the exchange: recv holds the pieces of this rank's buckets from every source s at
+//    roff[s] (source-major, each source's pieces in bucket order), hb_all[s * (Btot + 1) + g] =
+//    source s's bucket starts.  Sorts them into out (nrecv keys).  Kill stages 1 and 2 fire here.
+template <typename T>
+int bx_local_sort(dsort_ctx *ctx, T *recv, T *out, const BxPlan &pl, const uint64_t *hb_all,
+                  const uint64_t *roff, hipStream_t s, bool timed);
 
 }  // namespace dsort
 

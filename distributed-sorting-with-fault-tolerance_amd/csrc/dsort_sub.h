@@ -42,7 +42,7 @@ template <typename T> constexpr int SB_SUB = SB_T * SB_KPT<T>;   // keys of a su
 template <typename T> constexpr int SB_CH = SB_ST * SB_SUB<T>;   // keys of a chunk
 
 struct BInfo {       // one first-level bucket (host-built)
-    uint64_t start;  // first key (position in the first level's output)
+    uint64_t start;  // first key of its output range (one piece: also its first key in the source)
     uint64_t soff;   // first sample
     uint32_t len;    // keys
     uint32_t nsub;   // sub-buckets, 1..SB_MAXS
@@ -50,13 +50,30 @@ struct BInfo {       // one first-level bucket (host-built)
     uint32_t c0, c1; // chunks [c0, c1)
     uint32_t single; // sample single keys (the retry after the local partition: its chunks are
                      // partitioned, so adjacent keys lie in one old sub-bucket)
+    uint32_t multi;  // the bucket's keys lie in several source pieces (the multi-GPU path: one per
+                     // sending rank), found through its chunks (Chunk.boff); else at start..
 };
 
 struct Chunk {
-    uint64_t start;
+    uint64_t start;  // first key in the source
     uint32_t len;
     uint32_t b;
+    uint32_t boff;   // keys of its bucket in the chunks before it
+    uint32_t pad;
 };
+
+// Source position of key p (0 <= p < len) of bucket b in the order of its chunks: b.start + p for a
+// one-piece bucket; a bucket of several pieces finds its chunk (binary search over boff).
+__device__ __forceinline__ uint64_t bucket_src_pos(const BInfo &b, const Chunk *ch, uint64_t p) {
+    if (!b.multi) return b.start + p;
+    uint32_t lo = b.c0, hi = b.c1 - 1;  // the last chunk with boff <= p
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (ch[mid].boff <= p) lo = mid;
+        else hi = mid - 1;
+    }
+    return ch[lo].start + (p - ch[lo].boff);
+}
 
 // Chunk c: from the table, or (ch == NULL: the first level, one segment) SB_CH<T>-key pieces of
 // segment 0 in order.
@@ -64,7 +81,8 @@ template <typename T>
 __device__ __forceinline__ Chunk chunk_of(const Chunk *ch, const BInfo *bi, uint32_t c) {
     if (ch) return ch[c];
     const uint64_t o = (uint64_t)c * SB_CH<T>, len = bi[0].len;
-    return Chunk{bi[0].start + o, (uint32_t)(len - o < (uint64_t)SB_CH<T> ? len - o : (uint64_t)SB_CH<T>), 0u};
+    return Chunk{bi[0].start + o, (uint32_t)(len - o < (uint64_t)SB_CH<T> ? len - o : (uint64_t)SB_CH<T>), 0u,
+                 (uint32_t)o, 0u};
 }
 
 template <typename T> struct KeyU;
@@ -148,10 +166,11 @@ __device__ __forceinline__ int sub_of(const Spl<T> *spl, const uint32_t *rng, T 
 // not a multiple of 4) samples single keys.
 constexpr uint32_t SB_RUN = 4;
 __host__ __device__ __forceinline__ uint32_t sample_run(const BInfo &b) { return b.single || b.ns % SB_RUN ? 1u : SB_RUN; }
+// (positions relative to the bucket: bucket_src_pos maps them to the source)
 __host__ __device__ __forceinline__ uint64_t sample_run_pos(const BInfo &b, uint32_t run, uint64_t r) {
     const uint64_t nr = b.ns / run;
     const uint64_t p = ((2 * r + 1) * b.len) / (2 * nr);
-    return b.start + (p + run > b.len ? b.len - run : p);
+    return p + run > b.len ? b.len - run : p;
 }
 __host__ __device__ __forceinline__ uint64_t sample_pos(const BInfo &b, uint64_t k) {
     const uint32_t run = sample_run(b);
@@ -159,17 +178,18 @@ __host__ __device__ __forceinline__ uint64_t sample_pos(const BInfo &b, uint64_t
 }
 template <typename T>
 __global__ void __launch_bounds__(SB_T) sb_sample_kernel(const T *__restrict__ src, const BInfo *__restrict__ bi,
-                                                         T *__restrict__ smp, int64_t *__restrict__ cmp) {
+                                                         const Chunk *__restrict__ ch, T *__restrict__ smp,
+                                                         int64_t *__restrict__ cmp) {
     const BInfo b = bi[blockIdx.x];
     auto put = [&](uint64_t k, T key) {
         const uint64_t g = b.soff + k;
         smp[g] = key;
         if constexpr (sizeof(T) == 4) cmp[g] = (int64_t)((uint64_t)(int64_t)key << 32 | (uint32_t)g);
     };
-    if (sample_run(b) == SB_RUN) {
+    if (sample_run(b) == SB_RUN && !b.multi) {
 #pragma unroll 2  // (independent gathers in flight)
         for (uint32_t r = threadIdx.x; r < b.ns / SB_RUN; r += SB_T) {
-            const T *p = src + sample_run_pos(b, SB_RUN, r);
+            const T *p = src + b.start + sample_run_pos(b, SB_RUN, r);
             T key[SB_RUN];
 #pragma unroll
             for (uint32_t i = 0; i < SB_RUN; ++i) key[i] = p[i];
@@ -177,7 +197,8 @@ __global__ void __launch_bounds__(SB_T) sb_sample_kernel(const T *__restrict__ s
             for (uint32_t i = 0; i < SB_RUN; ++i) put((uint64_t)r * SB_RUN + i, key[i]);
         }
     } else {
-        for (uint32_t k = threadIdx.x; k < b.ns; k += SB_T) put(k, src[sample_run_pos(b, 1, k)]);
+        // (a run of a bucket of several pieces may cross a chunk: every key mapped on its own)
+        for (uint32_t k = threadIdx.x; k < b.ns; k += SB_T) put(k, src[bucket_src_pos(b, ch, sample_pos(b, k))]);
     }
 }
 
@@ -222,7 +243,8 @@ __global__ void __launch_bounds__(SB_T) sb_rank_kernel(const int64_t *__restrict
 // (splitters with slot <= s) << 16.
 template <typename T>
 __global__ void __launch_bounds__(SB_MAXS) sb_splitter_kernel(const int64_t *__restrict__ cmp, const T *__restrict__ smp,
-                                                              const BInfo *__restrict__ bi, int os, int SS,
+                                                              const BInfo *__restrict__ bi, const Chunk *__restrict__ ch,
+                                                              int os, int SS,
                                                               Spl<T> *__restrict__ spl, uint32_t *__restrict__ rng,
                                                               SlotFn<T> *__restrict__ sfn) {
     using U = typename KeyU<T>::U;
@@ -242,7 +264,7 @@ __global__ void __launch_bounds__(SB_MAXS) sb_splitter_kernel(const int64_t *__r
             const T K = smp[g];
             Spl<T> sp{};
             sp.k = K;
-            sp.p = (uint32_t)sample_pos(b, g - b.soff);
+            sp.p = (uint32_t)bucket_src_pos(b, ch, sample_pos(b, g - b.soff));
             spl[(uint64_t)blockIdx.x * SS + tid] = sp;
             sslot[tid] = slot_of<T>(K, klo, sh);
         }

@@ -1662,16 +1662,51 @@ static int merge_split_subbuckets(dsort_ctx *ctx, const sb::Ovf *d_ovf, uint32_t
     return DSORT_OK;
 }
 
+// Where the second level's buckets lie in its source (sub_sort): nullptr -- bucket b is
+// src[hb[b], hb[b+1]), the first level's own output; or a PieceMap -- bucket b is the
+// concatenation of pieces p[first[b] .. first[b+1]) (the multi-GPU path: one piece per sending
+// rank in the receive buffer), and pure buckets are written as their one key.
+struct SrcPiece {
+    uint64_t src, len;
+};
+template <typename T>
+struct PieceMap {
+    std::vector<SrcPiece> p;
+    std::vector<uint32_t> first;  // B + 1
+    std::vector<T> pure_key;      // B: the key of a pure bucket
+};
+// Fill of output ranges with one key (pure buckets of the multi-GPU path): segment blockIdx.y.
+template <typename T>
+struct FillSeg {
+    uint64_t dst, len;
+    T key;
+};
+template <typename T>
+__global__ void __launch_bounds__(256) fill_segments_kernel(T *out, const FillSeg<T> *segs) {
+    const FillSeg<T> f = segs[blockIdx.y];
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < f.len; i += (uint64_t)gridDim.x * 256)
+        out[f.dst + i] = f.key;
+}
+
 template <typename T>
 static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_t *hb, int B, uint64_t m,
                     hipStream_t s, bool timed, bool local, const uint8_t *pure, bool pure_done, const void *bspl,
-                    bool retry = false) {
+                    bool retry = false, const PieceMap<T> *pm = nullptr) {
     using namespace sb;
     constexpr int TILE = TILE_OF<T>;
     constexpr uint64_t ALIGN = KPC<T>;
     const bool asked_local = local;
+    const uint64_t LCH = SB_LCH<T>;
+    // chunks of bucket b at chunk size ch
+    auto bucket_chunks = [&](int b, uint64_t ch) -> uint64_t {
+        if (pure[b]) return 0;
+        if (!pm) return ceil_div(hb[b + 1] - hb[b], ch);
+        uint64_t c = 0;
+        for (uint32_t q = pm->first[b]; q < pm->first[b + 1]; ++q) c += ceil_div(pm->p[q].len, ch);
+        return c;
+    };
     for (int b = 0; b < B && local; ++b)
-        if (!pure[b] && ceil_div(hb[b + 1] - hb[b], (uint64_t)SB_LCH<T>) > (uint64_t)kMaxPieces<T>) local = false;
+        if (bucket_chunks(b, LCH) > (uint64_t)kMaxPieces<T>) local = false;
     if (reinterpret_cast<uintptr_t>(src) % 16) local = false;  // (the gather reads aligned 16-byte vectors)
     if (asked_local && !local) ctx->stats.sub_scatter_fallback = 1;
     const uint64_t CH = local ? SB_LCH<T> : SB_CH<T>;
@@ -1698,7 +1733,7 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         const uint64_t len = pure[b] ? 0 : hb[b + 1] - hb[b];  // (a pure bucket: no chunks, no tiles)
         uint64_t ns = len <= (uint64_t)TILE ? 1 : ceil_div(len, m);
         ns = ns > (uint64_t)SB_MAXS ? SB_MAXS : ns;
-        const uint64_t nc = ceil_div(len, CH);
+        const uint64_t nc = bucket_chunks(b, CH);
         if (local && len) {
             PS = nc > PS ? (uint32_t)nc : PS;
             // (+ 8: the split tiles of a rare sub-bucket above a tile; beyond the bound the sort
@@ -1706,7 +1741,7 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
             tcap += 2 * len / ((uint64_t)TILE - 2 * (ALIGN - 1) * nc) + 1 + 8;
         }
         bi[b] = BInfo{hb[b], nsmp, (uint32_t)len, (uint32_t)ns, ns > 1 ? (uint32_t)(ns * os) : 0u, (uint32_t)nch,
-                      (uint32_t)(nch + nc), retry ? 1u : 0u};
+                      (uint32_t)(nch + nc), retry ? 1u : 0u, pm ? 1u : 0u};
         nsmp += bi[b].ns;
         nch += nc;
         nsubs += ns;
@@ -1723,7 +1758,7 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
                  o_cnt = take(nch * (SS + 1) * 4), o_offs = take(local ? 0 : nch * SS * 4),
                  o_tt = take(tmax * sizeof(GTile)),
                  o_ovf = take(nsubs * sizeof(Ovf)), o_num = take(8), o_stl = take(B * sizeof(bk::TileRef) + 16),
-                 o_pcs = take(local ? tcap * PS * sizeof(uint2) : 0);
+                 o_pcs = take(local ? tcap * PS * sizeof(uint2) : 0), o_fill = take(pm ? B * sizeof(FillSeg<T>) : 0);
     int rc = ensure(ctx, &ctx->sub, &ctx->sub_bytes, off, "sub-bucket partition");
     if (rc) return rc;
     char *a = static_cast<char *>(ctx->sub);
@@ -1743,7 +1778,8 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
     // pinned staging: the two tables, the sample tiles + count, then the two counters read back
     const size_t h_ch = (B * sizeof(BInfo) + 15) & ~(size_t)15, h_stl = h_ch + nch * sizeof(Chunk);
     const size_t h_num = h_stl + B * sizeof(bk::TileRef) + 16;
-    const size_t hbytes = h_num + 16;
+    const size_t h_fill = h_num + 16;
+    const size_t hbytes = h_fill + (pm ? B * sizeof(FillSeg<T>) : 0);
     if (ctx->sub_host_bytes < hbytes) {
         if (ctx->sub_host) (void)hipHostFree(ctx->sub_host);
         ctx->sub_host = nullptr;
@@ -1757,9 +1793,31 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
     char *h = static_cast<char *>(ctx->sub_host);
     std::memcpy(h, bi.data(), B * sizeof(BInfo));
     Chunk *hc = reinterpret_cast<Chunk *>(h + h_ch);
-    for (int b = 0; b < B; ++b)
-        for (uint64_t o = 0; o < bi[b].len; o += CH)
-            *hc++ = Chunk{bi[b].start + o, (uint32_t)(bi[b].len - o < CH ? bi[b].len - o : CH), (uint32_t)b};
+    for (int b = 0; b < B; ++b) {
+        if (!bi[b].len) continue;
+        if (!pm) {
+            for (uint64_t o = 0; o < bi[b].len; o += CH)
+                *hc++ = Chunk{bi[b].start + o, (uint32_t)(bi[b].len - o < CH ? bi[b].len - o : CH), (uint32_t)b,
+                              (uint32_t)o, 0u};
+            continue;
+        }
+        uint64_t boff = 0;  // the bucket's pieces in order, each cut into chunks
+        for (uint32_t q = pm->first[b]; q < pm->first[b + 1]; ++q) {
+            const SrcPiece &pc = pm->p[q];
+            for (uint64_t o = 0; o < pc.len; o += CH, boff += CH)
+                *hc++ = Chunk{pc.src + o, (uint32_t)(pc.len - o < CH ? pc.len - o : CH), (uint32_t)b, (uint32_t)boff, 0u};
+            boff -= ceil_div(pc.len, CH) * CH - pc.len;  // (the last chunk of a piece may be short)
+        }
+    }
+    // pure buckets of a piece map: their one key written over their output range
+    FillSeg<T> *hf = reinterpret_cast<FillSeg<T> *>(h + h_fill);
+    uint32_t nfill = 0;
+    uint64_t maxfill = 0;
+    for (int b = 0; pm && b < B; ++b)
+        if (pure[b] && hb[b + 1] > hb[b]) {
+            hf[nfill++] = FillSeg<T>{hb[b], hb[b + 1] - hb[b], pm->pure_key[b]};
+            maxfill = std::max(maxfill, hb[b + 1] - hb[b]);
+        }
     bk::TileRef *hst = reinterpret_cast<bk::TileRef *>(h + h_stl);
     uint32_t nst = 0;
     for (int b = 0; b < B; ++b)
@@ -1775,14 +1833,22 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
     if (nch) DSORT_HIP(ctx, hipMemcpyAsync(dch, h + h_ch, nch * sizeof(Chunk), hipMemcpyHostToDevice, ctx->side));
     DSORT_HIP(ctx, hipMemcpyAsync(stl, hst, B * sizeof(bk::TileRef) + 16, hipMemcpyHostToDevice, ctx->side));
     DSORT_HIP(ctx, hipMemsetAsync(num, 0, 8, ctx->side));
+    if (nfill)
+        DSORT_HIP(ctx, hipMemcpyAsync(a + o_fill, hf, nfill * sizeof(FillSeg<T>), hipMemcpyHostToDevice, ctx->side));
     DSORT_HIP(ctx, hipEventRecord(ctx->side_ev, ctx->side));
     DSORT_HIP(ctx, hipStreamWaitEvent(s, ctx->side_ev, 0));
     uint64_t npure = 0;
     for (int b = 0; b < B; ++b) npure += pure[b] ? hb[b + 1] - hb[b] : 0;
     ctx->stats.tile_sort_keys = n - npure;
     // pure buckets (one key) to the output as they lie, runs of them in one copy (unless the
-    // scatter wrote them there)
-    for (int b = 0; b < B && !pure_done;) {
+    // scatter wrote them there); a piece map's pure buckets are filled with their key
+    if (nfill) {
+        const unsigned gx = (unsigned)std::min<uint64_t>(ceil_div(maxfill, 256 * 16), 1024);
+        hipLaunchKernelGGL(fill_segments_kernel<T>, dim3(gx, nfill), dim3(256), 0, s, d_keys,
+                           reinterpret_cast<const FillSeg<T> *>(a + o_fill));
+        DSORT_HIP(ctx, hipGetLastError());
+    }
+    for (int b = 0; b < B && !pure_done && !pm;) {
         if (!pure[b]) {
             ++b;
             continue;
@@ -1797,7 +1863,7 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
     // 1. splitters of every bucket from a regular sample.  A bucket's samples fit one int64 tile,
     // so the tile sort alone sorts them, one workgroup per bucket.
     if (nsmp) {
-        hipLaunchKernelGGL(sb_sample_kernel<T>, dim3((unsigned)B), dim3(SB_T), 0, s, src, dbi, smp, cmp);
+        hipLaunchKernelGGL(sb_sample_kernel<T>, dim3((unsigned)B), dim3(SB_T), 0, s, src, dbi, dch, smp, cmp);
         DSORT_HIP(ctx, hipGetLastError());
         const uint4 *stl4 = reinterpret_cast<const uint4 *>(stl);
         const uint32_t *pnst = reinterpret_cast<const uint32_t *>(stl + B);
@@ -1808,7 +1874,7 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         }
         rc = tile_sort<int64_t, false>(ctx, cmp, cmp, nsmp, stl4, pnst, sb::Gather{}, nst, s, false);
         if (rc) return rc;
-        hipLaunchKernelGGL(sb_splitter_kernel<T>, dim3((unsigned)B), dim3(SB_MAXS), 0, s, cmp, smp, dbi, os, SS, spl,
+        hipLaunchKernelGGL(sb_splitter_kernel<T>, dim3((unsigned)B), dim3(SB_MAXS), 0, s, cmp, smp, dbi, dch, os, SS, spl,
                            rng, sfn);
         DSORT_HIP(ctx, hipGetLastError());
     }
@@ -1838,7 +1904,7 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         // in one sub-bucket of this attempt.
         if (ntiles > tmax || ntiles > tcap) {
             ctx->stats.sub_scatter_fallback = 1;
-            return sub_sort<T>(ctx, src, d_keys, n, hb, B, m, s, timed, false, pure, pure_done, bspl, true);
+            return sub_sort<T>(ctx, src, d_keys, n, hb, B, m, s, timed, false, pure, pure_done, bspl, true, pm);
         }
         fault_point(ctx, s, 1);  // second-level partition done
         ctx->stats.merge_passes = 0;
@@ -1860,8 +1926,8 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
             if (rc) return rc;
         }
         if (timed && ctx->ev_ok) {
-            DSORT_HIP(ctx, hipEventRecord(ctx->ev[2], s));
-            ctx->ev_mask |= 4u;
+            DSORT_HIP(ctx, hipEventRecord(ctx->ev[ctx->ev_done], s));
+            ctx->ev_mask |= 1u << ctx->ev_done;
         }
         return DSORT_OK;
     }
@@ -1920,49 +1986,55 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         ctx->stats.sub_split_subbuckets = (int)novf;
     }
     if (timed && ctx->ev_ok) {
-        DSORT_HIP(ctx, hipEventRecord(ctx->ev[2], s));
-        ctx->ev_mask |= 4u;
+        DSORT_HIP(ctx, hipEventRecord(ctx->ev[ctx->ev_done], s));
+        ctx->ev_mask |= 1u << ctx->ev_done;
     }
     return DSORT_OK;
 }
 
+// The first level's device arena (ctx->bucket): the splitter samples (their layout is the
+// caller's: smp_bytes), splitters, per-workgroup counts, chunk sums, offsets, bucket starts, the
+// tile table of the merge path, the slot map.
 template <typename T>
-static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipStream_t s, bool timed, int B) {
+struct BkLayout {
+    using C = typename bk::Comp<T>::C;
+    int B, BP, subs;
+    uint64_t G, nchunk, tmax;
+    char *smp;
+    C *spl;
+    uint32_t *cnt, *offs, *ntl;
+    uint64_t *part, *bst;
+    bk::TileRef *tt;
+    bk::BkMap *map;
+};
+template <typename T>
+static int bk_layout(dsort_ctx *ctx, uint64_t n, int B, size_t smp_bytes, BkLayout<T> &L) {
     using namespace bk;
     using C = typename Comp<T>::C;
-    constexpr int TILE = TILE_OF<T>;
-    constexpr uint64_t ALIGN = KPC<T>;
-    const int BP = 1 << ceil_log2((uint64_t)B);
-    const int subs = bucket_wg_subs<T>(n);
-    const uint64_t G = ceil_div(n, (uint64_t)subs * BK_T * Geo<T>::KPT);
-    const uint64_t nchunk = ceil_div(G, BK_CHUNK);
-    const int os = bucket_os(ctx);
-    const uint32_t S = (uint32_t)B * (uint32_t)os;
-    const uint64_t tmax = ceil_div(n, TILE) + 2 * (uint64_t)B;  // + a head and a tail per bucket
-    // device arena: samples, splitters, counts, chunk sums, offsets, bucket starts, tile table
+    L.B = B;
+    L.BP = 1 << ceil_log2((uint64_t)B);
+    L.subs = bucket_wg_subs<T>(n);
+    L.G = ceil_div(n ? n : 1, (uint64_t)L.subs * BK_T * Geo<T>::KPT);
+    L.nchunk = ceil_div(L.G, BK_CHUNK);
+    L.tmax = ceil_div(n, TILE_OF<T>) + 2 * (uint64_t)B;  // + a head and a tail per bucket
     size_t off = 0;
     auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
-    // samples: int32 composites; int64 keys, sorted keys and composites (3 x 8 bytes)
-    const size_t o_smp = take((size_t)S * (sizeof(T) == 8 ? 24 : sizeof(C))), o_spl = take((size_t)BP * sizeof(C)),
-                 o_cnt = take((size_t)G * B * 4), o_part = take((size_t)nchunk * B * 8),
-                 o_offs = take((size_t)G * B * 4), o_bst = take((size_t)(B + 1) * 8),
-                 o_tt = take((size_t)tmax * sizeof(TileRef)), o_nt = take(4), o_map = take(sizeof(BkMap));
+    const size_t o_smp = take(smp_bytes), o_spl = take((size_t)L.BP * sizeof(C)), o_cnt = take((size_t)L.G * B * 4),
+                 o_part = take((size_t)L.nchunk * B * 8), o_offs = take((size_t)L.G * B * 4),
+                 o_bst = take((size_t)(B + 1) * 8), o_tt = take((size_t)L.tmax * sizeof(TileRef)), o_nt = take(4),
+                 o_map = take(sizeof(BkMap));
     int rc = ensure(ctx, &ctx->bucket, &ctx->bucket_bytes, off, "bucket partition");
     if (rc) return rc;
     char *a = static_cast<char *>(ctx->bucket);
-    C *smp = reinterpret_cast<C *>(a + o_smp);
-    C *spl = reinterpret_cast<C *>(a + o_spl);
-    uint32_t *cnt = reinterpret_cast<uint32_t *>(a + o_cnt);
-    uint64_t *part = reinterpret_cast<uint64_t *>(a + o_part);
-    uint32_t *offs = reinterpret_cast<uint32_t *>(a + o_offs);  // (positions mod 2^32: the scatter's index width)
-    uint64_t *bst = reinterpret_cast<uint64_t *>(a + o_bst);
-    TileRef *tt = reinterpret_cast<TileRef *>(a + o_tt);
-    uint32_t *ntl = reinterpret_cast<uint32_t *>(a + o_nt);
-    BkMap *map = reinterpret_cast<BkMap *>(a + o_map);
-    // (+ 16 bytes: the gathering tile sort reads the 16-byte vector that holds the last key)
-    rc = ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, n * sizeof(T) + 16, "sort scratch");
-    if (rc) return rc;
-    T *scratch = static_cast<T *>(ctx->scratch);
+    L.smp = a + o_smp;
+    L.spl = reinterpret_cast<C *>(a + o_spl);
+    L.cnt = reinterpret_cast<uint32_t *>(a + o_cnt);
+    L.part = reinterpret_cast<uint64_t *>(a + o_part);
+    L.offs = reinterpret_cast<uint32_t *>(a + o_offs);  // (positions mod 2^32: the scatter's index width)
+    L.bst = reinterpret_cast<uint64_t *>(a + o_bst);
+    L.tt = reinterpret_cast<TileRef *>(a + o_tt);
+    L.ntl = reinterpret_cast<uint32_t *>(a + o_nt);
+    L.map = reinterpret_cast<BkMap *>(a + o_map);
     const size_t hbytes = (size_t)(BK_MAXB + 1) * 8 + (size_t)BK_MAXB * 16;  // starts, then the splitters
     if (ctx->bucket_host_bytes < hbytes) {
         if (ctx->bucket_host) (void)hipHostFree(ctx->bucket_host);
@@ -1973,7 +2045,89 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
     }
     if (!ctx->bucket_ev && hipEventCreateWithFlags(&ctx->bucket_ev, hipEventDisableTiming) != hipSuccess)
         return set_err(ctx, DSORT_EHIP, "hipEventCreate");
-    uint64_t *hb = static_cast<uint64_t *>(ctx->bucket_host);
+    return DSORT_OK;
+}
+
+// The first level once the splitters are in L.spl: slot map, histograms, their scan, the scatter of
+// d_in into part_out (pure buckets into `direct` when not null).  On return the host holds the
+// bucket starts hb[0..B] and the splitters hspl[0..B-2] (it waits for them while the scatter runs).
+// ioff = the composite index of d_in[0].  `tile` != 0: also the merge path's tile table.
+template <typename T>
+static int first_level(dsort_ctx *ctx, const T *d_in, uint64_t n, uint64_t ioff, T *part_out, T *direct,
+                       const BkLayout<T> &L, uint32_t tile, hipStream_t s, bool timed, uint64_t *&hb,
+                       typename bk::Comp<T>::C *&hspl) {
+    using namespace bk;
+    using C = typename Comp<T>::C;
+    const int B = L.B, BP = L.BP;
+    int rc;
+    hb = static_cast<uint64_t *>(ctx->bucket_host);
+    hspl = reinterpret_cast<C *>(hb + BK_MAXB + 1);
+    hipLaunchKernelGGL(bucket_slotmap_kernel<T>, dim3(1), dim3(BK_MAXB), 0, s, L.spl, B, n, L.map);
+    if ((rc = stage_event(ctx, s, timed, 9))) return rc;
+    hipLaunchKernelGGL(bucket_hist_kernel<T>, dim3((unsigned)L.G), dim3(BK_T), 0, s, d_in, n, L.spl, L.map, B, BP,
+                       L.subs, L.cnt, ioff);
+    if ((rc = stage_event(ctx, s, timed, 10))) return rc;
+    hipLaunchKernelGGL(bucket_colsum_kernel, dim3((unsigned)L.nchunk), dim3(BK_MAXB), 0, s, L.cnt, (uint32_t)L.G, B,
+                       L.part);
+    hipLaunchKernelGGL(bucket_scan_kernel, dim3(1), dim3(BK_MAXB), 0, s, L.part, (uint32_t)L.nchunk, B, tile,
+                       (uint32_t)KPC<T>, L.bst, L.tt, L.ntl);
+    hipLaunchKernelGGL(bucket_offsets_kernel<uint32_t>, dim3((unsigned)L.nchunk), dim3(BK_MAXB), 0, s, L.cnt, L.part,
+                       L.bst, (uint32_t)L.G, B, L.offs);
+    DSORT_HIP(ctx, hipGetLastError());
+    // bucket starts to the host (the second level is planned from the bucket sizes); the host
+    // waits for them while the scatter runs.  (The copies run on the side stream once the offsets
+    // are written, so the scatter does not queue behind them: ~10 us of idle GPU per sort.)
+    if ((rc = side_stream(ctx))) return rc;
+    DSORT_HIP(ctx, hipEventRecord(ctx->ready_ev, s));
+    DSORT_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->ready_ev, 0));
+    DSORT_HIP(ctx, hipMemcpyAsync(hb, L.bst, (size_t)(B + 1) * 8, hipMemcpyDeviceToHost, ctx->side));
+    if (B > 1) DSORT_HIP(ctx, hipMemcpyAsync(hspl, L.spl, (size_t)(B - 1) * sizeof(C), hipMemcpyDeviceToHost, ctx->side));
+    DSORT_HIP(ctx, hipEventRecord(ctx->bucket_ev, ctx->side));
+    if ((rc = stage_event(ctx, s, timed, 11))) return rc;
+    hipLaunchKernelGGL(bucket_scatter_lines_kernel<T>, dim3((unsigned)L.G), dim3(BK_T), 0, s, d_in, n, L.spl, L.map, B,
+                       BP, L.subs, L.offs, part_out, direct, ioff);
+    DSORT_HIP(ctx, hipGetLastError());
+    if ((rc = stage_event(ctx, s, timed, 12))) return rc;
+    fault_point(ctx, s, 0);  // first-level partition done
+    DSORT_HIP(ctx, hipEventSynchronize(ctx->bucket_ev));
+    if (hb[B] != n) return set_err(ctx, DSORT_EHIP, "bucket partition lost keys");
+    return DSORT_OK;
+}
+
+// The stats and events of a bucketed sort start after its nested splitter sort.
+static int bucketed_stats_start(dsort_ctx *ctx, uint64_t n, int tile, hipStream_t s, bool timed) {
+    ctx->stats = dsort_stats{};
+    ctx->stats.keys_in = ctx->stats.keys_out = n;
+    ctx->stats.tile_sort_keys = n;
+    ctx->stats.tile_keys = tile;
+    ctx->ev_mask = 0;
+    ctx->kev_used = 0;
+    ctx->last_stream = s;
+    return stage_event(ctx, s, timed, 0);
+}
+
+template <typename T>
+static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipStream_t s, bool timed, int B) {
+    using namespace bk;
+    using C = typename Comp<T>::C;
+    constexpr int TILE = TILE_OF<T>;
+    constexpr uint64_t ALIGN = KPC<T>;
+    const int os = bucket_os(ctx);
+    const uint32_t S = (uint32_t)B * (uint32_t)os;
+    // samples: int32 composites; int64 keys, sorted keys and composites (3 x 8 bytes)
+    BkLayout<T> L;
+    int rc = bk_layout<T>(ctx, n, B, (size_t)S * (sizeof(T) == 8 ? 24 : sizeof(C)), L);
+    if (rc) return rc;
+    const int BP = L.BP;
+    C *smp = reinterpret_cast<C *>(L.smp);
+    C *spl = L.spl;
+    TileRef *tt = L.tt;
+    uint32_t *ntl = L.ntl;
+    const uint64_t tmax = L.tmax;
+    // (+ 16 bytes: the gathering tile sort reads the 16-byte vector that holds the last key)
+    rc = ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, n * sizeof(T) + 16, "sort scratch");
+    if (rc) return rc;
+    T *scratch = static_cast<T *>(ctx->scratch);
     // 1. splitters from a regular sample in (key, input index) order, sorted on the GPU (the
     // sample sorts never bucket and never fire the fault injection)
     int64_t *pk = reinterpret_cast<int64_t *>(smp), *psrt = pk + S, *pcmp = pk + 2 * (size_t)S;
@@ -1995,59 +2149,24 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
     --ctx->nested;
     if (rc) return rc;
     // (the nested sort reset the statistics and events; this sort's start from here)
-    ctx->stats = dsort_stats{};
-    ctx->stats.keys_in = ctx->stats.keys_out = n;
-    ctx->stats.tile_sort_keys = n;
-    ctx->stats.tile_keys = TILE;
-    ctx->ev_mask = 0;
-    ctx->kev_used = 0;
-    ctx->last_stream = s;
-    if (timed && ctx->ev_ok) {
-        DSORT_HIP(ctx, hipEventRecord(ctx->ev[0], s));
-        ctx->ev_mask |= 1u;
-    }
+    if ((rc = bucketed_stats_start(ctx, n, TILE, s, timed))) return rc;
     if constexpr (std::is_same<T, int32_t>::value) {
         hipLaunchKernelGGL(bucket_splitter_kernel<int32_t>, dim3(1), dim3(BK_MAXB), 0, s, smp, B, BP, os, spl);
     } else {
         hipLaunchKernelGGL(pair_splitter_kernel, dim3(1), dim3(BK_MAXB), 0, s, pcmp, pk, (uint64_t)n, S, B, BP, os,
                            spl);
     }
-    // 2. the lookups' slot map, histograms, their scan, the scatter
-    hipLaunchKernelGGL(bucket_slotmap_kernel<T>, dim3(1), dim3(BK_MAXB), 0, s, spl, B, (uint64_t)n, map);
-    if ((rc = stage_event(ctx, s, timed, 9))) return rc;
-    hipLaunchKernelGGL(bucket_hist_kernel<T>, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, map, B, BP,
-                       subs, cnt);
-    if ((rc = stage_event(ctx, s, timed, 10))) return rc;
-    hipLaunchKernelGGL(bucket_colsum_kernel, dim3((unsigned)nchunk), dim3(BK_MAXB), 0, s, cnt, (uint32_t)G, B, part);
-    hipLaunchKernelGGL(bucket_scan_kernel, dim3(1), dim3(BK_MAXB), 0, s, part, (uint32_t)nchunk, B,
-                       sub_keys<T>(ctx) ? 0u : (uint32_t)TILE, (uint32_t)ALIGN, bst, tt, ntl);
-    hipLaunchKernelGGL(bucket_offsets_kernel<uint32_t>, dim3((unsigned)nchunk), dim3(BK_MAXB), 0, s, cnt, part, bst, (uint32_t)G, B, offs);
-    DSORT_HIP(ctx, hipGetLastError());
-    // bucket starts to the host (the pass plan depends on the bucket sizes); the host waits for
-    // them while the scatter runs.  The scatter always writes the scratch buffer (never the
-    // input: the context owns it); the tile sort then writes whichever buffer makes the last
-    // pass land in d_keys.
-    // (the copies run on the side stream once the offsets are written, so the scatter does not
-    // queue behind them: ~10 us of idle GPU per sort)
-    if ((rc = side_stream(ctx))) return rc;
-    DSORT_HIP(ctx, hipEventRecord(ctx->ready_ev, s));
-    DSORT_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->ready_ev, 0));
-    DSORT_HIP(ctx, hipMemcpyAsync(hb, bst, (size_t)(B + 1) * 8, hipMemcpyDeviceToHost, ctx->side));
-    C *hspl = reinterpret_cast<C *>(hb + BK_MAXB + 1);
-    DSORT_HIP(ctx, hipMemcpyAsync(hspl, spl, (size_t)(B - 1) * sizeof(C), hipMemcpyDeviceToHost, ctx->side));
-    DSORT_HIP(ctx, hipEventRecord(ctx->bucket_ev, ctx->side));
+    // 2. the first level.  The scatter always writes the scratch buffer (never the input: the
+    // context owns it); the tile sort then writes whichever buffer makes the last pass land in
+    // d_keys.  Pure buckets (one key, see below) go straight to d_keys, in their final places, when
+    // the second level runs (it skips them) and d_keys is not the input the scatter still reads.
     T *part_out = scratch;
-    // Pure buckets (one key, see below) go straight to d_keys, in their final places, when the
-    // second level runs (it skips them) and d_keys is not the input the scatter still reads.
     T *direct = sub_keys<T>(ctx) && (const void *)d_in != (const void *)d_keys && n < (1ull << 31) ? d_keys : nullptr;
-    if ((rc = stage_event(ctx, s, timed, 11))) return rc;
-    hipLaunchKernelGGL(bucket_scatter_lines_kernel<T>, dim3((unsigned)G), dim3(BK_T), 0, s, d_in, (uint64_t)n, spl, map,
-                       B, BP, subs, offs, part_out, direct);
-    DSORT_HIP(ctx, hipGetLastError());
-    if ((rc = stage_event(ctx, s, timed, 12))) return rc;
-    fault_point(ctx, s, 0);  // first-level partition done
-    DSORT_HIP(ctx, hipEventSynchronize(ctx->bucket_ev));
-    if (hb[B] != n) return set_err(ctx, DSORT_EHIP, "bucket partition lost keys");
+    uint64_t *hb;
+    C *hspl;
+    rc = first_level<T>(ctx, d_in, n, 0, part_out, direct, L, sub_keys<T>(ctx) ? 0u : (uint32_t)TILE, s, timed, hb,
+                        hspl);
+    if (rc) return rc;
     if (const uint64_t m = sub_keys<T>(ctx)) {
         // A bucket between two splitters of the same key holds only that key: it is sorted as it
         // lies (a heavy duplicate -- Zipf's top keys fill whole buckets).  The second level skips
@@ -2195,6 +2314,241 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
     }
     return DSORT_OK;
 }
+
+// ---- bucket exchange (dsort_internal.h; the multi-GPU sample sort) ------------
+// Samples of the bucket exchange: record k < s_r at position ((2k + 1) n) / (2 s_r) with its global
+// index (ioff + position), the rest of the s_max records +inf (they sort last and are never picked).
+template <typename T>
+__global__ void __launch_bounds__(256) bx_sample_kernel(const T *__restrict__ in, uint64_t n, uint64_t ioff,
+                                                        uint32_t s_r, uint32_t s_max, BxSample *__restrict__ out) {
+    const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= s_max) return;
+    if (k < s_r) {
+        const uint64_t pos = ((2 * (uint64_t)k + 1) * n) / (2 * (uint64_t)s_r);
+        out[k] = BxSample{(int64_t)in[pos], ioff + pos};
+    } else {
+        out[k] = BxSample{INT64_MAX, ~0ull};
+    }
+}
+// The records as sort keys: int32 -> the composite key * 2^32 + (global index mod 2^32) (padding:
+// INT64_MAX); int64 -> the keys (their composites follow the rank kernel, as in bucket_sort).
+template <typename T>
+__global__ void __launch_bounds__(256) bx_compose_kernel(const BxSample *__restrict__ all, uint32_t S,
+                                                         int64_t *__restrict__ out) {
+    const uint32_t g = blockIdx.x * 256 + threadIdx.x;
+    if (g >= S) return;
+    const BxSample r = all[g];
+    if constexpr (sizeof(T) == 4)
+        out[g] = r.i == ~0ull ? INT64_MAX : (int64_t)((uint64_t)(int64_t)(int32_t)r.k << 32 | (uint32_t)r.i);
+    else
+        out[g] = r.k;
+}
+// Global splitter b (b < Btot - 1): the sample of rank ((b + 1) S_real) / Btot - 1 in (key, global
+// index) order; +inf up to BP.
+template <typename T>
+__global__ void __launch_bounds__(bk::BK_MAXB) bx_splitter_kernel(const int64_t *__restrict__ srt,
+                                                                 const int64_t *__restrict__ keys,
+                                                                 const BxSample *__restrict__ all, uint64_t S_real,
+                                                                 int Btot, int BP, typename bk::Comp<T>::C *__restrict__ spl) {
+    const int b = threadIdx.x;
+    if (b >= BP) return;
+    if (b >= Btot - 1) {
+        spl[b] = bk::Comp<T>::inf();
+        return;
+    }
+    uint64_t pos = ((uint64_t)(b + 1) * S_real) / (uint64_t)Btot;
+    pos = pos ? pos - 1 : 0;
+    if constexpr (sizeof(T) == 4) {
+        spl[b] = srt[pos];
+    } else {
+        const uint32_t g = (uint32_t)srt[pos];  // composite rank * 2^32 + record index
+        spl[b] = bk::Pair{keys[g], (uint32_t)all[g].i, 0};
+    }
+}
+
+// The bucket arena of a bucket exchange: the first level of n_local keys into Btot buckets, with
+// room for every rank's samples as int64 keys, sorted keys and composites.
+template <typename T>
+static int bx_layout(dsort_ctx *ctx, const BxPlan &pl, BkLayout<T> &L) {
+    const size_t S = (size_t)pl.P * pl.s_max;
+    return bk_layout<T>(ctx, pl.n_local, pl.Btot, S * 24, L);
+}
+
+}  // namespace wv
+
+bool bx_make_plan(const dsort_opts &opt, int P, int me, const uint64_t *n_of, int key_bytes, BxPlan &pl) {
+    pl.P = P;
+    pl.me = me;
+    pl.n_of.assign(n_of, n_of + P);
+    pl.ioff.assign(P + 1, 0);
+    for (int r = 0; r < P; ++r) pl.ioff[r + 1] = pl.ioff[r] + n_of[r];
+    pl.n_total = pl.ioff[P];
+    pl.n_local = n_of[me];
+    // (the one-GPU sort's switches: no partition, or no second level -> the sort-then-merge path)
+    if (opt.buckets == 0 || opt.sub_keys == 0 || P < 1) return false;
+    if (pl.n_total < (uint64_t)P << 22) return false;                 // small: sort locally, then merge
+    if (key_bytes == 4 && pl.n_total > (1ull << 32)) return false;    // composite indices are 32-bit
+    const uint64_t bk = opt.bucket_keys > 0 ? (uint64_t)opt.bucket_keys : (1ull << 20);
+    // (DSORT_OPT_BUCKETS = B forces about B global buckets: B / P per rank)
+    uint64_t bl = opt.buckets > 0 ? (uint64_t)opt.buckets / (uint64_t)P : (pl.n_total / P + bk - 1) / bk;
+    const uint64_t cap = (uint64_t)bk::BK_MAXB / (uint64_t)P;
+    bl = bl > cap ? cap : bl;
+    bl = bl < 1 ? 1 : bl;
+    pl.Bl = (int)bl;
+    pl.Btot = P * pl.Bl;
+    if (pl.Btot < 2) return false;
+    // samples: bucket_os per global bucket, shared out in proportion to the ranks' keys
+    const uint64_t os = opt.bucket_os < 1 ? 1 : (opt.bucket_os > 4096 ? 4096 : (uint64_t)opt.bucket_os);
+    const uint64_t S = (uint64_t)pl.Btot * os;
+    pl.s_of.assign(P, 0);
+    uint32_t mx = 1;
+    for (int r = 0; r < P; ++r) {
+        uint64_t sr = pl.n_total ? (S * n_of[r] + pl.n_total - 1) / pl.n_total : 0;
+        sr = sr > n_of[r] ? n_of[r] : sr;
+        pl.s_of[r] = (uint32_t)sr;
+        mx = (uint32_t)sr > mx ? (uint32_t)sr : mx;
+    }
+    pl.s_max = mx;
+    return true;
+}
+
+template <typename T>
+int bx_sample(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, BxSample *d_smp, hipStream_t s) {
+    hipLaunchKernelGGL(wv::bx_sample_kernel<T>, dim3(wv::ceil_div(pl.s_max, 256)), dim3(256), 0, s, d_in, pl.n_local,
+                       pl.ioff[pl.me], pl.s_of[pl.me], pl.s_max, d_smp);
+    DSORT_HIP(ctx, hipGetLastError());
+    return DSORT_OK;
+}
+
+template <typename T>
+int bx_partition(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, const BxSample *d_all, hipStream_t s, bool timed,
+                 const uint64_t **hb_out, T **part) {
+    using namespace wv;
+    using C = typename bk::Comp<T>::C;
+    ctx->stages_done = 0;
+    BkLayout<T> L;
+    int rc = bx_layout<T>(ctx, pl, L);
+    if (rc) return rc;
+    const uint32_t S = (uint32_t)((size_t)pl.P * pl.s_max);
+    uint64_t S_real = 0;
+    for (int r = 0; r < pl.P; ++r) S_real += pl.s_of[r];
+    int64_t *pk = reinterpret_cast<int64_t *>(L.smp), *psrt = pk + S, *pcmp = pk + 2 * (size_t)S;
+    // the global splitters, identical on every rank (the same records, the same sorts)
+    ++ctx->nested;
+    hipLaunchKernelGGL(bx_compose_kernel<T>, dim3(ceil_div(S, 256)), dim3(256), 0, s, d_all, S, pk);
+    rc = hipGetLastError() == hipSuccess ? DSORT_OK : set_err(ctx, DSORT_EHIP, "bx_compose_kernel launch");
+    if (!rc) {
+        if constexpr (sizeof(T) == 4) {
+            rc = sort_device<int64_t>(ctx, pk, psrt, S, s, false);
+        } else {
+            rc = sort_device<int64_t>(ctx, pk, psrt, S, s, false);
+            if (!rc) {
+                hipLaunchKernelGGL(bk::pair_rank_kernel, dim3(ceil_div(S, 256)), dim3(256), 0, s, pk, psrt, S, pcmp);
+                rc = sort_device<int64_t>(ctx, pcmp, pcmp, S, s, false);
+            }
+        }
+    }
+    --ctx->nested;
+    if (rc) return rc;
+    if ((rc = bucketed_stats_start(ctx, pl.n_local, TILE_OF<T>, s, timed))) return rc;
+    hipLaunchKernelGGL(bx_splitter_kernel<T>, dim3(1), dim3(bk::BK_MAXB), 0, s, sizeof(T) == 4 ? psrt : pcmp, pk, d_all,
+                       S_real, pl.Btot, L.BP, L.spl);
+    DSORT_HIP(ctx, hipGetLastError());
+    rc = ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, pl.n_local * sizeof(T) + 16, "sort scratch");
+    if (rc) return rc;
+    T *scratch = static_cast<T *>(ctx->scratch);
+    uint64_t *hb;
+    C *hspl;
+    if (pl.n_local) {
+        rc = first_level<T>(ctx, d_in, pl.n_local, pl.ioff[pl.me], scratch, nullptr, L, 0u, s, timed, hb, hspl);
+        if (rc) return rc;
+    } else {
+        // no keys here: empty buckets (the splitters still go to the host for the second level)
+        hb = static_cast<uint64_t *>(ctx->bucket_host);
+        hspl = reinterpret_cast<C *>(hb + bk::BK_MAXB + 1);
+        for (int b = 0; b <= pl.Btot; ++b) hb[b] = 0;
+        DSORT_HIP(ctx, hipMemcpyAsync(hspl, L.spl, (size_t)(pl.Btot - 1) * sizeof(C), hipMemcpyDeviceToHost, s));
+        DSORT_HIP(ctx, hipStreamSynchronize(s));
+        fault_point(ctx, s, 0);
+    }
+    if ((rc = stage_event(ctx, s, timed, 2))) return rc;  // the local part done: the exchange starts
+    *hb_out = hb;
+    *part = scratch;
+    return DSORT_OK;
+}
+
+template <typename T>
+int bx_local_sort(dsort_ctx *ctx, T *recv, T *out, const BxPlan &pl, const uint64_t *hb_all, const uint64_t *roff,
+                  hipStream_t s, bool timed) {
+    using namespace wv;
+    using C = typename bk::Comp<T>::C;
+    const int P = pl.P, me = pl.me, Bl = pl.Bl, Bt = pl.Btot;
+    const uint64_t g0 = (uint64_t)me * Bl;
+    // this rank's buckets: one piece per source, in source order
+    PieceMap<T> pm;
+    pm.first.assign(Bl + 1, 0);
+    pm.pure_key.assign(Bl, T(0));
+    std::vector<uint64_t> hbo(Bl + 1, 0);
+    std::vector<uint8_t> pure(Bl, 0);
+    const C *hspl = reinterpret_cast<const C *>(static_cast<const uint64_t *>(ctx->bucket_host) + bk::BK_MAXB + 1);
+    for (int j = 0; j < Bl; ++j) {
+        const uint64_t g = g0 + (uint64_t)j;
+        pm.first[j] = (uint32_t)pm.p.size();
+        uint64_t tot = 0;
+        for (int r = 0; r < P; ++r) {
+            const uint64_t *h = hb_all + (size_t)r * (Bt + 1);
+            const uint64_t len = h[g + 1] - h[g];
+            if (len) pm.p.push_back(SrcPiece{roff[r] + (h[g] - h[g0]), len});
+            tot += len;
+        }
+        hbo[j + 1] = hbo[j] + tot;
+        // a global bucket between two splitters of one key holds only that key
+        if (g >= 1 && g + 2 <= (uint64_t)Bt && bk::Comp<T>::key_of(hspl[g - 1]) == bk::Comp<T>::key_of(hspl[g])) {
+            pure[j] = 1;
+            pm.pure_key[j] = bk::Comp<T>::key_of(hspl[g]);
+        }
+    }
+    pm.first[Bl] = (uint32_t)pm.p.size();
+    const uint64_t nrecv = hbo[Bl];
+    ctx->stats.keys_out = nrecv;
+    ctx->stats.tile_sort_keys = 0;
+    int rc = DSORT_OK;
+    if (nrecv) {
+        BkLayout<T> L;
+        if ((rc = bx_layout<T>(ctx, pl, L))) return rc;  // (the arena as bx_partition left it: the splitters)
+        const int saved = ctx->ev_done;
+        ctx->ev_done = 4;
+        rc = sub_sort<T>(ctx, recv, out, nrecv, hbo.data(), Bl, sub_keys<T>(ctx), s, timed, ctx->opt.sub_gather != 0,
+                         pure.data(), false, L.spl + g0, false, &pm);
+        ctx->ev_done = saved;
+        if (rc) return rc;
+    } else {
+        fault_point(ctx, s, 1);
+        fault_point(ctx, s, 2);
+        if (timed && ctx->ev_ok) {
+            DSORT_HIP(ctx, hipEventRecord(ctx->ev[4], s));
+            ctx->ev_mask |= 16u;
+        }
+    }
+    if (ctx->opt.kill_after_pass >= 0)  // (a kill stage this sort never reached)
+        return set_err(ctx, DSORT_ESTAGE, "DSORT_OPT_KILL_AFTER_STAGE = " + std::to_string(ctx->opt.kill_after_pass) +
+                                              ": the bucket exchange has " + std::to_string(ctx->stages_done) +
+                                              " stages (kill points 0.." + std::to_string(ctx->stages_done - 1) + ")");
+    return DSORT_OK;
+}
+
+template int bx_sample<int32_t>(dsort_ctx *, const int32_t *, const BxPlan &, BxSample *, hipStream_t);
+template int bx_sample<int64_t>(dsort_ctx *, const int64_t *, const BxPlan &, BxSample *, hipStream_t);
+template int bx_partition<int32_t>(dsort_ctx *, const int32_t *, const BxPlan &, const BxSample *, hipStream_t, bool,
+                                   const uint64_t **, int32_t **);
+template int bx_partition<int64_t>(dsort_ctx *, const int64_t *, const BxPlan &, const BxSample *, hipStream_t, bool,
+                                   const uint64_t **, int64_t **);
+template int bx_local_sort<int32_t>(dsort_ctx *, int32_t *, int32_t *, const BxPlan &, const uint64_t *,
+                                    const uint64_t *, hipStream_t, bool);
+template int bx_local_sort<int64_t>(dsort_ctx *, int64_t *, int64_t *, const BxPlan &, const uint64_t *,
+                                    const uint64_t *, hipStream_t, bool);
+
+namespace wv {
 
 template <typename T>
 static int wave_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipStream_t s, bool timed) {

@@ -66,7 +66,7 @@ class Stats(ctypes.Structure):
                 ("partition_ms", ctypes.c_double), ("tile_sort_keys", ctypes.c_size_t),
                 ("bucket_hist_ms", ctypes.c_double), ("bucket_scatter_ms", ctypes.c_double),
                 ("sub_partition_ms", ctypes.c_double), ("sub_split_subbuckets", ctypes.c_int),
-                ("sub_scatter_fallback", ctypes.c_int)]
+                ("sub_scatter_fallback", ctypes.c_int), ("exchange_path", ctypes.c_int)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -5,12 +5,13 @@
  *
  * Per job: map the master's chunk replicas and pin them (dsort_host_register); stage this rank's
  * chunk in HBM (generated on the GPU and copied into the replica, or copied from it); build the
- * communicator of epoch 0; on GO sort the chunk (dsort_sort_dev_copy_*: where client.c:117 calls
- * merge_sort) and run the exchange (dsort_sample_merge_dev_*), report DONE.  A PLAN from the
+ * communicator of epoch 0; on GO run the sample sort of the chunk (dsort_sample_sort_dev_*: the
+ * bucket exchange partitions the unsorted chunk, ships the buckets and sorts the received ones --
+ * where client.c:117 calls merge_sort and server.c:414-415 gathers), report DONE.  A PLAN from the
  * master (a peer failed) aborts the communicator -- also from inside a running exchange, through
  * dsort_comm_abort on the reader thread -- and starts the recovery epoch: the chunks this worker
- * now owns that it has not sorted yet come from the pinned replica, are sorted and merged into
- * its run, and the exchange runs again over the survivors. */
+ * now owns come from the pinned replica and are appended to its keys, and the sample sort runs
+ * again over the survivors. */
 #define _GNU_SOURCE
 #include <arpa/inet.h>
 #include <errno.h>
@@ -328,9 +329,8 @@ int samplesort_worker(const char *host, int port, int device, int verbose) {
     close(sfd);
     CHECK(dsort_host_register(ctx, rep, shm_bytes));
     const uint64_t n0 = job.chunk_len;
-    void *d_chunk = NULL, *d_run = NULL;
+    void *d_chunk = NULL;
     CHECK(dsort_dev_alloc(ctx, &d_chunk, (n0 ? n0 : 1) * kb));
-    CHECK(dsort_dev_alloc(ctx, &d_run, (n0 ? n0 : 1) * kb));
     char *my_rep = rep + job.chunk_off * kb;
     if (job.source == 2) {
         CHECK(dsort_copy_h2d(ctx, d_chunk, my_rep, n0 * kb));
@@ -362,16 +362,12 @@ int samplesort_worker(const char *host, int port, int device, int verbose) {
     pthread_mutex_unlock(&w.mu);
     int exit_code = 0;
     if (start) {
-        const double t_go = now_ms();
-        /* the local sort: the worker's merge_sort (client.c:117); the fault injection of config C5
-         * strikes inside it, after merge pass k */
+        /* the fault injection of config C5 strikes inside the first epoch's sort (after stage k of
+         * the local part: the first partition level, before the exchange; or the second level /
+         * tile sort of the received buckets) */
         CHECK(dsort_set_option(ctx, DSORT_OPT_KILL_AFTER_STAGE, job.kill_after_pass));
-        if (i64) CHECK(dsort_sort_dev_copy_i64(ctx, (const int64_t *)d_chunk, (int64_t *)d_run, n0, NULL));
-        else CHECK(dsort_sort_dev_copy_i32(ctx, (const int32_t *)d_chunk, (int32_t *)d_run, n0, NULL));
-        CHECK(dsort_synchronize(ctx));
-        CHECK(dsort_set_option(ctx, DSORT_OPT_KILL_AFTER_STAGE, -1));
-        const double t_sorted = now_ms() - t_go;
         if (job.hang_before_exchange) raise(SIGSTOP); /* fault injection: hung, not dead */
+        void *d_run = d_chunk; /* the keys this worker owns (unsorted): its chunk, then inherited ones */
         uint64_t run_len = n0;
         uint32_t owned[SS_MAX_CHUNKS];
         uint32_t nowned = 1;
@@ -382,9 +378,14 @@ int samplesort_worker(const char *host, int port, int device, int verbose) {
             const double t_ex = now_ms();
             void *out = NULL;
             size_t nout = 0;
-            rc = i64 ? dsort_sample_merge_dev_i64(ctx, (const int64_t *)d_run, run_len, (int64_t **)&out, &nout, NULL)
-                     : dsort_sample_merge_dev_i32(ctx, (const int32_t *)d_run, run_len, (int32_t **)&out, &nout, NULL);
+            rc = i64 ? dsort_sample_sort_dev_i64(ctx, (const int64_t *)d_run, run_len, (int64_t **)&out, &nout, NULL)
+                     : dsort_sample_sort_dev_i32(ctx, (const int32_t *)d_run, run_len, (int32_t **)&out, &nout, NULL);
             if (!rc) rc = dsort_synchronize(ctx);
+            dsort_set_option(ctx, DSORT_OPT_KILL_AFTER_STAGE, -1); /* (the first epoch only) */
+            /* the local part of the sort: from the call to the start of the key exchange */
+            dsort_stats sst;
+            double t_sorted = 0.0;
+            if (!rc && !dsort_get_stats(ctx, &sst)) t_sorted = sst.total_ms - sst.exchange_ms - sst.final_merge_ms;
             ss_done done;
             memset(&done, 0, sizeof done);
             done.epoch = w.epoch;
@@ -392,7 +393,7 @@ int samplesort_worker(const char *host, int port, int device, int verbose) {
             done.status = rc;
             done.run_keys = run_len;
             done.t_local_sort_ms = t_sorted;
-            done.t_exchange_ms = now_ms() - t_ex;
+            done.t_exchange_ms = now_ms() - t_ex; /* the whole sample sort call */
             done.t_rebuild_ms = t_rebuild;
             if (!rc) {
                 if (nout) {
@@ -445,9 +446,10 @@ int samplesort_worker(const char *host, int port, int device, int verbose) {
             }
             if (!have_plan) break;
             if (job.kill_in_recovery) raise(SIGKILL); /* fault injection: a second failure during recovery */
-            /* recovery epoch: drop the communicator, rebuild the run from the chunks now owned.  A
-             * PLAN for a newer epoch (another worker died meanwhile) restarts from that plan: the
-             * chunks already merged stay owned, the new ones are added. */
+            /* recovery epoch: drop the communicator, append the chunks now owned to the keys (from
+             * the master's pinned replicas; nothing is sorted here: the next sample sort partitions
+             * them with the rest).  A PLAN for a newer epoch (another worker died meanwhile)
+             * restarts from that plan: the chunks already added stay owned, the new ones are added. */
             const double t_rb = now_ms();
         rebuild:
             dsort_comm_abort(ctx);
@@ -458,22 +460,12 @@ int samplesort_worker(const char *host, int port, int device, int verbose) {
                 if (have) continue;
                 uint64_t off, len;
                 chunk_range(job.n_total, job.world, c, &off, &len);
-                void *d_x = NULL, *d_both = NULL, *d_m = NULL;
-                CHECK(dsort_dev_alloc(ctx, &d_x, (len ? len : 1) * kb));
+                void *d_both = NULL;
                 CHECK(dsort_dev_alloc(ctx, &d_both, (run_len + len + 1) * kb));
-                CHECK(dsort_dev_alloc(ctx, &d_m, (run_len + len + 1) * kb));
-                CHECK(dsort_copy_h2d(ctx, d_x, rep + off * kb, len * kb)); /* the master's pinned replica */
                 CHECK(dsort_copy_d2d(ctx, d_both, d_run, run_len * kb));
-                if (i64) CHECK(dsort_sort_dev_copy_i64(ctx, (const int64_t *)d_x, (int64_t *)((char *)d_both + run_len * kb), len, NULL));
-                else CHECK(dsort_sort_dev_copy_i32(ctx, (const int32_t *)d_x, (int32_t *)((char *)d_both + run_len * kb), len, NULL));
-                const size_t lens[2] = {run_len, len};
-                if (i64) CHECK(dsort_merge_dev_i64(ctx, (const int64_t *)d_both, lens, 2, (int64_t *)d_m, NULL));
-                else CHECK(dsort_merge_dev_i32(ctx, (const int32_t *)d_both, lens, 2, (int32_t *)d_m, NULL));
-                CHECK(dsort_synchronize(ctx));
-                dsort_dev_free(ctx, d_x);
-                dsort_dev_free(ctx, d_both);
-                dsort_dev_free(ctx, d_run);
-                d_run = d_m;
+                CHECK(dsort_copy_h2d(ctx, (char *)d_both + run_len * kb, rep + off * kb, len * kb)); /* the replica */
+                if (d_run != d_chunk) dsort_dev_free(ctx, d_run);
+                d_run = d_both;
                 run_len += len;
                 owned[nowned++] = c;
             }
@@ -487,6 +479,7 @@ int samplesort_worker(const char *host, int port, int device, int verbose) {
             t_rebuild = now_ms() - t_rb;
             if (rc) fprintf(stderr, "worker: communicator of epoch %u failed (%d): %s\n", plan.epoch, rc, dsort_last_error(ctx));
         }
+        if (d_run != d_chunk) dsort_dev_free(ctx, d_run);
     }
     pthread_mutex_lock(&w.mu);
     w.stop = 1;
@@ -498,7 +491,6 @@ int samplesort_worker(const char *host, int port, int device, int verbose) {
     pthread_join(rd_th, NULL);
     close(fd);
     dsort_dev_free(ctx, d_chunk);
-    dsort_dev_free(ctx, d_run);
     dsort_host_unregister(ctx, rep);
     munmap(rep, shm_bytes);
     dsort_finalize(ctx);

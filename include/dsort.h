@@ -82,6 +82,9 @@ typedef struct dsort_stats {
     int sub_scatter_fallback; /* 1 when the sort left the default local partition for the
                                  scatter path on its own (a bucket of too many chunks, or more
                                  split tiles than the tile tables hold)                         */
+    int exchange_path;        /* the last sample sort: 1 = bucket exchange (partition, exchange,
+                                 sort the received buckets), 2 = sort, exchange, merge the received
+                                 runs (small inputs, dsort_sample_merge_dev), 0 = not a sample sort */
 } dsort_stats;
 
 /* ---------------------------------------------------------------- lifecycle ---------- */

@@ -105,6 +105,12 @@ int dsort_get_option(const dsort_ctx *ctx, int option, int64_t *v) {
     return DSORT_OK;
 }
 int dsort_synchronize(dsort_ctx *ctx) { (void)ctx; return DSORT_OK; }
+int dsort_get_stats(const dsort_ctx *ctx, dsort_stats *out) {
+    (void)ctx;
+    if (!out) return DSORT_EINVAL;
+    memset(out, 0, sizeof *out); /* (no device timings on the CPU) */
+    return DSORT_OK;
+}
 int dsort_dev_alloc(dsort_ctx *ctx, void **p, size_t bytes) { (void)ctx; *p = malloc(bytes ? bytes : 1); return *p ? DSORT_OK : DSORT_ENOMEM; }
 int dsort_dev_free(dsort_ctx *ctx, void *p) { (void)ctx; free(p); return DSORT_OK; }
 int dsort_copy_h2d(dsort_ctx *ctx, void *d, const void *h, size_t b) { (void)ctx; if (b) memmove(d, h, b); return DSORT_OK; }
@@ -245,6 +251,15 @@ int dsort_sort_stages(const dsort_ctx *ctx, size_t n, int key_bytes, int *stages
         *n_out = tot;                                                                                \
         free(mine); free(all); free(sm); free(cuts); free(cnt); free(mat); free(sc); free(lens); free(recv); \
         return DSORT_OK;                                                                             \
+    }                                                                                                \
+    /* the whole sample sort: the double's local sort (its kill stages), then the exchange */      \
+    int dsort_sample_sort_dev_##SFX(dsort_ctx *ctx, const T *in, size_t n, T **d_out, size_t *n_out, void *st) { \
+        T *tmp = (T *)malloc(sizeof(T) * (n ? n : 1));                                               \
+        if (!tmp) return DSORT_ENOMEM;                                                               \
+        int rc = dsort_sort_dev_copy_##SFX(ctx, in, tmp, n, st);                                     \
+        if (!rc) rc = dsort_sample_merge_dev_##SFX(ctx, tmp, n, d_out, n_out, st);                   \
+        free(tmp);                                                                                   \
+        return rc;                                                                                   \
     }
 #include <limits.h>
 DOUBLE_SORT(int32_t, i32)

@@ -36,8 +36,14 @@ def run(rank, world, port, n_total, dtype, dist, out_path, transport="rccl", dev
     t = torch.empty(max(sz, 1), dtype=tdt, device="cuda")[:sz]
     if dist == "zipf":
         ctx.gen_zipf_i64(t, 0x5EED2026, first)
+    elif dist in ("seq", "rev"):  # globally ascending / descending input (every rank a key range)
+        g = torch.arange(first, first + sz, dtype=torch.int64, device="cuda")
+        g = g if dist == "seq" else n_total - 1 - g
+        t.copy_((g - n_total // 2).to(tdt))
     else:
         ctx.gen_uniform(t, 0x5EED2026, first)
+        if dist == "few":  # 8 distinct keys: whole buckets of one key on every rank
+            t.copy_(t >> (29 if dtype == "i32" else 61))
     torch.cuda.synchronize()
     ptr, nout = ctx.sample_sort_dev(t)
     ctx.synchronize()

@@ -73,3 +73,31 @@ def test_rccl_refuses_shared_gpu_with_clear_error(tmp_path):
 def test_sample_sort_tiny_and_empty_ranks(tmp_path):
     ins, outs, meta = run_ranks(tmp_path, 4, 3)  # rank 3 holds no key
     assert np.array_equal(np.concatenate(outs), np.sort(ins))
+
+
+@pytest.mark.parametrize("world,dtype,dist", [(1, "i32", "uniform"), (2, "i32", "uniform"), (3, "i32", "uniform"),
+                                              (4, "i32", "uniform"), (3, "i32", "seq"), (2, "i32", "rev"),
+                                              (3, "i32", "few"), (2, "i64", "uniform"), (3, "i64", "zipf"),
+                                              (2, "i64", "few")])
+def test_bucket_exchange_bit_exact(tmp_path, world, dtype, dist):
+    """The bucket exchange (dsort_api.hip sample_sort_bx: global splitters from every rank's
+    samples, the first partition level before the exchange, the received pieces finished by the
+    second level and the tile sort): ranks sharing the GPU over the host transport, the
+    concatenated slices equal numpy's sort of the whole input element for element, for uniform,
+    globally sorted / reversed (every rank one key range), few distinct keys (pure buckets filled
+    with their key) and Zipf int64 (heavy keys split across ranks)."""
+    n = world * (1 << 22) + 12_345
+    ins, outs, meta = run_ranks(tmp_path, world, n, dtype, dist)
+    assert ins.size == n
+    assert all(m["stats"]["exchange_path"] == 1 for m in meta), [m["stats"]["exchange_path"] for m in meta]
+    assert np.array_equal(np.concatenate(outs), np.sort(ins))
+    if dist in ("uniform", "seq", "rev"):
+        sizes = [o.size for o in outs]
+        assert max(sizes) <= 1.1 * n / world, sizes
+
+
+def test_small_sample_sort_takes_the_merge_path(tmp_path):
+    """Below 2^22 keys per rank the sample sort sorts locally and merges the received runs."""
+    ins, outs, meta = run_ranks(tmp_path, 2, 1_000_003)
+    assert all(m["stats"]["exchange_path"] == 2 for m in meta)
+    assert np.array_equal(np.concatenate(outs), np.sort(ins))
