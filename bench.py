@@ -388,44 +388,62 @@ STAGE_KERNELS = {
 }
 # the generator and runtime copies are not part of the sort
 NOT_SORT = ("gen_uniform", "gen_zipf", "__amd_rocclr", "fingerprint", "descents")
-PMC_FILES = ("r3_pmc_traffic.json", "r2_pmc_traffic.json")
+PMC_FILES = ("r4_pmc_traffic.json", "r3_pmc_traffic.json", "r2_pmc_traffic.json")
 
 
-def _pmc_doc(w):
+def lib_sha256():
+    """sha256 of the libdsort.so this run loads: the PMC tables record the build they measured."""
+    import hashlib
+
+    import dsort
+    try:
+        with open(dsort.LIB_PATH, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()
+    except OSError:
+        return None
+
+
+def _pmc_doc(w, dist="uniform"):
     """The newest committed rocprofv3 PMC traffic table for key width w (bytes per launch:
-    FETCH_SIZE x 2 + WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md), or None."""
+    FETCH_SIZE x 2 + WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md), or None.  `match`
+    says whether it was measured on this very library build and key distribution (an
+    older table is only an estimate for a newer build)."""
     for name in PMC_FILES:
         path = os.path.join(REPO, "profiles", name)
         try:
             with open(path) as f:
-                doc = json.load(f)
+                top = json.load(f)
         except (OSError, ValueError):
             continue
+        doc = top
         if w != doc.get("key_bytes", 4) and "int64" in doc:
-            doc = doc["int64"]
+            doc = dict(doc["int64"])
         if w == doc.get("key_bytes", 4):
             doc["file"] = "profiles/" + name
+            sha = top.get("lib_sha256")
+            doc["match"] = bool(sha) and sha == lib_sha256() and doc.get("dist", "uniform") == dist
             return doc
     return None
 
 
-def pmc_traffic(kernel, n, w):
+def pmc_traffic(kernel, n, w, dist="uniform"):
     """HBM bytes per launch of `kernel` from the newest PMC table, scaled to this run's key count;
-    None when absent or measured on another key width."""
-    doc = _pmc_doc(w)
-    if not doc or kernel not in doc["kernels"]:
+    None when absent, measured on another key width, or on another build / distribution."""
+    doc = _pmc_doc(w, dist)
+    if not doc or not doc["match"] or kernel not in doc["kernels"]:
         return None
     rec = doc["kernels"][kernel]
     return round(rec["traffic_bytes_per_launch"] * n / doc.get("keys", 1 << 30))
 
 
-def pmc_sort_bytes(n, w):
-    """HBM bytes of one whole sort: every kernel of the PMC table but the generator / copies."""
-    doc = _pmc_doc(w)
+def pmc_sort_bytes(n, w, dist="uniform"):
+    """HBM bytes of one whole sort: every kernel of the PMC table but the generator / copies, and
+    whether the table was measured on this build and distribution."""
+    doc = _pmc_doc(w, dist)
     if not doc:
-        return None, None
+        return None, None, False
     tot = sum(r["traffic_bytes_per_launch"] for k, r in doc["kernels"].items() if not k.startswith(NOT_SORT))
-    return round(tot * n / doc.get("keys", 1 << 30)), doc["file"]
+    return round(tot * n / doc.get("keys", 1 << 30)), doc["file"], doc["match"]
 
 
 # ------------------------------------------------------------------------- GPU runs
@@ -551,7 +569,7 @@ def run_multi(args, rank, world):
     timed = ("exchange_ms", "alltoall_ms", "final_merge_ms", "merge_kernel_ms", "tile_sort_kernel_ms",
              "bucket_hist_ms", "bucket_scatter_ms", "sub_partition_ms")
     acc = {k: 0.0 for k in timed}
-    acc.update({"merge_kernel_launches": 0, "merge_passes": 0, "sent": 0, "tile_sort_keys": 0})
+    acc.update({"merge_kernel_launches": 0, "merge_passes": 0, "sent": 0, "tile_sort_keys": 0, "exchange_path": 0})
     for _ in range(args.steps):
         ptr, nout = ctx.sample_sort_dev(t_in)
         st = ctx.stats()  # synchronizes this rank's stream
@@ -561,6 +579,7 @@ def run_multi(args, rank, world):
         acc["merge_kernel_launches"] += st["merge_kernel_launches"]
         acc["merge_passes"] += st["merge_passes"]
         acc["sent"] += st["keys_sent"]
+        acc["exchange_path"] = st["exchange_path"]
     torch.cuda.synchronize()
     dist.barrier()
     # per-rank figures of the roofline, gathered (rank 0 reports the slowest rank)
@@ -568,7 +587,8 @@ def run_multi(args, rank, world):
     mine = torch.tensor([acc["tile_sort_kernel_ms"] / steps, acc["alltoall_ms"] / steps, acc["exchange_ms"] / steps,
                          acc["final_merge_ms"] / steps, acc["sent"] / steps, sz,
                          acc["bucket_hist_ms"] / steps, acc["bucket_scatter_ms"] / steps,
-                         acc["sub_partition_ms"] / steps, acc["tile_sort_keys"] / steps], dtype=torch.float64)
+                         acc["sub_partition_ms"] / steps, acc["tile_sort_keys"] / steps, acc["exchange_path"]],
+                        dtype=torch.float64)
     everyone = [torch.zeros_like(mine) for _ in range(world)]
     dist.all_gather(everyone, mine)
     A = torch.stack(allinfo)
@@ -597,7 +617,7 @@ def result_header(args, world):
             "data": f"synthetic {args.dist} keys, splitmix64(seed={SEED:#x} + global index)"}
 
 
-def stage_roofline(k, w, n):
+def stage_roofline(k, w, n, dist="uniform"):
     """Per-stage HIP-event times of the sort's kernels (the average launch of each over the timed
     steps) against their algorithmic bytes, and the slowest of them."""
     stages = []
@@ -609,7 +629,7 @@ def stage_roofline(k, w, n):
         ach = nb / (ms * 1e-3) / 1e9
         stages.append({"kernel": kernel, "avg_launch_ms": round(ms, 4), "algorithmic_bytes_per_launch": nb,
                        "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
-                       "traffic": pmc_traffic(kernel, n, w)})
+                       "traffic": pmc_traffic(kernel, n, w, dist)})
     return stages
 
 
@@ -623,7 +643,7 @@ def report_single(args, elapsed, k):
                                     f"(BASELINE metric size); tile {k['tile']} keys, {k['passes']} merge passes",
                         "keys": n, "parallelism": "1 GPU"}
     w = k["w"]
-    stages = stage_roofline(k, w, n)
+    stages = stage_roofline(k, w, n, args.dist)
     if stages:  # the bucketed path: the dominant kernel is the slowest stage
         dom = max(stages, key=lambda r: r["avg_launch_ms"])
     else:  # below 2^25 keys: tile sort + merge passes
@@ -632,7 +652,7 @@ def report_single(args, elapsed, k):
         ach = nb / (tile_ms * 1e-3) / 1e9 if tile_ms > 0 else 0.0
         dom = {"kernel": STAGE_KERNELS[w][3][0], "avg_launch_ms": round(tile_ms, 4),
                "algorithmic_bytes_per_launch": nb, "achieved": round(ach, 1),
-               "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(STAGE_KERNELS[w][3][0], n, w)}
+               "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(STAGE_KERNELS[w][3][0], n, w, args.dist)}
     roof = {"bound": "hbm", "kernel": dom["kernel"], "achieved": dom["achieved"], "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": dom["frac"], "traffic": dom["traffic"],
             "avg_launch_ms": dom["avg_launch_ms"], "algorithmic_bytes_per_launch": dom["algorithmic_bytes_per_launch"],
@@ -642,10 +662,13 @@ def report_single(args, elapsed, k):
             "merge_passes": k["npass"] // max(args.steps, 1), "merge_kernel_ms": round(k["merge_kernel_ms"], 4),
             "whole_sort_single_pass_bound_frac": round(2 * w * n / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
     # SURVEY.md §8d primary: every sort kernel's PMC bytes over the sort's device time
-    pb, src = pmc_sort_bytes(n, w)
+    pb, src, match = pmc_sort_bytes(n, w, args.dist)
     if pb and k["total_ms"] > 0:
-        roof["all_kernels_frac"] = round(pb / (k["total_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        # (a table measured on another build or distribution gives an estimate only, so labelled)
+        key = "all_kernels_frac" if match else "all_kernels_frac_estimate"
+        roof[key] = round(pb / (k["total_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
         roof["all_kernels"] = {"pmc_bytes_per_sort": pb, "device_ms": round(k["total_ms"], 3), "pmc_source": src,
+                               "pmc_measured_on_this_build": match,
                                "rule": "sum of FETCH_SIZE x2 + WRITE_SIZE over the sort's kernels / device time "
                                        "of the sort (HIP events, first splitter kernel to last tile) / 8 TB/s"}
     result["roofline"] = roof
@@ -659,9 +682,14 @@ def report_multi(args, world, elapsed, per_rank, w):
     n = args.keys
     step_ms = 1000.0 * elapsed / args.steps
     result.update({"value": n * args.steps / elapsed, "ms_per_step": step_ms})
+    bx = int(per_rank[0, 10]) == 1
+    how = ("bucket exchange: global splitters, first partition level of the unsorted chunk, RCCL all-to-all of "
+           "buckets over xGMI, second level + tile sort of the received buckets" if bx else
+           "local sort, splitters, RCCL all-to-all over xGMI, merge of the received runs")
     result["config"] = {"workload": f"sample sort of {n} {args.dist} {result['dtype']} keys over {world} GPUs "
-                                    "(equal contiguous chunks, splitters, RCCL all-to-all over xGMI, merge)",
-                        "keys": n, "keys_per_gpu": n // world, "parallelism": f"samplesort x{world}"}
+                                    f"(equal contiguous chunks; {how})",
+                        "keys": n, "keys_per_gpu": n // world, "parallelism": f"samplesort x{world}",
+                        "exchange_path": "bucket exchange" if bx else "sort + merge"}
     # the local sort's stages on every rank (HIP events); the dominant kernel is the slowest stage
     # of the slowest rank
     best = None
@@ -669,7 +697,7 @@ def report_multi(args, world, elapsed, per_rank, w):
         kr = {"tile_sort_kernel_ms": float(per_rank[r, 0]), "bucket_hist_ms": float(per_rank[r, 6]),
               "bucket_scatter_ms": float(per_rank[r, 7]), "sub_partition_ms": float(per_rank[r, 8]),
               "n": float(per_rank[r, 5]), "tile_sort_keys": float(per_rank[r, 9])}
-        for st in stage_roofline(kr, w, int(kr["n"])):
+        for st in stage_roofline(kr, w, int(kr["n"]), args.dist):
             if best is None or st["avg_launch_ms"] > best[1]["avg_launch_ms"]:
                 best = (r, st)
     if best is None:  # below 2^25 keys per rank: the tile sort
@@ -680,7 +708,7 @@ def report_multi(args, world, elapsed, per_rank, w):
         best = (slow, {"kernel": STAGE_KERNELS[w][3][0], "avg_launch_ms": round(tile_ms, 4),
                        "algorithmic_bytes_per_launch": int(bpl), "achieved": round(ach, 1),
                        "frac": round(ach / HBM_PEAK_GBS, 4),
-                       "traffic": pmc_traffic(STAGE_KERNELS[w][3][0], int(n_gpu), w)})
+                       "traffic": pmc_traffic(STAGE_KERNELS[w][3][0], int(n_gpu), w, args.dist)})
     rk, dom = best
     roof = {"bound": "hbm", "kernel": dom["kernel"] + f" (local sort, rank {rk}: the slowest stage of any rank)",
             "achieved": dom["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": dom["frac"],
@@ -702,7 +730,7 @@ def report_multi(args, world, elapsed, per_rank, w):
                         "measured_bytes_slowest_rank": int(sent[r]),
                         "alltoall_ms": round(float(a2a[r]), 4),
                         "exchange_stage_ms": round(float(per_rank[:, 2].max()), 4),
-                        "final_merge_ms": round(float(per_rank[:, 3].max()), 4)}
+                        ("received_buckets_sort_ms" if bx else "final_merge_ms"): round(float(per_rank[:, 3].max()), 4)}
     result["roofline"] = roof
     print(json.dumps(result), flush=True)
 

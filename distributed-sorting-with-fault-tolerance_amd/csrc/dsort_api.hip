@@ -497,11 +497,29 @@ static int sample_sort_bx(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, T **d
         roff[q + 1] = roff[q] + rlen[q];
     }
     const uint64_t nrecv = roff[P];
-    rc = ensure(ctx, &ctx->recv, &ctx->recv_bytes, (nrecv ? nrecv : 1) * sizeof(T) + 16, "receive buffer");
-    if (rc) return rc;
+    // The other ranks' pieces land behind this rank's partitioned keys when they fit (its own buckets
+    // are then read in place: no copy); else everything goes to a receive buffer.
+    const bool behind = nrecv - rlen[me] <= pl.recv_room;
+    std::vector<uint64_t> base(P), rpos(P);  // a source's first key of bucket me*Bl / where it lands
+    {
+        uint64_t o = pl.n_local;
+        for (int q = 0; q < P; ++q) {
+            if (behind && q == me) {
+                base[q] = sdsp[me];
+                rpos[q] = 0;
+                continue;
+            }
+            base[q] = rpos[q] = behind ? o : roff[q];
+            o += behind ? rlen[q] : 0;
+        }
+    }
+    if (!behind) {
+        rc = ensure(ctx, &ctx->recv, &ctx->recv_bytes, (nrecv ? nrecv : 1) * sizeof(T) + 16, "receive buffer");
+        if (rc) return rc;
+    }
     rc = ensure(ctx, &ctx->recv2, &ctx->recv2_bytes, (nrecv ? nrecv : 1) * sizeof(T), "sorted slice");
     if (rc) return rc;
-    T *rb = static_cast<T *>(ctx->recv);
+    T *rb = behind ? part : static_cast<T *>(ctx->recv);  // (the second level's source)
     exchange_fault_point(ctx, 2);
     // 4. the buckets to their ranks: one send and one receive per peer (all-to-all-v over xGMI)
     if (ctx->ev_ok) {
@@ -513,13 +531,13 @@ static int sample_sort_bx(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, T **d
         for (int q = 0; q < P; ++q) {
             if (q == me) continue;
             if (scnt[q]) DSORT_NCCLNB(ctx, ncclSend(part + sdsp[q], scnt[q], nccl_type<T>(), q, ctx->comm, s));
-            if (rlen[q]) DSORT_NCCLNB(ctx, ncclRecv(rb + roff[q], rlen[q], nccl_type<T>(), q, ctx->comm, s));
+            if (rlen[q]) DSORT_NCCLNB(ctx, ncclRecv(rb + rpos[q], rlen[q], nccl_type<T>(), q, ctx->comm, s));
         }
         DSORT_NCCLNB(ctx, ncclGroupEnd());
         rc = exch_wait(ctx, s, false, deadline, "key all-to-all (enqueue)");
         if (rc) return rc;
-        if (scnt[me])
-            DSORT_HIP(ctx, hipMemcpyAsync(rb + roff[me], part + sdsp[me], scnt[me] * sizeof(T), hipMemcpyDeviceToDevice, s));
+        if (scnt[me] && !behind)
+            DSORT_HIP(ctx, hipMemcpyAsync(rb + rpos[me], part + sdsp[me], scnt[me] * sizeof(T), hipMemcpyDeviceToDevice, s));
     } else {
         rc = ensure_host(ctx, &ctx->xfer, &ctx->xfer_bytes, (pl.n_local ? pl.n_local : 1) * sizeof(T));
         if (rc) return rc;
@@ -529,17 +547,22 @@ static int sample_sort_bx(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, T **d
             DSORT_HIP(ctx, hipMemcpyAsync(ctx->xfer, part, pl.n_local * sizeof(T), hipMemcpyDeviceToHost, s));
         rc = exch_wait(ctx, s, true, deadline, "key staging");
         if (rc) return rc;
+        // (the receive layout of the host buffer is the device one minus the partition: behind ->
+        // the other sources from n_local on, this rank's own buckets not shipped)
         std::vector<size_t> sc(P), sd(P), rcn(P), rd(P);
+        const uint64_t shift = behind ? pl.n_local : 0;
         for (int q = 0; q < P; ++q) {
-            sc[q] = scnt[q] * sizeof(T);
+            const bool self = behind && q == me;
+            sc[q] = self ? 0 : scnt[q] * sizeof(T);
             sd[q] = sdsp[q] * sizeof(T);
-            rcn[q] = rlen[q] * sizeof(T);
-            rd[q] = roff[q] * sizeof(T);
+            rcn[q] = self ? 0 : rlen[q] * sizeof(T);
+            rd[q] = self ? 0 : (rpos[q] - shift) * sizeof(T);
         }
         if (ctx->transport.alltoallv(ctx->transport.user, ctx->xfer, sc.data(), sd.data(), ctx->xfer2, rcn.data(),
                                      rd.data()))
             return set_err(ctx, DSORT_ECOMM, "host transport alltoallv (keys) failed");
-        if (nrecv) DSORT_HIP(ctx, hipMemcpyAsync(rb, ctx->xfer2, nrecv * sizeof(T), hipMemcpyHostToDevice, s));
+        const uint64_t nland = behind ? nrecv - rlen[me] : nrecv;
+        if (nland) DSORT_HIP(ctx, hipMemcpyAsync(rb + shift, ctx->xfer2, nland * sizeof(T), hipMemcpyHostToDevice, s));
     }
     if (ctx->ev_ok) {
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[6], s));
@@ -552,7 +575,7 @@ static int sample_sort_bx(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, T **d
     if (rc) return rc;
     // 5. the second level and the tile sort of this rank's buckets; kill stages 1 and 2
     T *outp = static_cast<T *>(ctx->recv2);
-    rc = bx_local_sort<T>(ctx, rb, outp, pl, hb_all.data(), roff.data(), s, true);
+    rc = bx_local_sort<T>(ctx, rb, outp, pl, hb_all.data(), base.data(), s, true);
     if (rc) return rc;
     ctx->last_stream = s;
     ctx->stats.keys_in = pl.n_local;

@@ -211,6 +211,8 @@ struct BxPlan {
     int P, me, Bl, Btot;
     uint64_t n_local, n_total;
     uint32_t s_max;                 // sample records per rank (the all-gather's unit)
+    uint64_t recv_room;             // keys the partition buffer holds past this rank's own: the
+                                    // other ranks' pieces land there (no copy of its own buckets)
     std::vector<uint64_t> n_of;     // keys of every rank
     std::vector<uint64_t> ioff;     // composite index of every rank's first key (prefix of n_of)
     std::vector<uint32_t> s_of;     // real samples of every rank (the rest of its s_max: padding)
@@ -222,17 +224,19 @@ bool bx_make_plan(const dsort_opts &opt, int P, int me, const uint64_t *n_of, in
 template <typename T>
 int bx_sample(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, BxSample *d_smp, hipStream_t s);
 // 2. the global splitters from every rank's records (d_all: P * s_max), then the first partition
-//    level of d_in into ctx->scratch (bucket-major, Btot buckets).  *hb = this rank's bucket starts
-//    (host, Btot + 1), *part = the partitioned keys.  Kill stage 0 fires here.
+//    level of d_in into ctx->scratch (bucket-major, Btot buckets; recv_room more keys fit behind
+//    them).  *hb = this rank's bucket starts (host, Btot + 1), *part = the partitioned keys.  Kill
+//    stage 0 fires here.
 template <typename T>
 int bx_partition(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, const BxSample *d_all, hipStream_t s, bool timed,
                  const uint64_t **hb, T **part);
-// 3. after the exchange: recv holds the pieces of this rank's buckets from every source s at
-//    roff[s] (source-major, each source's pieces in bucket order), hb_all[s * (Btot + 1) + g] =
-//    source s's bucket starts.  Sorts them into out (nrecv keys).  Kill stages 1 and 2 fire here.
+// 3. after the exchange: src holds the pieces of this rank's buckets from every source r, source
+//    r's in bucket order from src[base[r]] on; hb_all[r * (Btot + 1) + g] = source r's bucket
+//    starts.  Sorts them into out (nrecv keys; src holds at least nrecv keys: the second level's
+//    scratch).  Kill stages 1 and 2 fire here.
 template <typename T>
-int bx_local_sort(dsort_ctx *ctx, T *recv, T *out, const BxPlan &pl, const uint64_t *hb_all,
-                  const uint64_t *roff, hipStream_t s, bool timed);
+int bx_local_sort(dsort_ctx *ctx, T *src, T *out, const BxPlan &pl, const uint64_t *hb_all,
+                  const uint64_t *base, hipStream_t s, bool timed);
 
 }  // namespace dsort
 

@@ -165,6 +165,7 @@ __device__ __forceinline__ int sub_of(const Spl<T> *spl, const uint32_t *rng, T 
 // by (key, position).  A bucket whose ns is not a multiple of SB_RUN (DSORT_OPT_SUB_OVERSAMPLE
 // not a multiple of 4) samples single keys.
 constexpr uint32_t SB_RUN = 4;
+constexpr uint32_t SB_SMP_CH = 1024;  // chunks of a several-piece bucket staged in LDS for its sampling
 __host__ __device__ __forceinline__ uint32_t sample_run(const BInfo &b) { return b.single || b.ns % SB_RUN ? 1u : SB_RUN; }
 // (positions relative to the bucket: bucket_src_pos maps them to the source)
 __host__ __device__ __forceinline__ uint64_t sample_run_pos(const BInfo &b, uint32_t run, uint64_t r) {
@@ -196,8 +197,37 @@ __global__ void __launch_bounds__(SB_T) sb_sample_kernel(const T *__restrict__ s
 #pragma unroll
             for (uint32_t i = 0; i < SB_RUN; ++i) put((uint64_t)r * SB_RUN + i, key[i]);
         }
+    } else if (b.multi && b.c1 - b.c0 <= SB_SMP_CH) {
+        // a bucket of several pieces: its chunks' offsets in LDS, a run's chunk found there (a run
+        // crossing a chunk end takes its keys one by one)
+        __shared__ uint32_t cbo[SB_SMP_CH + 1];
+        __shared__ uint64_t cst[SB_SMP_CH];
+        const uint32_t nc = b.c1 - b.c0;
+        for (uint32_t c = threadIdx.x; c < nc; c += SB_T) {
+            const Chunk x = ch[b.c0 + c];
+            cbo[c] = x.boff;
+            cst[c] = x.start;
+        }
+        if (threadIdx.x == 0) cbo[nc] = b.len;
+        __syncthreads();
+        const uint32_t run = sample_run(b);
+        for (uint32_t r = threadIdx.x; r < b.ns / run; r += SB_T) {
+            const uint32_t p = (uint32_t)sample_run_pos(b, run, r);
+            uint32_t lo = 0, hi = nc - 1;  // the last chunk with boff <= p
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) >> 1;
+                if (cbo[mid] <= p) lo = mid;
+                else hi = mid - 1;
+            }
+            if (p + run <= cbo[lo + 1]) {
+                const T *q = src + cst[lo] + (p - cbo[lo]);
+                for (uint32_t i = 0; i < run; ++i) put((uint64_t)r * run + i, q[i]);
+            } else {
+                for (uint32_t i = 0; i < run; ++i) put((uint64_t)r * run + i, src[bucket_src_pos(b, ch, p + i)]);
+            }
+        }
     } else {
-        // (a run of a bucket of several pieces may cross a chunk: every key mapped on its own)
+        // (a run of a bucket of many pieces may cross a chunk: every key mapped on its own)
         for (uint32_t k = threadIdx.x; k < b.ns; k += SB_T) put(k, src[bucket_src_pos(b, ch, sample_pos(b, k))]);
     }
 }
@@ -402,11 +432,10 @@ struct Gather {
 // TileRefs.
 // LOCAL: a tile's room is tile - cpad * (the bucket's chunks): the gathering tile sort reads every
 // piece as the 16-byte vectors covering it, up to cpad extra slots per piece (gather_tile).
-// LOCAL also writes every tile's piece table (pieces, PS entries per tile, tiles below tcap;
-// chunk c's keys start at ch[c].start): the gathering tile sort then reads it together with the
-// tile record, one round trip before its key loads instead of two (record, then the prefix
-// tables).  Tile records past trec (the record array's size) are not written: the host sees
-// *ntiles > trec and takes the scatter path.
+// (LOCAL: sb_pieces_kernel then writes every tile's piece table: the gathering tile sort reads it
+// together with the tile record, one round trip before its key loads instead of two.)  Tile
+// records past trec (the record array's size) are not written: the host sees *ntiles > trec and
+// takes the scatter path.
 //
 // Split of sub-bucket j (LOCAL, above a tile): greedy over the bucket's chunks, a tile taking
 // consecutive chunks' pieces while its keys plus cpad per piece fit `full`.  Calls f(ca, cb, valid)
@@ -440,14 +469,11 @@ __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restric
                                                           uint32_t *__restrict__ offs, int tile, int align,
                                                           uint32_t mis, uint32_t cpad, void *__restrict__ tiles,
                                                           uint32_t *__restrict__ ntiles, Ovf *__restrict__ ovf,
-                                                          uint32_t *__restrict__ novf, uint2 *__restrict__ pieces,
-                                                          uint32_t PS, uint32_t tcap, const Chunk *__restrict__ ch,
-                                                          uint32_t trec) {
+                                                          uint32_t *__restrict__ novf, uint32_t trec) {
     __shared__ uint32_t wsum[SB_MAXS / 64];
     __shared__ uint32_t ss[SB_MAXS + 1];   // sub-bucket starts (positions)
     __shared__ uint16_t nxt[SB_MAXS];      // first sub-bucket after the tile starting at i
     __shared__ uint16_t chain[SB_MAXS];    // sub-buckets that start a tile
-    __shared__ uint16_t tix[SB_MAXS];      // LOCAL: tile of chain entry i, relative to tbase (0xFFFF: none)
     __shared__ uint32_t nchain, tbase;
     const BInfo b = bi[blockIdx.x];
     const int j = threadIdx.x;
@@ -536,7 +562,6 @@ __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restric
     const uint32_t tex = scan_excl_1024(nt, wsum, tall);
     if (j == 0) tbase = tall ? atomicAdd(ntiles, tall) : 0;
     __syncthreads();
-    if (LOCAL && j < nc) tix[j] = nt && !over ? (uint16_t)tex : (uint16_t)0xFFFF;
     if (j < nc && nt) {
         const uint32_t p = ss[i0], len = ss[i1] - p;
         uint32_t k = tbase + tex;
@@ -546,17 +571,13 @@ __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restric
                 if (k < trec)
                     gt[k] = GTile{p, b.start, len, blockIdx.x, i0, i1, b.c0, b.c1 - b.c0, b.nsub, len > room ? 1u : 0u};
             } else {
-                // the split tiles and their piece tables (this thread alone: a rare path)
+                // the split tiles (this thread alone: a rare path); sb_pieces_kernel writes their
+                // piece tables like any tile's
                 uint32_t q = p;
                 split_tiles(counts, SS, b.c0, b.c1, (int)i0, (uint32_t)full, cpad,
                             [&](uint32_t ca, uint32_t cb, uint32_t v) {
                                 if (k < trec)
                                     gt[k] = GTile{q, b.start, v, blockIdx.x, i0, i1, ca, cb - ca, b.nsub, 0u};
-                                for (uint32_t c = ca; c < cb && k < tcap; ++c) {
-                                    const uint32_t *pc = counts + (uint64_t)c * (SS + 1);
-                                    const uint32_t base = (uint32_t)ch[c].start;
-                                    pieces[(uint64_t)k * PS + (c - ca)] = make_uint2(base + pc[i0], base + pc[i1]);
-                                }
                                 q += v;
                                 ++k;
                             });
@@ -574,21 +595,24 @@ __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restric
             }
         }
     }
-    if constexpr (LOCAL) {
-        __syncthreads();
-        // the piece tables: a wave per tile, a lane per chunk (no division per entry)
-        const uint32_t nch = b.c1 - b.c0, lane = threadIdx.x & 63;
-        for (uint32_t t = threadIdx.x >> 6; t < (uint32_t)nc; t += blockDim.x >> 6) {
-            if (tix[t] == 0xFFFF) continue;
-            const uint32_t k = tbase + tix[t];
-            if (k >= tcap) continue;  // (the host sees ntiles > tcap and fails the sort)
-            const uint32_t a0 = chain[t], a1 = nxt[a0];
-            for (uint32_t c = lane; c < nch; c += 64) {
-                const uint32_t *pc = counts + (uint64_t)(b.c0 + c) * (SS + 1);
-                const uint32_t base = (uint32_t)ch[b.c0 + c].start;
-                pieces[(uint64_t)k * PS + c] = make_uint2(base + pc[a0], base + pc[a1]);
-            }
-        }
+}
+
+// The piece table of every gathered tile (LOCAL path): a wave per tile, a lane per chunk -- the
+// tile's chunks [c0, c0 + nch), its sub-buckets [j0, j1): chunk c's piece is [pref[c][j0],
+// pref[c][j1]) of the chunk.  (Inside sb_scan_kernel this was one workgroup per bucket walking all
+// its tiles: 270 us for 128 buckets of 4M keys, where every tile has ~280 pieces.)
+__global__ void __launch_bounds__(256) sb_pieces_kernel(const GTile *__restrict__ tiles,
+                                                        const uint32_t *__restrict__ ntiles,
+                                                        const Chunk *__restrict__ ch,
+                                                        const uint32_t *__restrict__ counts, int SS,
+                                                        uint2 *__restrict__ pieces, uint32_t PS, uint32_t tcap) {
+    const uint32_t k = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (k >= *ntiles || k >= tcap) return;  // (wave-uniform; the host fails a sort past tcap)
+    const GTile t = tiles[k];
+    for (uint32_t c = lane; c < t.nch; c += 64) {
+        const uint32_t *pc = counts + (uint64_t)(t.c0 + c) * (SS + 1);
+        const uint32_t base = (uint32_t)ch[t.c0 + c].start;
+        pieces[(uint64_t)k * PS + c] = make_uint2(base + pc[t.j0], base + pc[t.j1]);
     }
 }
 

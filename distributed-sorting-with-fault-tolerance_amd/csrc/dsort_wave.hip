@@ -1736,9 +1736,12 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         const uint64_t nc = bucket_chunks(b, CH);
         if (local && len) {
             PS = nc > PS ? (uint32_t)nc : PS;
-            // (+ 8: the split tiles of a rare sub-bucket above a tile; beyond the bound the sort
-            // takes the scatter path)
-            tcap += 2 * len / ((uint64_t)TILE - 2 * (ALIGN - 1) * nc) + 1 + 8;
+            // (+ 8: the split tiles of a rare sub-bucket above a tile -- sub-buckets split by chunks
+            // add up to one tile each beyond the bound; nominal sub-buckets above half a tile
+            // (DSORT_OPT_SUB_KEYS) make that every one of them.  Beyond the tables the sort takes
+            // the scatter path.)
+            const uint64_t room = (uint64_t)TILE - 2 * (ALIGN - 1) * nc;
+            tcap += 2 * len / room + 1 + 8 + (2 * m > room ? ns : 0);
         }
         bi[b] = BInfo{hb[b], nsmp, (uint32_t)len, (uint32_t)ns, ns > 1 ? (uint32_t)(ns * os) : 0u, (uint32_t)nch,
                       (uint32_t)(nch + nc), retry ? 1u : 0u, pm ? 1u : 0u};
@@ -1748,7 +1751,8 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         SS = (int)ns > SS ? (int)ns : SS;
     }
     SS = (SS + 63) & ~63;
-    const uint64_t tmax = nsubs + ceil_div(n, TILE) + (uint64_t)B;  // tiles, bound (sb_scan_kernel)
+    // tiles, bound (sb_scan_kernel); the local path's split tiles: tcap
+    const uint64_t tmax = std::max<uint64_t>(nsubs + ceil_div(n, TILE) + (uint64_t)B, local ? tcap : 0);
     size_t off = 0;
     auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
     const size_t o_bi = take(B * sizeof(BInfo)), o_ch = take(nch * sizeof(Chunk)), o_smp = take(nsmp * sizeof(T)),
@@ -1890,8 +1894,7 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
             if ((rc = stage_event(ctx, s, timed, 14))) return rc;
         }
         hipLaunchKernelGGL(sb_scan_kernel<true>, dim3((unsigned)B), dim3(SB_MAXS), 0, s, dbi, SS, cnt, nullptr, TILE, 1,
-                           0u, (uint32_t)(2 * (ALIGN - 1)), tt, num, ovf, num + 1, pcs, PS, (uint32_t)tcap,
-                           static_cast<const Chunk *>(dch), (uint32_t)tmax);
+                           0u, (uint32_t)(2 * (ALIGN - 1)), tt, num, ovf, num + 1, (uint32_t)tmax);
         DSORT_HIP(ctx, hipGetLastError());
         DSORT_HIP(ctx, hipMemcpyAsync(hn, num, 8, hipMemcpyDeviceToHost, s));
         DSORT_HIP(ctx, hipEventRecord(ctx->sub_ev, s));
@@ -1905,6 +1908,13 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         if (ntiles > tmax || ntiles > tcap) {
             ctx->stats.sub_scatter_fallback = 1;
             return sub_sort<T>(ctx, src, d_keys, n, hb, B, m, s, timed, false, pure, pure_done, bspl, true, pm);
+        }
+        // every tile's piece table
+        if (ntiles) {
+            hipLaunchKernelGGL(sb_pieces_kernel, dim3((unsigned)ceil_div(ntiles, 4)), dim3(256), 0, s,
+                               static_cast<const GTile *>(tt), num, static_cast<const Chunk *>(dch), cnt, SS, pcs, PS,
+                               (uint32_t)tcap);
+            DSORT_HIP(ctx, hipGetLastError());
         }
         fault_point(ctx, s, 1);  // second-level partition done
         ctx->stats.merge_passes = 0;
@@ -1939,7 +1949,7 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         DSORT_HIP(ctx, hipGetLastError());
     }
     hipLaunchKernelGGL(sb_scan_kernel<false>, dim3((unsigned)B), dim3(SB_MAXS), 0, s, dbi, SS, cnt, offs, TILE,
-                       (int)ALIGN, mis, 0u, tt, num, ovf, num + 1, nullptr, 0u, 0u, nullptr, (uint32_t)tmax);
+                       (int)ALIGN, mis, 0u, tt, num, ovf, num + 1, (uint32_t)tmax);
     DSORT_HIP(ctx, hipGetLastError());
     DSORT_HIP(ctx, hipMemcpyAsync(hn, num, 8, hipMemcpyDeviceToHost, s));
     DSORT_HIP(ctx, hipEventRecord(ctx->sub_ev, s));
@@ -2409,6 +2419,9 @@ bool bx_make_plan(const dsort_opts &opt, int P, int me, const uint64_t *n_of, in
         mx = (uint32_t)sr > mx ? (uint32_t)sr : mx;
     }
     pl.s_max = mx;
+    // the others' pieces behind this rank's partitioned keys: its expected share plus a margin (a
+    // larger receive takes a separate buffer and copies this rank's own buckets there)
+    pl.recv_room = P == 1 ? 0 : pl.n_total / P + pl.n_total / (4 * (uint64_t)P) + (1u << 16);
     return true;
 }
 
@@ -2454,7 +2467,7 @@ int bx_partition(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, const BxSample
     hipLaunchKernelGGL(bx_splitter_kernel<T>, dim3(1), dim3(bk::BK_MAXB), 0, s, sizeof(T) == 4 ? psrt : pcmp, pk, d_all,
                        S_real, pl.Btot, L.BP, L.spl);
     DSORT_HIP(ctx, hipGetLastError());
-    rc = ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, pl.n_local * sizeof(T) + 16, "sort scratch");
+    rc = ensure(ctx, &ctx->scratch, &ctx->scratch_bytes, (pl.n_local + pl.recv_room) * sizeof(T) + 16, "sort scratch");
     if (rc) return rc;
     T *scratch = static_cast<T *>(ctx->scratch);
     uint64_t *hb;
@@ -2478,7 +2491,7 @@ int bx_partition(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, const BxSample
 }
 
 template <typename T>
-int bx_local_sort(dsort_ctx *ctx, T *recv, T *out, const BxPlan &pl, const uint64_t *hb_all, const uint64_t *roff,
+int bx_local_sort(dsort_ctx *ctx, T *recv, T *out, const BxPlan &pl, const uint64_t *hb_all, const uint64_t *base,
                   hipStream_t s, bool timed) {
     using namespace wv;
     using C = typename bk::Comp<T>::C;
@@ -2498,7 +2511,7 @@ int bx_local_sort(dsort_ctx *ctx, T *recv, T *out, const BxPlan &pl, const uint6
         for (int r = 0; r < P; ++r) {
             const uint64_t *h = hb_all + (size_t)r * (Bt + 1);
             const uint64_t len = h[g + 1] - h[g];
-            if (len) pm.p.push_back(SrcPiece{roff[r] + (h[g] - h[g0]), len});
+            if (len) pm.p.push_back(SrcPiece{base[r] + (h[g] - h[g0]), len});
             tot += len;
         }
         hbo[j + 1] = hbo[j] + tot;

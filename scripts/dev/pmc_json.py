@@ -35,9 +35,16 @@ def per_launch(tag):
 
 t32 = sys.argv[2] if len(sys.argv) > 2 else "i32_"
 t64 = sys.argv[3] if len(sys.argv) > 3 else "i64_"
+import hashlib  # noqa: E402
+import os  # noqa: E402
+
+# the build the counters were taken on (bench.py uses the table as measured only for this build)
+LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..",
+                   "distributed-sorting-with-fault-tolerance_amd", "lib", "libdsort.so")
 doc = {"source": "rocprofv3 --pmc (separate passes, scripts/dev/pmc_sub.sh) over scripts/dev/ktime.py --reps 1, "
                  "2^30 keys; converted by scripts/dev/pmc_json.py",
-       "keys": 1 << 30, "key_bytes": 4, "kernels": per_launch(t32),
+       "lib_sha256": hashlib.sha256(open(LIB, "rb").read()).hexdigest(),
+       "keys": 1 << 30, "key_bytes": 4, "dist": "uniform", "kernels": per_launch(t32),
        "int64": {"keys": 1 << 30, "key_bytes": 8, "dist": "zipf", "kernels": per_launch(t64)}}
 json.dump(doc, open(sys.argv[1] if len(sys.argv) > 1 else "profiles/r2_pmc_traffic.json", "w"), indent=1)
 for t, ks in (("int32", doc["kernels"]), ("int64", doc["int64"]["kernels"])):
