@@ -387,7 +387,7 @@ static int exch_wait(dsort_ctx *ctx, hipStream_t s, bool with_stream, double dea
             return set_err(ctx, DSORT_ETIMEOUT, std::string(what) + ": no progress before the deadline "
                                                     "(DSORT_OPT_COMM_TIMEOUT_MS); communicator aborted");
         }
-        usleep(20);
+        usleep(4);  // (a few us: a wait on the critical path of every exchange step)
     }
 }
 
@@ -569,13 +569,19 @@ static int sample_sort_bx(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, T **d
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[3], s));
         ctx->ev_mask |= 64u | 8u;
     }
-    // the receives must have landed before the second level: its host waits (the tile count) would
-    // block on a stream a dead peer never completes -- this wait polls the abort flag and deadline
-    rc = exch_wait(ctx, s, true, deadline, "key all-to-all", ctx->opt.test_hold_exchange != 0);
-    if (rc) return rc;
-    // 5. the second level and the tile sort of this rank's buckets; kill stages 1 and 2
+    // 5. the second level and the tile sort of this rank's buckets, queued behind the receives on
+    //    the stream while the keys are in flight (the host builds and uploads its tables meanwhile);
+    //    its host waits poll the abort flag and the deadline, as a dead peer never completes the
+    //    stream.  Kill stages 1 and 2.
     T *outp = static_cast<T *>(ctx->recv2);
+    ctx->poll_waits = !host_tx;
+    ctx->poll_deadline = deadline;
     rc = bx_local_sort<T>(ctx, rb, outp, pl, hb_all.data(), base.data(), s, true);
+    ctx->poll_waits = false;
+    if (rc == DSORT_ECOMM || rc == DSORT_ETIMEOUT) abort_comm_locked(ctx);
+    if (rc) return rc;
+    // the receives have landed (and the test hold, DSORT_OPT_TEST_HOLD_EXCHANGE, is released)
+    rc = exch_wait(ctx, s, true, deadline, "key all-to-all", ctx->opt.test_hold_exchange != 0);
     if (rc) return rc;
     ctx->last_stream = s;
     ctx->stats.keys_in = pl.n_local;

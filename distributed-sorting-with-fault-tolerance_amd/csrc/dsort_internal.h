@@ -138,6 +138,11 @@ struct dsort_ctx {
     size_t bxs_bytes = 0;
     int ev_done = 2;        // the stage event a sort's second level records at its end (the bucket
                             // exchange records its own end as event 4)
+    // The bucket exchange runs its second level while the keys are still in flight: the sort's
+    // host waits then poll (abort flag, deadline) instead of blocking on a stream a dead peer
+    // would never complete (sync_event / sync_stream, dsort_wave.hip).
+    bool poll_waits = false;
+    double poll_deadline = 0.0;  // ms on the CLOCK_MONOTONIC scale, 0 = none
     // stage timing
     hipEvent_t ev[15] = {};  // 0 start, 1 tile sort done, 2 local sort done, 3 exchange done,
                              // 4 final merge done, 5/6 around the key all-to-all, 7/8 around the
@@ -193,6 +198,10 @@ void fault_point(dsort_ctx *ctx, hipStream_t s, int stage);
 // Kill points of a top-level sort of n keys of key_bytes bytes under `opt` (the bucketed path
 // without the second level has data-dependent merge passes: the guaranteed minimum).
 int sort_stages(const dsort_opts &opt, uint64_t n, int key_bytes);
+// Host waits of the sort: blocking, or (ctx->poll_waits) polling with the abort flag and deadline
+// (DSORT_ECOMM / DSORT_ETIMEOUT).
+int sync_event(dsort_ctx *ctx, hipEvent_t e, const char *what);
+int sync_stream(dsort_ctx *ctx, hipStream_t s, const char *what);
 // Largest log2 fan-in of one merge pass: the option, else the key type's default.
 int max_logf(const dsort_opts &opt, int type_default, int type_cap);
 

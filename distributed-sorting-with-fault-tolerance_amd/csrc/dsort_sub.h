@@ -432,10 +432,12 @@ struct Gather {
 // TileRefs.
 // LOCAL: a tile's room is tile - cpad * (the bucket's chunks): the gathering tile sort reads every
 // piece as the 16-byte vectors covering it, up to cpad extra slots per piece (gather_tile).
-// (LOCAL: sb_pieces_kernel then writes every tile's piece table: the gathering tile sort reads it
-// together with the tile record, one round trip before its key loads instead of two.)  Tile
-// records past trec (the record array's size) are not written: the host sees *ntiles > trec and
-// takes the scatter path.
+// LOCAL: every tile's piece table (PS entries per tile, tiles below tcap) -- here when `pieces` is
+// given (many buckets: the workgroups fill the chip), else by sb_pieces_kernel afterwards (few large
+// buckets, e.g. 128 of 4M keys: a workgroup per bucket would walk ~280 tiles of ~280 pieces); the
+// gathering tile sort reads it together with the tile record, one round trip before its key loads
+// instead of two.  Tile records past trec (the record array's size) are not written: the host sees
+// *ntiles > trec and takes the scatter path.
 //
 // Split of sub-bucket j (LOCAL, above a tile): greedy over the bucket's chunks, a tile taking
 // consecutive chunks' pieces while its keys plus cpad per piece fit `full`.  Calls f(ca, cb, valid)
@@ -469,11 +471,14 @@ __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restric
                                                           uint32_t *__restrict__ offs, int tile, int align,
                                                           uint32_t mis, uint32_t cpad, void *__restrict__ tiles,
                                                           uint32_t *__restrict__ ntiles, Ovf *__restrict__ ovf,
-                                                          uint32_t *__restrict__ novf, uint32_t trec) {
+                                                          uint32_t *__restrict__ novf, uint32_t trec,
+                                                          const Chunk *__restrict__ ch, uint2 *__restrict__ pieces,
+                                                          uint32_t PS, uint32_t tcap) {
     __shared__ uint32_t wsum[SB_MAXS / 64];
     __shared__ uint32_t ss[SB_MAXS + 1];   // sub-bucket starts (positions)
     __shared__ uint16_t nxt[SB_MAXS];      // first sub-bucket after the tile starting at i
     __shared__ uint16_t chain[SB_MAXS];    // sub-buckets that start a tile
+    __shared__ uint16_t tix[SB_MAXS];      // LOCAL: tile of chain entry i, relative to tbase (0xFFFF: none)
     __shared__ uint32_t nchain, tbase;
     const BInfo b = bi[blockIdx.x];
     const int j = threadIdx.x;
@@ -562,6 +567,7 @@ __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restric
     const uint32_t tex = scan_excl_1024(nt, wsum, tall);
     if (j == 0) tbase = tall ? atomicAdd(ntiles, tall) : 0;
     __syncthreads();
+    if (LOCAL && j < nc) tix[j] = nt && !over ? (uint16_t)tex : (uint16_t)0xFFFF;
     if (j < nc && nt) {
         const uint32_t p = ss[i0], len = ss[i1] - p;
         uint32_t k = tbase + tex;
@@ -578,6 +584,11 @@ __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restric
                             [&](uint32_t ca, uint32_t cb, uint32_t v) {
                                 if (k < trec)
                                     gt[k] = GTile{q, b.start, v, blockIdx.x, i0, i1, ca, cb - ca, b.nsub, 0u};
+                                for (uint32_t c = ca; pieces && c < cb && k < tcap; ++c) {
+                                    const uint32_t *pc = counts + (uint64_t)c * (SS + 1);
+                                    const uint32_t base = (uint32_t)ch[c].start;
+                                    pieces[(uint64_t)k * PS + (c - ca)] = make_uint2(base + pc[i0], base + pc[i1]);
+                                }
                                 q += v;
                                 ++k;
                             });
@@ -592,6 +603,22 @@ __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restric
                 for (uint32_t q = room; q < len; q += (uint32_t)tile)
                     tt[k++] = bk::TileRef{(uint64_t)p + q, len - q < (uint32_t)tile ? len - q : (uint32_t)tile, 0};
                 ovf[atomicAdd(novf, 1u)] = Ovf{p, len, 0u, 0u};
+            }
+        }
+    }
+    if (LOCAL && pieces) {
+        __syncthreads();
+        // the piece tables: a wave per tile, a lane per chunk (no division per entry)
+        const uint32_t nch = b.c1 - b.c0, lane = threadIdx.x & 63;
+        for (uint32_t t = threadIdx.x >> 6; t < (uint32_t)nc; t += blockDim.x >> 6) {
+            if (tix[t] == 0xFFFF) continue;
+            const uint32_t k = tbase + tix[t];
+            if (k >= tcap) continue;  // (the host sees ntiles > tcap and fails the sort)
+            const uint32_t a0 = chain[t], a1 = nxt[a0];
+            for (uint32_t c = lane; c < nch; c += 64) {
+                const uint32_t *pc = counts + (uint64_t)(b.c0 + c) * (SS + 1);
+                const uint32_t base = (uint32_t)ch[b.c0 + c].start;
+                pieces[(uint64_t)k * PS + c] = make_uint2(base + pc[a0], base + pc[a1]);
             }
         }
     }

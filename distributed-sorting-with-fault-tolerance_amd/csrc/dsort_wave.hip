@@ -35,6 +35,8 @@
 
 #include <algorithm>
 #include <climits>
+#include <ctime>
+#include <unistd.h>
 #include <csignal>
 #include <cstdlib>
 #include <cstring>
@@ -1636,12 +1638,12 @@ static int merge_split_subbuckets(dsort_ctx *ctx, const sb::Ovf *d_ovf, uint32_t
     using namespace sb;
     std::vector<Ovf> ov(novf);
     DSORT_HIP(ctx, hipMemcpyAsync(ov.data(), d_ovf, novf * sizeof(Ovf), hipMemcpyDeviceToHost, s));
-    DSORT_HIP(ctx, hipStreamSynchronize(s));
+    if (int rc_ = sync_stream(ctx, s, "sort stream")) return rc_;
     int lv = 0;
     for (const Ovf &o : ov) {
         std::vector<GTile> gt(o.nt);
         DSORT_HIP(ctx, hipMemcpyAsync(gt.data(), d_tiles + o.tile0, o.nt * sizeof(GTile), hipMemcpyDeviceToHost, s));
-        DSORT_HIP(ctx, hipStreamSynchronize(s));
+        if (int rc_ = sync_stream(ctx, s, "sort stream")) return rc_;
         std::vector<size_t> runs(o.nt);
         uint64_t tot = 0;
         for (uint32_t i = 0; i < o.nt; ++i) {
@@ -1793,7 +1795,7 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
     }
     if (!ctx->sub_ev && hipEventCreateWithFlags(&ctx->sub_ev, hipEventDisableTiming) != hipSuccess)
         return set_err(ctx, DSORT_EHIP, "hipEventCreate");
-    DSORT_HIP(ctx, hipEventSynchronize(ctx->sub_ev));  // the previous call's read-back is done with the staging
+    if (int rc_ = sync_event(ctx, ctx->sub_ev, "tile count")) return rc_;  // the previous call's read-back is done with the staging
     char *h = static_cast<char *>(ctx->sub_host);
     std::memcpy(h, bi.data(), B * sizeof(BInfo));
     Chunk *hc = reinterpret_cast<Chunk *>(h + h_ch);
@@ -1893,14 +1895,17 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
             DSORT_HIP(ctx, hipGetLastError());
             if ((rc = stage_event(ctx, s, timed, 14))) return rc;
         }
+        // (the piece tables inside the scan with many buckets; with few, a kernel of their own)
+        const bool pieces_in_scan = B >= 256;
         hipLaunchKernelGGL(sb_scan_kernel<true>, dim3((unsigned)B), dim3(SB_MAXS), 0, s, dbi, SS, cnt, nullptr, TILE, 1,
-                           0u, (uint32_t)(2 * (ALIGN - 1)), tt, num, ovf, num + 1, (uint32_t)tmax);
+                           0u, (uint32_t)(2 * (ALIGN - 1)), tt, num, ovf, num + 1, (uint32_t)tmax,
+                           static_cast<const Chunk *>(dch), pieces_in_scan ? pcs : nullptr, PS, (uint32_t)tcap);
         DSORT_HIP(ctx, hipGetLastError());
         DSORT_HIP(ctx, hipMemcpyAsync(hn, num, 8, hipMemcpyDeviceToHost, s));
         DSORT_HIP(ctx, hipEventRecord(ctx->sub_ev, s));
         // (the tile count sizes the grid: a grid at its bound, 9x the tiles at 2^30 int32, cost
         // more in empty workgroups than this wait -- measured 10.6 vs 10.1 ms)
-        DSORT_HIP(ctx, hipEventSynchronize(ctx->sub_ev));
+        if (int rc_ = sync_event(ctx, ctx->sub_ev, "tile count")) return rc_;
         const uint32_t ntiles = hn[0], novf = hn[1];
         // Beyond the tile tables (only when many sub-buckets were split): the scatter path over the
         // partitioned chunks -- its sample takes single keys, since a run of adjacent keys now lies
@@ -1910,7 +1915,7 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
             return sub_sort<T>(ctx, src, d_keys, n, hb, B, m, s, timed, false, pure, pure_done, bspl, true, pm);
         }
         // every tile's piece table
-        if (ntiles) {
+        if (ntiles && !pieces_in_scan) {
             hipLaunchKernelGGL(sb_pieces_kernel, dim3((unsigned)ceil_div(ntiles, 4)), dim3(256), 0, s,
                                static_cast<const GTile *>(tt), num, static_cast<const Chunk *>(dch), cnt, SS, pcs, PS,
                                (uint32_t)tcap);
@@ -1949,7 +1954,7 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         DSORT_HIP(ctx, hipGetLastError());
     }
     hipLaunchKernelGGL(sb_scan_kernel<false>, dim3((unsigned)B), dim3(SB_MAXS), 0, s, dbi, SS, cnt, offs, TILE,
-                       (int)ALIGN, mis, 0u, tt, num, ovf, num + 1, (uint32_t)tmax);
+                       (int)ALIGN, mis, 0u, tt, num, ovf, num + 1, (uint32_t)tmax, nullptr, nullptr, 0u, 0u);
     DSORT_HIP(ctx, hipGetLastError());
     DSORT_HIP(ctx, hipMemcpyAsync(hn, num, 8, hipMemcpyDeviceToHost, s));
     DSORT_HIP(ctx, hipEventRecord(ctx->sub_ev, s));
@@ -1960,7 +1965,7 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         DSORT_HIP(ctx, hipGetLastError());
         if ((rc = stage_event(ctx, s, timed, 14))) return rc;
     }
-    DSORT_HIP(ctx, hipEventSynchronize(ctx->sub_ev));
+    if (int rc_ = sync_event(ctx, ctx->sub_ev, "tile count")) return rc_;
     const uint32_t ntiles = hn[0], novf = hn[1];
     if (ntiles > tmax || novf > nsubs) return set_err(ctx, DSORT_EHIP, "sub-bucket packing overflow");
     fault_point(ctx, s, 1);  // second-level partition done
@@ -1979,7 +1984,7 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
     if (novf) {
         std::vector<Ovf> ov(novf);
         DSORT_HIP(ctx, hipMemcpyAsync(ov.data(), ovf, novf * sizeof(Ovf), hipMemcpyDeviceToHost, s));
-        DSORT_HIP(ctx, hipStreamSynchronize(s));
+        if (int rc_ = sync_stream(ctx, s, "sort stream")) return rc_;
         T *tmp = src;
         int lv = 0;
         for (const Ovf &o : ov) {
@@ -2099,7 +2104,7 @@ static int first_level(dsort_ctx *ctx, const T *d_in, uint64_t n, uint64_t ioff,
     DSORT_HIP(ctx, hipGetLastError());
     if ((rc = stage_event(ctx, s, timed, 12))) return rc;
     fault_point(ctx, s, 0);  // first-level partition done
-    DSORT_HIP(ctx, hipEventSynchronize(ctx->bucket_ev));
+    if (int rc_ = sync_event(ctx, ctx->bucket_ev, "bucket starts")) return rc_;
     if (hb[B] != n) return set_err(ctx, DSORT_EHIP, "bucket partition lost keys");
     return DSORT_OK;
 }
@@ -2287,7 +2292,7 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
     if (passes > 0) {
         const size_t gbytes = groups.size() * sizeof(GroupK), tbytes = tgroup.size() * sizeof(uint32_t);
         const size_t tb_off = (gbytes + 255) & ~(size_t)255;
-        if (ctx->groups_ev_pending) DSORT_HIP(ctx, hipEventSynchronize(ctx->groups_ev));
+        if (ctx->groups_ev_pending) { if (int rc_ = sync_event(ctx, ctx->groups_ev, "group table")) return rc_; }
         ctx->groups_ev_pending = false;
         if (ctx->groups_host_bytes < tb_off + tbytes) {
             if (ctx->groups_host) (void)hipHostFree(ctx->groups_host);
@@ -2481,7 +2486,7 @@ int bx_partition(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, const BxSample
         hspl = reinterpret_cast<C *>(hb + bk::BK_MAXB + 1);
         for (int b = 0; b <= pl.Btot; ++b) hb[b] = 0;
         DSORT_HIP(ctx, hipMemcpyAsync(hspl, L.spl, (size_t)(pl.Btot - 1) * sizeof(C), hipMemcpyDeviceToHost, s));
-        DSORT_HIP(ctx, hipStreamSynchronize(s));
+        if (int rc_ = sync_stream(ctx, s, "sort stream")) return rc_;
         fault_point(ctx, s, 0);
     }
     if ((rc = stage_event(ctx, s, timed, 2))) return rc;  // the local part done: the exchange starts
@@ -2673,7 +2678,7 @@ static int wave_merge(dsort_ctx *ctx, const T *d_in, const size_t *lens, int k, 
         const int logf = ceil_log2((uint64_t)per) < 1 ? 1 : ceil_log2((uint64_t)per);
         const int ng = (nr + MAXF - 1) / MAXF;
         const size_t gbytes = (size_t)ng * sizeof(GroupK);
-        if (ctx->groups_ev_pending) DSORT_HIP(ctx, hipEventSynchronize(ctx->groups_ev));
+        if (ctx->groups_ev_pending) { if (int rc_ = sync_event(ctx, ctx->groups_ev, "group table")) return rc_; }
         ctx->groups_ev_pending = false;
         if (ctx->groups_host_bytes < gbytes) {
             if (ctx->groups_host) (void)hipHostFree(ctx->groups_host);
@@ -2741,6 +2746,38 @@ extern "C" int dsort_debug_sbstamps(void *host, size_t bytes) {
 // from different runs are emitted lower run first, like the reference's `<=` (client.c:152) and
 // lowest-index-wins argmin (server.c:504) -- unobservable for keys-only data.
 // ------------------------------------------------------------------------------------------
+static double mono_ms() {
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+}
+static int poll_done(dsort_ctx *ctx, hipError_t (*query)(void *), void *h, const char *what) {
+    for (;;) {
+        const hipError_t q = query(h);
+        if (q == hipSuccess) return DSORT_OK;
+        if (q != hipErrorNotReady) return hip_err(ctx, q, what);
+        if (ctx->abort_req.load())
+            return set_err(ctx, DSORT_ECOMM, std::string(what) + ": aborted by dsort_comm_abort (keys in flight)");
+        if (ctx->poll_deadline > 0 && mono_ms() > ctx->poll_deadline)
+            return set_err(ctx, DSORT_ETIMEOUT, std::string(what) + ": no progress before the deadline (keys in flight)");
+        usleep(4);
+    }
+}
+int sync_event(dsort_ctx *ctx, hipEvent_t e, const char *what) {
+    if (!ctx->poll_waits) {
+        DSORT_HIP(ctx, hipEventSynchronize(e));
+        return DSORT_OK;
+    }
+    return poll_done(ctx, [](void *h) { return hipEventQuery(static_cast<hipEvent_t>(h)); }, e, what);
+}
+int sync_stream(dsort_ctx *ctx, hipStream_t s, const char *what) {
+    if (!ctx->poll_waits) {
+        DSORT_HIP(ctx, hipStreamSynchronize(s));
+        return DSORT_OK;
+    }
+    return poll_done(ctx, [](void *h) { return hipStreamQuery(static_cast<hipStream_t>(h)); }, s, what);
+}
+
 int max_logf(const dsort_opts &opt, int type_default, int type_cap) {
     const int64_t o = opt.max_logf;
     const int x = o < 0 ? type_default : (int)o;

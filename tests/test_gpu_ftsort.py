@@ -1,8 +1,10 @@
 """Fault-tolerant multi-GPU sample sort (BASELINE config C5) on the 1-GPU box, through the C master
 (dsort_master --mode samplesort) and the C GPU workers with the real libdsort.so: the workers share
 cuda:0, so they exchange through the master (relay transport; RCCL needs one GPU per rank).  One
-worker SIGKILLs itself in the middle of its local sort (DSORT_OPT_KILL_AFTER_PASS, after merge
-pass 0) or inside the exchange (DSORT_OPT_KILL_IN_EXCHANGE) and the survivors must still produce
+worker SIGKILLs itself in the middle of its sort (DSORT_OPT_KILL_AFTER_STAGE: after the first
+partition level of its chunk, before the exchange, or after the second level of its received
+buckets; below 2^22 keys per worker after its tile sort) or inside the exchange
+(DSORT_OPT_KILL_IN_EXCHANGE) and the survivors must still produce
 the sorted input, the dead worker's chunk reassigned from the master's pinned replica as in
 server.c:368-391.  Verified bit-exactly (order, multiset fingerprint, slice boundaries; --output
 against numpy)."""
@@ -91,3 +93,22 @@ def test_single_rank_rccl_through_c_master():
 
     r = ftsort.run_master(1, 1_000_003, transport="rccl", devices=[0], timeout_s=180)
     assert r["ok"], r
+
+
+def test_bench_fault_line_reports_recovery():
+    """bench.py's config-C5 line (--kill-rank) through the C master on this box's shared GPU: a
+    fault-free run and a run with worker 1 killed mid-sort (after its first partition level), the
+    line carrying the recovery time, when the master saw the death, the survivors' rebuild time and
+    the verification (server.c:358-395's reassignment, reported)."""
+    import json
+    import subprocess
+    import sys as _sys
+    p = subprocess.run([_sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "3", "--keys", str(3 << 25),
+                        "--kill-rank", "1"], capture_output=True, text=True, timeout=240,
+                       env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["verified"] is True and line["unit"] == "ms"
+    for k in ("fault_seen_by_master_ms", "survivors_notified_ms", "rebuild_ms", "fault_free_ms", "fault_ms"):
+        assert line[k] is not None, k
+    assert line["fault_ms"] > 0 and line["fault_free_ms"] > 0
