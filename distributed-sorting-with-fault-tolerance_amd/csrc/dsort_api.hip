@@ -1034,6 +1034,18 @@ int dsort_sort_stages(const dsort_ctx *ctx, size_t n, int key_bytes, int *stages
     return DSORT_OK;
 }
 
+int dsort_sample_sort_stages(const dsort_ctx *ctx, size_t n_total, int nranks, int rank, int key_bytes,
+                             int *stages) {
+    if (!stages || nranks < 1 || rank < 0 || rank >= nranks || (key_bytes != 4 && key_bytes != 8)) return DSORT_EINVAL;
+    static const dsort_opts defaults{};
+    const dsort_opts &o = ctx ? ctx->opt : defaults;
+    std::vector<uint64_t> n_of(nranks);
+    for (int r = 0; r < nranks; ++r) n_of[r] = n_total / nranks + ((uint64_t)r < n_total % nranks ? 1 : 0);
+    BxPlan pl;
+    *stages = bx_make_plan(o, nranks, rank, n_of.data(), key_bytes, pl) ? 3 : sort_stages(o, n_of[rank], key_bytes);
+    return DSORT_OK;
+}
+
 int dsort_sort_i32(dsort_ctx *ctx, int32_t *keys, size_t n) { return sort_host<int32_t>(ctx, keys, n); }
 int dsort_sort_i64(dsort_ctx *ctx, int64_t *keys, size_t n) { return sort_host<int64_t>(ctx, keys, n); }
 

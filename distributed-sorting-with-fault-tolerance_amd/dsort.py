@@ -27,7 +27,7 @@ ERRORS = {-1: "EINVAL", -2: "ENOMEM", -3: "EHIP", -4: "ECOMM", -5: "ENODEV", -6:
 # every symbol include/dsort.h declares (checked by tests/test_abi.py)
 EXPORTS = [
     "dsort_init", "dsort_finalize", "dsort_last_error", "dsort_version", "dsort_get_stats",
-    "dsort_synchronize", "dsort_set_option", "dsort_get_option", "dsort_sort_stages", "dsort_sort_i32", "dsort_sort_i64", "dsort_sort_dev_i32",
+    "dsort_synchronize", "dsort_set_option", "dsort_get_option", "dsort_sort_stages", "dsort_sample_sort_stages", "dsort_sort_i32", "dsort_sort_i64", "dsort_sort_dev_i32",
     "dsort_sort_dev_i64", "dsort_sort_dev_copy_i32", "dsort_sort_dev_copy_i64",
     "dsort_merge_i32", "dsort_merge_i64", "dsort_merge_dev_i32", "dsort_merge_dev_i64",
     "dsort_comm_unique_id", "dsort_comm_init", "dsort_comm_init_transport", "dsort_comm_abort",
@@ -161,6 +161,8 @@ def load():
         "dsort_set_option": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int64]),
         "dsort_get_option": (ctypes.c_int, [P, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]),
         "dsort_sort_stages": (ctypes.c_int, [P, SZ, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
+        "dsort_sample_sort_stages": (ctypes.c_int, [P, SZ, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                    ctypes.POINTER(ctypes.c_int)]),
         "dsort_sort_i32": (ctypes.c_int, [P, P, SZ]),
         "dsort_sort_i64": (ctypes.c_int, [P, P, SZ]),
         "dsort_sort_dev_i32": (ctypes.c_int, [P, P, SZ, P]),

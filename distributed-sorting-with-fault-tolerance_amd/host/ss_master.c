@@ -237,8 +237,9 @@ int samplesort_master(int argc, char **argv, const char *argv0) {
         const uint64_t q = o.keys / (uint64_t)o.n, rm = o.keys % (uint64_t)o.n;
         const uint64_t len = q + ((uint64_t)o.kill_rank < rm ? 1 : 0);
         int stages = 0;
-        if (dsort_sort_stages(NULL, len, o.key_bytes, &stages) || o.kill_after_pass >= stages) {
-            fprintf(stderr, "master: --kill-after-stage %d: the local sort of worker %d (%llu keys) has %d stages "
+        if (dsort_sample_sort_stages(NULL, o.keys, o.n, o.kill_rank, o.key_bytes, &stages) ||
+            o.kill_after_pass >= stages) {
+            fprintf(stderr, "master: --kill-after-stage %d: the sort of worker %d (%llu keys) has %d stages "
                     "(kill points 0..%d)\n", o.kill_after_pass, o.kill_rank, (unsigned long long)len, stages,
                     stages - 1);
             free(parsed);

@@ -143,6 +143,12 @@ int dsort_get_option(const dsort_ctx *ctx, int option, int64_t *value);
  * DSORT_OPT_SUB_KEYS = 0 the bucketed sort's merge passes depend on the data: the guaranteed
  * minimum. */
 int dsort_sort_stages(const dsort_ctx *ctx, size_t n, int key_bytes, int *stages);
+/* ABI 4: kill points of rank `rank`'s part of a sample sort of n_total keys over nranks ranks in the
+ * reference's equal contiguous chunks (server.c:185-216): the bucket exchange's three stages (first
+ * partition level, second level of the received buckets, their tile sort), or below 2^22 keys per
+ * rank those of its local sort (dsort_sort_stages). */
+int dsort_sample_sort_stages(const dsort_ctx *ctx, size_t n_total, int nranks, int rank, int key_bytes,
+                             int *stages);
 
 /* Drop-in for `merge_sort(chunk, 0, n-1)` (client.c:117 -> client.c:166-173): sorts the
  * caller-owned HOST buffer in place, ascending.  Copies to HBM, sorts on the GPU, copies

@@ -151,6 +151,10 @@ int dsort_sort_stages(const dsort_ctx *ctx, size_t n, int key_bytes, int *stages
     *stages = n < 2 ? 0 : 3;
     return DSORT_OK;
 }
+int dsort_sample_sort_stages(const dsort_ctx *ctx, size_t n_total, int nranks, int rank, int key_bytes, int *stages) {
+    if (nranks < 1 || rank < 0 || rank >= nranks) return DSORT_EINVAL;
+    return dsort_sort_stages(ctx, n_total / nranks + ((size_t)rank < n_total % nranks), key_bytes, stages);
+}
 #define DOUBLE_SORT(T, SFX)                                                                          \
     int dsort_sort_dev_copy_##SFX(dsort_ctx *ctx, const T *in, T *out, size_t n, void *s) {            \
         (void)ctx; (void)s;                                                                          \

@@ -111,3 +111,13 @@ def test_sort_stages(dsort_mod):
     assert stages((1 << 25) - 1, 4) == 1 + 3       # 2048 tiles: 11 bits in 3 passes
     m = ctypes.c_int()
     assert lib.dsort_sort_stages(None, 100, 2, ctypes.byref(m)) == -1
+
+    def ss_stages(n, p, r=0, w=4):
+        m = ctypes.c_int()
+        assert lib.dsort_sample_sort_stages(None, n, p, r, w, ctypes.byref(m)) == 0
+        return m.value
+
+    # the bucket exchange from 2^22 keys per rank: three stages; below, the local sort's
+    assert ss_stages(1 << 32, 8) == 3 and ss_stages(3 << 22, 3, 2) == 3 and ss_stages(1 << 30, 1) == 3
+    assert ss_stages(1 << 20, 4) == stages(1 << 18, 4)
+    assert lib.dsort_sample_sort_stages(None, 100, 2, 2, 4, ctypes.byref(m)) == -1
