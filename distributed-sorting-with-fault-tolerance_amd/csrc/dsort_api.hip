@@ -439,6 +439,16 @@ static int allgather_u64(dsort_ctx *ctx, const uint64_t *src, size_t count, uint
     return DSORT_OK;
 }
 
+// The context's comm stream (the bucket exchange's sends and receives) and its events.
+static int comm_stream(dsort_ctx *ctx) {
+    if (!ctx->xs && hipStreamCreateWithFlags(&ctx->xs, hipStreamNonBlocking) != hipSuccess)
+        return set_err(ctx, DSORT_EHIP, "hipStreamCreate (comm stream)");
+    for (auto &e : ctx->xev)
+        if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+            return set_err(ctx, DSORT_EHIP, "hipEventCreate (comm stream)");
+    return DSORT_OK;
+}
+
 // The bucket exchange (dsort_internal.h): samples of the unsorted keys from every
 // rank -> the same Btot global splitters everywhere -> this rank's keys partitioned into the Btot
 // buckets (the first level of the one-GPU sort) -> buckets [q Bl, (q+1) Bl) to rank q (RCCL
@@ -485,33 +495,42 @@ static int sample_sort_bx(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, T **d
         rc = allgather_u64(ctx, mine_hb.data(), (size_t)Bt + 1, hb_all.data(), s, deadline, "bucket starts all-gather");
         if (rc) return rc;
     }
-    std::vector<size_t> scnt(P), sdsp(P), rlen(P);
-    std::vector<uint64_t> roff(P + 1, 0);
+    // The exchange in W waves of this rank's buckets (RCCL, two or more buckets: W = 2): wave w ships
+    // buckets [jb[w], jb[w+1]) of every rank's range, and the second level of wave 0 runs while wave
+    // 1's keys are on the links (the sends and receives go on the comm stream; the sort stream waits
+    // for each wave's event).
+    const int W = (!host_tx && P > 1 && Bl >= 2) ? 2 : 1;
+    const int jb[3] = {0, W == 2 ? Bl / 2 : Bl, Bl};
+    const uint64_t *hme = hb_all.data() + (size_t)me * (Bt + 1);
+    auto hof = [&](int r) { return hb_all.data() + (size_t)r * (Bt + 1); };
+    std::vector<uint64_t> rlen(P, 0);
     uint64_t sent = 0;
     for (int q = 0; q < P; ++q) {
-        sdsp[q] = hb_all[(size_t)me * (Bt + 1) + (size_t)q * Bl];
-        scnt[q] = hb_all[(size_t)me * (Bt + 1) + (size_t)(q + 1) * Bl] - sdsp[q];
-        if (q != me) sent += scnt[q];
-        const uint64_t *h = hb_all.data() + (size_t)q * (Bt + 1);
-        rlen[q] = h[(size_t)(me + 1) * Bl] - h[(size_t)me * Bl];
-        roff[q + 1] = roff[q] + rlen[q];
+        rlen[q] = hof(q)[(size_t)(me + 1) * Bl] - hof(q)[(size_t)me * Bl];
+        if (q != me) sent += hme[(size_t)(q + 1) * Bl] - hme[(size_t)q * Bl];
     }
-    const uint64_t nrecv = roff[P];
+    uint64_t nrecv = 0;
+    for (int q = 0; q < P; ++q) nrecv += rlen[q];
     // The other ranks' pieces land behind this rank's partitioned keys when they fit (its own buckets
     // are then read in place: no copy); else everything goes to a receive buffer.
     const bool behind = nrecv - rlen[me] <= pl.recv_room;
-    std::vector<uint64_t> base(P), rpos(P);  // a source's first key of bucket me*Bl / where it lands
+    // per wave and source: where its pieces land (rpos) and the source position of its first key of
+    // the wave's first bucket (base)
+    std::vector<uint64_t> rpos((size_t)W * P), base((size_t)W * P), rcnt((size_t)W * P);
     {
-        uint64_t o = pl.n_local;
-        for (int q = 0; q < P; ++q) {
-            if (behind && q == me) {
-                base[q] = sdsp[me];
-                rpos[q] = 0;
-                continue;
+        uint64_t o = behind ? pl.n_local : 0;
+        for (int w = 0; w < W; ++w)
+            for (int q = 0; q < P; ++q) {
+                const size_t k = (size_t)w * P + q;
+                rcnt[k] = hof(q)[(size_t)me * Bl + jb[w + 1]] - hof(q)[(size_t)me * Bl + jb[w]];
+                if (behind && q == me) {
+                    base[k] = hme[(size_t)me * Bl + jb[w]];
+                    rpos[k] = 0;
+                    continue;
+                }
+                base[k] = rpos[k] = o;
+                o += rcnt[k];
             }
-            base[q] = rpos[q] = behind ? o : roff[q];
-            o += behind ? rlen[q] : 0;
-        }
     }
     if (!behind) {
         rc = ensure(ctx, &ctx->recv, &ctx->recv_bytes, (nrecv ? nrecv : 1) * sizeof(T) + 16, "receive buffer");
@@ -521,23 +540,36 @@ static int sample_sort_bx(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, T **d
     if (rc) return rc;
     T *rb = behind ? part : static_cast<T *>(ctx->recv);  // (the second level's source)
     exchange_fault_point(ctx, 2);
-    // 4. the buckets to their ranks: one send and one receive per peer (all-to-all-v over xGMI)
+    // 4. the buckets to their ranks: per wave one send and one receive per peer (all-to-all-v over
+    //    xGMI), on the comm stream after the partition
     if (ctx->ev_ok) {
         DSORT_HIP(ctx, hipEventRecord(ctx->ev[5], s));
         ctx->ev_mask |= 32u;
     }
+    hipStream_t cs = s;
     if (!host_tx) {
-        DSORT_NCCLNB(ctx, ncclGroupStart());
-        for (int q = 0; q < P; ++q) {
-            if (q == me) continue;
-            if (scnt[q]) DSORT_NCCLNB(ctx, ncclSend(part + sdsp[q], scnt[q], nccl_type<T>(), q, ctx->comm, s));
-            if (rlen[q]) DSORT_NCCLNB(ctx, ncclRecv(rb + rpos[q], rlen[q], nccl_type<T>(), q, ctx->comm, s));
+        if ((rc = comm_stream(ctx))) return rc;
+        cs = ctx->xs;
+        DSORT_HIP(ctx, hipEventRecord(ctx->xev[2], s));
+        DSORT_HIP(ctx, hipStreamWaitEvent(cs, ctx->xev[2], 0));
+        for (int w = 0; w < W; ++w) {
+            DSORT_NCCLNB(ctx, ncclGroupStart());
+            for (int q = 0; q < P; ++q) {
+                if (q == me) continue;
+                const uint64_t so = hme[(size_t)q * Bl + jb[w]], sn = hme[(size_t)q * Bl + jb[w + 1]] - so;
+                const size_t k = (size_t)w * P + q;
+                if (sn) DSORT_NCCLNB(ctx, ncclSend(part + so, sn, nccl_type<T>(), q, ctx->comm, cs));
+                if (rcnt[k]) DSORT_NCCLNB(ctx, ncclRecv(rb + rpos[k], rcnt[k], nccl_type<T>(), q, ctx->comm, cs));
+            }
+            DSORT_NCCLNB(ctx, ncclGroupEnd());
+            const size_t km = (size_t)w * P + me;
+            if (!behind && rcnt[km])
+                DSORT_HIP(ctx, hipMemcpyAsync(rb + rpos[km], part + hme[(size_t)me * Bl + jb[w]], rcnt[km] * sizeof(T),
+                                              hipMemcpyDeviceToDevice, cs));
+            DSORT_HIP(ctx, hipEventRecord(ctx->xev[w], cs));
         }
-        DSORT_NCCLNB(ctx, ncclGroupEnd());
-        rc = exch_wait(ctx, s, false, deadline, "key all-to-all (enqueue)");
+        rc = exch_wait(ctx, cs, false, deadline, "key all-to-all (enqueue)");
         if (rc) return rc;
-        if (scnt[me] && !behind)
-            DSORT_HIP(ctx, hipMemcpyAsync(rb + rpos[me], part + sdsp[me], scnt[me] * sizeof(T), hipMemcpyDeviceToDevice, s));
     } else {
         rc = ensure_host(ctx, &ctx->xfer, &ctx->xfer_bytes, (pl.n_local ? pl.n_local : 1) * sizeof(T));
         if (rc) return rc;
@@ -547,15 +579,15 @@ static int sample_sort_bx(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, T **d
             DSORT_HIP(ctx, hipMemcpyAsync(ctx->xfer, part, pl.n_local * sizeof(T), hipMemcpyDeviceToHost, s));
         rc = exch_wait(ctx, s, true, deadline, "key staging");
         if (rc) return rc;
-        // (the receive layout of the host buffer is the device one minus the partition: behind ->
-        // the other sources from n_local on, this rank's own buckets not shipped)
+        // (one wave; the receive layout of the host buffer is the device one minus the partition:
+        // behind -> the other sources from n_local on, this rank's own buckets not shipped)
         std::vector<size_t> sc(P), sd(P), rcn(P), rd(P);
         const uint64_t shift = behind ? pl.n_local : 0;
         for (int q = 0; q < P; ++q) {
             const bool self = behind && q == me;
-            sc[q] = self ? 0 : scnt[q] * sizeof(T);
-            sd[q] = sdsp[q] * sizeof(T);
-            rcn[q] = self ? 0 : rlen[q] * sizeof(T);
+            sd[q] = hme[(size_t)q * Bl] * sizeof(T);
+            sc[q] = self ? 0 : (hme[(size_t)(q + 1) * Bl] - hme[(size_t)q * Bl]) * sizeof(T);
+            rcn[q] = self ? 0 : rcnt[q] * sizeof(T);
             rd[q] = self ? 0 : (rpos[q] - shift) * sizeof(T);
         }
         if (ctx->transport.alltoallv(ctx->transport.user, ctx->xfer, sc.data(), sd.data(), ctx->xfer2, rcn.data(),
@@ -564,24 +596,37 @@ static int sample_sort_bx(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, T **d
         const uint64_t nland = behind ? nrecv - rlen[me] : nrecv;
         if (nland) DSORT_HIP(ctx, hipMemcpyAsync(rb + shift, ctx->xfer2, nland * sizeof(T), hipMemcpyHostToDevice, s));
     }
-    if (ctx->ev_ok) {
-        DSORT_HIP(ctx, hipEventRecord(ctx->ev[6], s));
-        DSORT_HIP(ctx, hipEventRecord(ctx->ev[3], s));
-        ctx->ev_mask |= 64u | 8u;
-    }
-    // 5. the second level and the tile sort of this rank's buckets, queued behind the receives on
-    //    the stream while the keys are in flight (the host builds and uploads its tables meanwhile);
-    //    its host waits poll the abort flag and the deadline, as a dead peer never completes the
-    //    stream.  Kill stages 1 and 2.
+    // 5. the second level and the tile sort of this rank's buckets, wave by wave, each queued behind
+    //    its receives while later waves are in flight (the host builds and uploads a wave's tables
+    //    meanwhile); the host waits inside poll the abort flag and the deadline, as a dead peer never
+    //    completes the stream.  Kill stages 1 and 2 (after the first wave's).
     T *outp = static_cast<T *>(ctx->recv2);
     ctx->poll_waits = !host_tx;
     ctx->poll_deadline = deadline;
-    rc = bx_local_sort<T>(ctx, rb, outp, pl, hb_all.data(), base.data(), s, true);
+    uint64_t out_off = 0;
+    for (int w = 0; w < W && !rc; ++w) {
+        if (!host_tx) {
+            DSORT_HIP(ctx, hipStreamWaitEvent(s, ctx->xev[w], 0));
+            if (w == 0 && ctx->ev_ok) {
+                DSORT_HIP(ctx, hipEventRecord(ctx->ev[6], s));  // (the first wave's keys in)
+                DSORT_HIP(ctx, hipEventRecord(ctx->ev[3], s));
+                ctx->ev_mask |= 64u | 8u;
+            }
+        }
+        uint64_t nw = 0;
+        rc = bx_local_sort<T>(ctx, rb, outp, pl, hb_all.data(), base.data() + (size_t)w * P, jb[w], jb[w + 1], out_off,
+                              w, W, s, true, &nw);
+        out_off += nw;
+    }
+    if (host_tx && ctx->ev_ok && !rc) {
+        DSORT_HIP(ctx, hipEventRecord(ctx->ev[6], s));
+        ctx->ev_mask |= 64u;
+    }
     ctx->poll_waits = false;
     if (rc == DSORT_ECOMM || rc == DSORT_ETIMEOUT) abort_comm_locked(ctx);
     if (rc) return rc;
     // the receives have landed (and the test hold, DSORT_OPT_TEST_HOLD_EXCHANGE, is released)
-    rc = exch_wait(ctx, s, true, deadline, "key all-to-all", ctx->opt.test_hold_exchange != 0);
+    rc = exch_wait(ctx, cs, true, deadline, "key all-to-all", ctx->opt.test_hold_exchange != 0);
     if (rc) return rc;
     ctx->last_stream = s;
     ctx->stats.keys_in = pl.n_local;
@@ -882,7 +927,7 @@ int dsort_finalize(dsort_ctx *ctx) {
     }
     void *bufs[] = {ctx->scratch, ctx->scratch2, ctx->splits, ctx->groups, ctx->io, ctx->io2, ctx->red,
                     ctx->local, ctx->recv, ctx->recv2, ctx->small, ctx->text_status,
-                    ctx->bucket, ctx->sub, ctx->tfb};
+                    ctx->bucket, ctx->sub, ctx->sub_alt, ctx->stmp, ctx->bxs, ctx->tfb};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (ctx->red_host) (void)hipHostFree(ctx->red_host);
@@ -898,6 +943,9 @@ int dsort_finalize(dsort_ctx *ctx) {
     if (ctx->side_ev) (void)hipEventDestroy(ctx->side_ev);
     if (ctx->ready_ev) (void)hipEventDestroy(ctx->ready_ev);
     if (ctx->side) (void)hipStreamDestroy(ctx->side);
+    for (auto &e : ctx->xev)
+        if (e) (void)hipEventDestroy(e);
+    if (ctx->xs) (void)hipStreamDestroy(ctx->xs);
     if (ctx->done_ev) (void)hipEventDestroy(ctx->done_ev);
     for (auto &e : ctx->ev)
         if (e) (void)hipEventDestroy(e);
@@ -1004,11 +1052,12 @@ int dsort_get_stats(const dsort_ctx *cctx, dsort_stats *out) {
     }
     out->block_sort_ms = el(0, 1);
     out->merge_ms = el(1, 2);
-    out->tile_sort_kernel_ms = el(7, 8);
+    // (the bucket exchange's first wave recorded its tile sort and second level at 22/23, 28/29)
+    out->tile_sort_kernel_ms = el(7, 8) + el(22, 23);
     out->partition_ms = el(0, 7);
     out->bucket_hist_ms = el(9, 10);
     out->bucket_scatter_ms = el(11, 12);
-    out->sub_partition_ms = el(13, 14);
+    out->sub_partition_ms = el(13, 14) + el(28, 29);
     if (ctx->ev_mask & 16u) {
         out->exchange_ms = el(2, 3);
         out->final_merge_ms = el(3, 4);

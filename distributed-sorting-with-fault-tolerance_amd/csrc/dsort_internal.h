@@ -97,6 +97,10 @@ struct dsort_ctx {
     hipEvent_t bucket_ev = nullptr;
     void *sub = nullptr;          // second partition level (dsort_sub.h)
     size_t sub_bytes = 0;
+    void *sub_alt = nullptr;      // the bucket exchange's second wave uses the other of the two
+    size_t sub_alt_bytes = 0;     // (the first wave's kernels still read theirs)
+    void *stmp = nullptr;         // merge output of a split sub-bucket (merge_split_subbuckets)
+    size_t stmp_bytes = 0;
     void *sub_host = nullptr;     // pinned: bucket table, chunk table, tile / merge-record counts
     size_t sub_host_bytes = 0;
     hipEvent_t sub_ev = nullptr;
@@ -136,6 +140,10 @@ struct dsort_ctx {
     size_t small_host_bytes = 0;
     void *bxs = nullptr;    // bucket exchange: this rank's and every rank's splitter samples
     size_t bxs_bytes = 0;
+    hipStream_t xs = nullptr;     // bucket exchange: the comm stream of its sends and receives
+    hipEvent_t xev[3] = {};       // ... a wave's receives done (0, 1), the partition done (2)
+    int ev_off = 0;               // stage events 1, 7, 8, 13, 14 of the bucket exchange's first
+                                  // wave go to 16, 22, 23, 28, 29 (dsort_get_stats adds them up)
     int ev_done = 2;        // the stage event a sort's second level records at its end (the bucket
                             // exchange records its own end as event 4)
     // The bucket exchange runs its second level while the keys are still in flight: the sort's
@@ -144,7 +152,7 @@ struct dsort_ctx {
     bool poll_waits = false;
     double poll_deadline = 0.0;  // ms on the CLOCK_MONOTONIC scale, 0 = none
     // stage timing
-    hipEvent_t ev[15] = {};  // 0 start, 1 tile sort done, 2 local sort done, 3 exchange done,
+    hipEvent_t ev[30] = {};  // 0 start, 1 tile sort done, 2 local sort done, 3 exchange done,
                              // 4 final merge done, 5/6 around the key all-to-all, 7/8 around the
                              // tile sort kernel, 9/10 around the first-level histogram, 11/12
                              // around the first-level scatter, 13/14 around the second-level
@@ -240,12 +248,14 @@ template <typename T>
 int bx_partition(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, const BxSample *d_all, hipStream_t s, bool timed,
                  const uint64_t **hb, T **part);
 // 3. after the exchange: src holds the pieces of this rank's buckets from every source r, source
-//    r's in bucket order from src[base[r]] on; hb_all[r * (Btot + 1) + g] = source r's bucket
-//    starts.  Sorts them into out (nrecv keys; src holds at least nrecv keys: the second level's
+//    r's in bucket order from src[base[r]] on (base: of the wave's first bucket);
+//    hb_all[r * (Btot + 1) + g] = source r's bucket starts.  Sorts them into out (nrecv keys; src holds at least nrecv keys: the second level's
 //    scratch).  Kill stages 1 and 2 fire here.
+//    The buckets [j_lo, j_hi) of this rank (wave w of W) into out + out_off; *n_out = their keys.
 template <typename T>
 int bx_local_sort(dsort_ctx *ctx, T *src, T *out, const BxPlan &pl, const uint64_t *hb_all,
-                  const uint64_t *base, hipStream_t s, bool timed);
+                  const uint64_t *base, int j_lo, int j_hi, uint64_t out_off, int w, int W, hipStream_t s,
+                  bool timed, uint64_t *n_out);
 
 }  // namespace dsort
 

@@ -1179,6 +1179,60 @@ __global__ void __launch_bounds__(64 * WG<T>::WAVES, WG<T>::OCC) bin_sort_kernel
         fb[atomicAdd(nfb, 1u)] = j;
 }
 
+// Persistent form of the gathering bin sort (two workgroups per CU looping over tiles): the next
+// tile's record and piece table are loaded while the current tile sorts, so a tile starts with its
+// key loads instead of two dependent round trips.  XCD x (workgroups b with b % 8 == x) takes the
+// contiguous block of tiles [x nt / 8, (x + 1) nt / 8), its workgroups interleaved over it.
+template <typename T>
+__global__ void __launch_bounds__(64 * WG<T>::WAVES, WG<T>::OCC) bin_sort_persist_kernel(const T *in, T *out,
+                                                                             const uint32_t *ntiles, sb::Gather ga,
+                                                                             uint32_t *fb, uint32_t *nfb) {
+    constexpr int TILE = TILE_OF<T>;
+    constexpr uint32_t NX = 8;
+    __shared__ __attribute__((aligned(16))) T s[TILE];
+    __shared__ __attribute__((aligned(16))) uint32_t cw[BIN_NB<T> / 2];
+    uint32_t *s32 = reinterpret_cast<uint32_t *>(s);
+    const uint32_t nt = *ntiles, G = gridDim.x, xc = blockIdx.x % NX, wi = blockIdx.x / NX;
+    const uint32_t gw = (G - xc + NX - 1) / NX;  // workgroups of this XCD
+    const uint32_t t1 = (uint32_t)(((uint64_t)xc + 1) * nt / NX);
+    uint32_t j = (uint32_t)((uint64_t)xc * nt / NX) + wi;
+    if (j >= t1) return;  // (workgroup-uniform)
+    uint2 pe[2];
+    gather_pieces(ga, j, pe);
+#pragma unroll 1
+    for (bool first = true; j < t1; j += gw, first = false) {
+        if (!first) __syncthreads();  // the previous tile's reads of s and cw are done
+        const sb::GTile gt = ga.tiles[j];
+        reinterpret_cast<uint4 *>(cw)[threadIdx.x] = make_uint4(0u, 0u, 0u, 0u);
+        const uint64_t base = gt.base;
+        const int valid = (int)gt.valid;
+        const sb::Spl<T> *sp = static_cast<const sb::Spl<T> *>(ga.spl) + (uint64_t)gt.b * ga.SS;
+        const auto *bs = static_cast<const typename bk::Comp<T>::C *>(ga.bspl);
+        const bool lk = gt.j0 > 0 || gt.b > 0, hk = gt.j1 < gt.nsub || (int)gt.b + 1 < ga.B;
+        const bool known = lk && hk;
+        T klo = T(0), khi = T(0);
+        if (known) {
+            klo = gt.j0 > 0 ? sp[gt.j0 - 1].k : bk::Comp<T>::key_of(bs[gt.b - 1]);
+            khi = gt.j1 < gt.nsub ? sp[gt.j1 - 1].k : bk::Comp<T>::key_of(bs[gt.b]);
+        }
+        const int jl = gt.j0 > 0 ? (int)gt.j0 - 1 : 0, jh = (int)gt.j1 - 1;
+        const int nspl = (int)gt.nsub - 1;
+        const int jj = jl + lane_id();
+        bool hint = false;
+        if (jj < jh && jj + 1 < nspl) hint = sp[jj].k == sp[jj + 1].k;
+        hint = __ballot(hint) != 0;
+        T x[R];
+        if (valid > 0) gather_tile<T>(ga, pe, gt, in, s32 + 128, s32 + 96, x, threadIdx.x);
+        // the next tile's piece table, in flight while this one sorts (its record is a scalar
+        // load at the top of the next iteration, issued with the splitter reads)
+        const uint32_t jn = j + gw;
+        if (jn < t1) gather_pieces(ga, jn, pe);
+        if (valid > 0 && !bin_sort_tile<T>(x, valid, s, cw, out + base, hint, known, klo, khi, threadIdx.x) &&
+            threadIdx.x == 0)
+            fb[atomicAdd(nfb, 1u)] = j;
+    }
+}
+
 // The bitonic tile sort of the bin sort's declined tiles fb[i], i < *nfb, each workgroup taking
 // i = blockIdx.x, blockIdx.x + gridDim.x, ... (the count stays on the device: the host never
 // waits for the bin sort, and with no declined tile every workgroup exits at once).
@@ -1476,6 +1530,7 @@ static std::vector<int> plan_passes(const dsort_opts &opt, uint64_t runs) {
 // first-level scatter, 13 / 14 the second-level partition.
 static int stage_event(dsort_ctx *ctx, hipStream_t s, bool timed, int i) {
     if (!timed || !ctx->ev_ok) return DSORT_OK;
+    if (i == 1 || i == 7 || i == 8 || i == 13 || i == 14) i += ctx->ev_off;
     DSORT_HIP(ctx, hipEventRecord(ctx->ev[i], s));
     ctx->ev_mask |= 1u << i;
     return DSORT_OK;
@@ -1501,6 +1556,12 @@ static int tile_sort(dsort_ctx *ctx, const T *in, T *out, uint64_t n, const uint
         if (rc) return rc;
         uint32_t *fb = static_cast<uint32_t *>(ctx->tfb), *nfb = fb + grid;
         DSORT_HIP(ctx, hipMemsetAsync(nfb, 0, 4, s));
+#ifdef DSORT_BIN_PERSIST
+        if constexpr (GATHER) {
+            const uint32_t pg = grid < 512 ? grid : 512;  // two workgroups per CU
+            hipLaunchKernelGGL((bin_sort_persist_kernel<T>), dim3(pg), blk, 0, s, in, out, ntiles, ga, fb, nfb);
+        } else
+#endif
         hipLaunchKernelGGL((bin_sort_kernel<T, GATHER>), dim3(grid), blk, 0, s, in, out, n, tiles, ntiles, ga, fb, nfb);
         DSORT_HIP(ctx, hipGetLastError());
         // the declined tiles: a grid of at most one round of workgroups over the chip walks the
@@ -1634,11 +1695,17 @@ static int side_stream(dsort_ctx *ctx) {
 // deepest such merge and sub_split_subbuckets to their number.
 template <typename T>
 static int merge_split_subbuckets(dsort_ctx *ctx, const sb::Ovf *d_ovf, uint32_t novf, const sb::GTile *d_tiles,
-                                  T *d_keys, T *tmp, hipStream_t s) {
+                                  T *d_keys, hipStream_t s) {
     using namespace sb;
     std::vector<Ovf> ov(novf);
     DSORT_HIP(ctx, hipMemcpyAsync(ov.data(), d_ovf, novf * sizeof(Ovf), hipMemcpyDeviceToHost, s));
     if (int rc_ = sync_stream(ctx, s, "sort stream")) return rc_;
+    // the merge output goes to a buffer of its own (the sort's source may still hold keys: the bucket
+    // exchange's later waves), then back
+    uint64_t mx = 0;
+    for (const Ovf &o : ov) mx = o.len > mx ? o.len : mx;
+    if (int rc_ = ensure(ctx, &ctx->stmp, &ctx->stmp_bytes, mx * sizeof(T) + 16, "split sub-bucket merge")) return rc_;
+    T *tmp = static_cast<T *>(ctx->stmp);
     int lv = 0;
     for (const Ovf &o : ov) {
         std::vector<GTile> gt(o.nt);
@@ -1652,9 +1719,9 @@ static int merge_split_subbuckets(dsort_ctx *ctx, const sb::Ovf *d_ovf, uint32_t
         }
         if (tot != o.len || (o.nt && gt[0].base != o.start))
             return set_err(ctx, DSORT_EHIP, "split sub-bucket: tile records do not cover it");
-        int rc = wave_merge<T>(ctx, d_keys + o.start, runs.data(), (int)runs.size(), tmp + o.start, s, true);
+        int rc = wave_merge<T>(ctx, d_keys + o.start, runs.data(), (int)runs.size(), tmp, s, true);
         if (rc) return rc;
-        DSORT_HIP(ctx, hipMemcpyAsync(d_keys + o.start, tmp + o.start, o.len * sizeof(T), hipMemcpyDeviceToDevice, s));
+        DSORT_HIP(ctx, hipMemcpyAsync(d_keys + o.start, tmp, o.len * sizeof(T), hipMemcpyDeviceToDevice, s));
         int l = 0;
         for (uint64_t r = runs.size(); r > 1; r = ceil_div(r, (uint64_t)1 << WG<T>::MAXLOGF)) ++l;
         lv = l > lv ? l : lv;
@@ -1929,15 +1996,12 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
             rc = tile_sort<T, true>(ctx, src, d_keys, n, nullptr, num, ga, ntiles, s, timed);
             if (rc) return rc;
         }
-        if (timed && ctx->ev_ok) {
-            DSORT_HIP(ctx, hipEventRecord(ctx->ev[1], s));
-            ctx->ev_mask |= 2u;
-        }
+        if ((rc = stage_event(ctx, s, timed, 1))) return rc;
         fault_point(ctx, s, 2);  // tile sort done (a split sub-bucket's merge follows)
         // sub-buckets above a tile (a sampling outlier): their split tiles' outputs merged (src,
         // read by the tile sort, is free scratch now)
         if (novf) {
-            rc = merge_split_subbuckets<T>(ctx, ovf, novf, static_cast<const GTile *>(tt), d_keys, src, s);
+            rc = merge_split_subbuckets<T>(ctx, ovf, novf, static_cast<const GTile *>(tt), d_keys, s);
             if (rc) return rc;
         }
         if (timed && ctx->ev_ok) {
@@ -2497,12 +2561,12 @@ int bx_partition(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, const BxSample
 
 template <typename T>
 int bx_local_sort(dsort_ctx *ctx, T *recv, T *out, const BxPlan &pl, const uint64_t *hb_all, const uint64_t *base,
-                  hipStream_t s, bool timed) {
+                  int j_lo, int j_hi, uint64_t out_off, int w, int W, hipStream_t s, bool timed, uint64_t *n_out) {
     using namespace wv;
     using C = typename bk::Comp<T>::C;
-    const int P = pl.P, me = pl.me, Bl = pl.Bl, Bt = pl.Btot;
-    const uint64_t g0 = (uint64_t)me * Bl;
-    // this rank's buckets: one piece per source, in source order
+    const int P = pl.P, me = pl.me, Bt = pl.Btot, Bl = j_hi - j_lo;  // (Bl: this wave's buckets)
+    const uint64_t g0 = (uint64_t)me * pl.Bl + (uint64_t)j_lo;
+    // this wave's buckets: one piece per source, in source order
     PieceMap<T> pm;
     pm.first.assign(Bl + 1, 0);
     pm.pure_key.assign(Bl, T(0));
@@ -2528,26 +2592,50 @@ int bx_local_sort(dsort_ctx *ctx, T *recv, T *out, const BxPlan &pl, const uint6
     }
     pm.first[Bl] = (uint32_t)pm.p.size();
     const uint64_t nrecv = hbo[Bl];
-    ctx->stats.keys_out = nrecv;
-    ctx->stats.tile_sort_keys = 0;
+    *n_out = nrecv;
+    const bool last = w + 1 == W;
+    // the statistics of the waves add up
+    const dsort_stats before = ctx->stats;
+    if (w == 0) ctx->stats.tile_sort_keys = 0;
     int rc = DSORT_OK;
     if (nrecv) {
         BkLayout<T> L;
         if ((rc = bx_layout<T>(ctx, pl, L))) return rc;  // (the arena as bx_partition left it: the splitters)
-        const int saved = ctx->ev_done;
-        ctx->ev_done = 4;
-        rc = sub_sort<T>(ctx, recv, out, nrecv, hbo.data(), Bl, sub_keys<T>(ctx), s, timed, ctx->opt.sub_gather != 0,
-                         pure.data(), false, L.spl + g0, false, &pm);
-        ctx->ev_done = saved;
+        // a second wave's tables go to the other second-level arena: the first wave's kernels may
+        // still read theirs when this wave's tables are uploaded
+        if (w & 1) {
+            std::swap(ctx->sub, ctx->sub_alt);
+            std::swap(ctx->sub_bytes, ctx->sub_alt_bytes);
+        }
+        const int saved_done = ctx->ev_done, saved_off = ctx->ev_off;
+        ctx->ev_off = last ? 0 : 15;
+        ctx->ev_done = last ? 4 : 16;
+        rc = sub_sort<T>(ctx, recv, out + out_off, nrecv, hbo.data(), Bl, sub_keys<T>(ctx), s, timed,
+                         ctx->opt.sub_gather != 0, pure.data(), false, L.spl + g0, false, &pm);
+        ctx->ev_done = saved_done;
+        ctx->ev_off = saved_off;
+        if (w & 1) {
+            std::swap(ctx->sub, ctx->sub_alt);
+            std::swap(ctx->sub_bytes, ctx->sub_alt_bytes);
+        }
         if (rc) return rc;
+        if (w > 0) {
+            ctx->stats.tile_sort_keys += before.tile_sort_keys;
+            ctx->stats.merge_passes = std::max(ctx->stats.merge_passes, before.merge_passes);
+            ctx->stats.sub_split_subbuckets += before.sub_split_subbuckets;
+            ctx->stats.sub_scatter_fallback |= before.sub_scatter_fallback;
+        }
     } else {
-        fault_point(ctx, s, 1);
-        fault_point(ctx, s, 2);
-        if (timed && ctx->ev_ok) {
+        if (w == 0) {
+            fault_point(ctx, s, 1);
+            fault_point(ctx, s, 2);
+        }
+        if (last && timed && ctx->ev_ok) {
             DSORT_HIP(ctx, hipEventRecord(ctx->ev[4], s));
             ctx->ev_mask |= 16u;
         }
     }
+    if (!last) return DSORT_OK;
     if (ctx->opt.kill_after_pass >= 0)  // (a kill stage this sort never reached)
         return set_err(ctx, DSORT_ESTAGE, "DSORT_OPT_KILL_AFTER_STAGE = " + std::to_string(ctx->opt.kill_after_pass) +
                                               ": the bucket exchange has " + std::to_string(ctx->stages_done) +
@@ -2562,9 +2650,9 @@ template int bx_partition<int32_t>(dsort_ctx *, const int32_t *, const BxPlan &,
 template int bx_partition<int64_t>(dsort_ctx *, const int64_t *, const BxPlan &, const BxSample *, hipStream_t, bool,
                                    const uint64_t **, int64_t **);
 template int bx_local_sort<int32_t>(dsort_ctx *, int32_t *, int32_t *, const BxPlan &, const uint64_t *,
-                                    const uint64_t *, hipStream_t, bool);
+                                    const uint64_t *, int, int, uint64_t, int, int, hipStream_t, bool, uint64_t *);
 template int bx_local_sort<int64_t>(dsort_ctx *, int64_t *, int64_t *, const BxPlan &, const uint64_t *,
-                                    const uint64_t *, hipStream_t, bool);
+                                    const uint64_t *, int, int, uint64_t, int, int, hipStream_t, bool, uint64_t *);
 
 namespace wv {
 
