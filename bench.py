@@ -504,7 +504,25 @@ def run_single(args):
     torch.cuda.synchronize()
     stats = ctx.stats()
     ctx.close()
+    # for context, not a baseline of the metric: the same keys through torch.sort (rocPRIM's radix
+    # sort of this image's PyTorch), outside the timed region
+    lib_ms = None
+    try:
+        del out
+        torch.cuda.empty_cache()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.sort(t_in)
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(3):
+            torch.sort(t_in)
+        e1.record()
+        torch.cuda.synchronize()
+        lib_ms = e0.elapsed_time(e1) / 3
+    except RuntimeError:  # (out of memory on a smaller device: no comparison)
+        lib_ms = None
     k = {key: v / max(args.steps, 1) for key, v in acc.items()}  # per step
+    k["torch_sort_ms"] = lib_ms
     k.update({"passes": stats["merge_passes"], "npass": npass, "tile": stats["tile_keys"], "w": w,
               "tile_sort_keys": tkeys // max(args.steps, 1), "n": n})
     return t1 - t0, k
@@ -672,6 +690,12 @@ def report_single(args, elapsed, k):
                                "rule": "sum of FETCH_SIZE x2 + WRITE_SIZE over the sort's kernels / device time "
                                        "of the sort (HIP events, first splitter kernel to last tile) / 8 TB/s"}
     result["roofline"] = roof
+    if k.get("torch_sort_ms"):
+        result["gpu_library_reference"] = {
+            "what": "torch.sort of the same resident keys on the same GPU (rocPRIM radix sort), values only; "
+                    "for context, outside the timed region",
+            "ms": round(k["torch_sort_ms"], 3), "keys_per_s": n / (k["torch_sort_ms"] * 1e-3),
+            "speedup_of_value": round(k["torch_sort_ms"] / step_ms, 3)}
     if not args.no_cpu_baseline and args.dtype == "i32":
         result["cpu_baseline"] = cpu_baseline(args.cpu_sample_keys, n)
     print(json.dumps(result), flush=True)

@@ -495,11 +495,12 @@ static int sample_sort_bx(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, T **d
         rc = allgather_u64(ctx, mine_hb.data(), (size_t)Bt + 1, hb_all.data(), s, deadline, "bucket starts all-gather");
         if (rc) return rc;
     }
-    // The exchange in W waves of this rank's buckets (RCCL, two or more buckets: W = 2): wave w ships
-    // buckets [jb[w], jb[w+1]) of every rank's range, and the second level of wave 0 runs while wave
-    // 1's keys are on the links (the sends and receives go on the comm stream; the sort stream waits
-    // for each wave's event).
-    const int W = (!host_tx && P > 1 && Bl >= 2) ? 2 : 1;
+    // The exchange in W waves of this rank's buckets (two or more buckets: W = 2): wave w ships
+    // buckets [jb[w], jb[w+1]) of every rank's range, and over RCCL the second level of wave 0 runs
+    // while wave 1's keys are on the links (the sends and receives go on the comm stream; the sort
+    // stream waits for each wave's event).  (The host transport and a single rank run the same waves
+    // one after the other: the same layout and second-level calls as the 8-GPU run.)
+    const int W = Bl >= 2 ? 2 : 1;
     const int jb[3] = {0, W == 2 ? Bl / 2 : Bl, Bl};
     const uint64_t *hme = hb_all.data() + (size_t)me * (Bt + 1);
     auto hof = [&](int r) { return hb_all.data() + (size_t)r * (Bt + 1); };
@@ -579,22 +580,32 @@ static int sample_sort_bx(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, T **d
             DSORT_HIP(ctx, hipMemcpyAsync(ctx->xfer, part, pl.n_local * sizeof(T), hipMemcpyDeviceToHost, s));
         rc = exch_wait(ctx, s, true, deadline, "key staging");
         if (rc) return rc;
-        // (one wave; the receive layout of the host buffer is the device one minus the partition:
-        // behind -> the other sources from n_local on, this rank's own buckets not shipped)
-        std::vector<size_t> sc(P), sd(P), rcn(P), rd(P);
+        // wave by wave; the receive layout of the host buffer is the device one minus the partition
+        // (behind: the other sources from n_local on, this rank's own buckets not shipped)
         const uint64_t shift = behind ? pl.n_local : 0;
-        for (int q = 0; q < P; ++q) {
-            const bool self = behind && q == me;
-            sd[q] = hme[(size_t)q * Bl] * sizeof(T);
-            sc[q] = self ? 0 : (hme[(size_t)(q + 1) * Bl] - hme[(size_t)q * Bl]) * sizeof(T);
-            rcn[q] = self ? 0 : rcnt[q] * sizeof(T);
-            rd[q] = self ? 0 : (rpos[q] - shift) * sizeof(T);
+        for (int w = 0; w < W; ++w) {
+            std::vector<size_t> sc(P), sd(P), rcn(P), rd(P);
+            uint64_t lo = ~0ull, hi = 0;
+            for (int q = 0; q < P; ++q) {
+                const size_t k = (size_t)w * P + q;
+                const bool self = behind && q == me;
+                const uint64_t so = hme[(size_t)q * Bl + jb[w]];
+                sd[q] = so * sizeof(T);
+                sc[q] = self ? 0 : (hme[(size_t)q * Bl + jb[w + 1]] - so) * sizeof(T);
+                rcn[q] = self ? 0 : rcnt[k] * sizeof(T);
+                rd[q] = self ? 0 : (rpos[k] - shift) * sizeof(T);
+                if (!self && rcnt[k]) {
+                    lo = std::min<uint64_t>(lo, rpos[k]);
+                    hi = std::max<uint64_t>(hi, rpos[k] + rcnt[k]);
+                }
+            }
+            if (ctx->transport.alltoallv(ctx->transport.user, ctx->xfer, sc.data(), sd.data(), ctx->xfer2, rcn.data(),
+                                         rd.data()))
+                return set_err(ctx, DSORT_ECOMM, "host transport alltoallv (keys) failed");
+            if (hi > lo)
+                DSORT_HIP(ctx, hipMemcpyAsync(rb + lo, static_cast<char *>(ctx->xfer2) + (lo - shift) * sizeof(T),
+                                              (hi - lo) * sizeof(T), hipMemcpyHostToDevice, s));
         }
-        if (ctx->transport.alltoallv(ctx->transport.user, ctx->xfer, sc.data(), sd.data(), ctx->xfer2, rcn.data(),
-                                     rd.data()))
-            return set_err(ctx, DSORT_ECOMM, "host transport alltoallv (keys) failed");
-        const uint64_t nland = behind ? nrecv - rlen[me] : nrecv;
-        if (nland) DSORT_HIP(ctx, hipMemcpyAsync(rb + shift, ctx->xfer2, nland * sizeof(T), hipMemcpyHostToDevice, s));
     }
     // 5. the second level and the tile sort of this rank's buckets, wave by wave, each queued behind
     //    its receives while later waves are in flight (the host builds and uploads a wave's tables

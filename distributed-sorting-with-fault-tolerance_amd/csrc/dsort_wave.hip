@@ -1179,60 +1179,6 @@ __global__ void __launch_bounds__(64 * WG<T>::WAVES, WG<T>::OCC) bin_sort_kernel
         fb[atomicAdd(nfb, 1u)] = j;
 }
 
-// Persistent form of the gathering bin sort (two workgroups per CU looping over tiles): the next
-// tile's record and piece table are loaded while the current tile sorts, so a tile starts with its
-// key loads instead of two dependent round trips.  XCD x (workgroups b with b % 8 == x) takes the
-// contiguous block of tiles [x nt / 8, (x + 1) nt / 8), its workgroups interleaved over it.
-template <typename T>
-__global__ void __launch_bounds__(64 * WG<T>::WAVES, WG<T>::OCC) bin_sort_persist_kernel(const T *in, T *out,
-                                                                             const uint32_t *ntiles, sb::Gather ga,
-                                                                             uint32_t *fb, uint32_t *nfb) {
-    constexpr int TILE = TILE_OF<T>;
-    constexpr uint32_t NX = 8;
-    __shared__ __attribute__((aligned(16))) T s[TILE];
-    __shared__ __attribute__((aligned(16))) uint32_t cw[BIN_NB<T> / 2];
-    uint32_t *s32 = reinterpret_cast<uint32_t *>(s);
-    const uint32_t nt = *ntiles, G = gridDim.x, xc = blockIdx.x % NX, wi = blockIdx.x / NX;
-    const uint32_t gw = (G - xc + NX - 1) / NX;  // workgroups of this XCD
-    const uint32_t t1 = (uint32_t)(((uint64_t)xc + 1) * nt / NX);
-    uint32_t j = (uint32_t)((uint64_t)xc * nt / NX) + wi;
-    if (j >= t1) return;  // (workgroup-uniform)
-    uint2 pe[2];
-    gather_pieces(ga, j, pe);
-#pragma unroll 1
-    for (bool first = true; j < t1; j += gw, first = false) {
-        if (!first) __syncthreads();  // the previous tile's reads of s and cw are done
-        const sb::GTile gt = ga.tiles[j];
-        reinterpret_cast<uint4 *>(cw)[threadIdx.x] = make_uint4(0u, 0u, 0u, 0u);
-        const uint64_t base = gt.base;
-        const int valid = (int)gt.valid;
-        const sb::Spl<T> *sp = static_cast<const sb::Spl<T> *>(ga.spl) + (uint64_t)gt.b * ga.SS;
-        const auto *bs = static_cast<const typename bk::Comp<T>::C *>(ga.bspl);
-        const bool lk = gt.j0 > 0 || gt.b > 0, hk = gt.j1 < gt.nsub || (int)gt.b + 1 < ga.B;
-        const bool known = lk && hk;
-        T klo = T(0), khi = T(0);
-        if (known) {
-            klo = gt.j0 > 0 ? sp[gt.j0 - 1].k : bk::Comp<T>::key_of(bs[gt.b - 1]);
-            khi = gt.j1 < gt.nsub ? sp[gt.j1 - 1].k : bk::Comp<T>::key_of(bs[gt.b]);
-        }
-        const int jl = gt.j0 > 0 ? (int)gt.j0 - 1 : 0, jh = (int)gt.j1 - 1;
-        const int nspl = (int)gt.nsub - 1;
-        const int jj = jl + lane_id();
-        bool hint = false;
-        if (jj < jh && jj + 1 < nspl) hint = sp[jj].k == sp[jj + 1].k;
-        hint = __ballot(hint) != 0;
-        T x[R];
-        if (valid > 0) gather_tile<T>(ga, pe, gt, in, s32 + 128, s32 + 96, x, threadIdx.x);
-        // the next tile's piece table, in flight while this one sorts (its record is a scalar
-        // load at the top of the next iteration, issued with the splitter reads)
-        const uint32_t jn = j + gw;
-        if (jn < t1) gather_pieces(ga, jn, pe);
-        if (valid > 0 && !bin_sort_tile<T>(x, valid, s, cw, out + base, hint, known, klo, khi, threadIdx.x) &&
-            threadIdx.x == 0)
-            fb[atomicAdd(nfb, 1u)] = j;
-    }
-}
-
 // The bitonic tile sort of the bin sort's declined tiles fb[i], i < *nfb, each workgroup taking
 // i = blockIdx.x, blockIdx.x + gridDim.x, ... (the count stays on the device: the host never
 // waits for the bin sort, and with no declined tile every workgroup exits at once).
@@ -1556,12 +1502,6 @@ static int tile_sort(dsort_ctx *ctx, const T *in, T *out, uint64_t n, const uint
         if (rc) return rc;
         uint32_t *fb = static_cast<uint32_t *>(ctx->tfb), *nfb = fb + grid;
         DSORT_HIP(ctx, hipMemsetAsync(nfb, 0, 4, s));
-#ifdef DSORT_BIN_PERSIST
-        if constexpr (GATHER) {
-            const uint32_t pg = grid < 512 ? grid : 512;  // two workgroups per CU
-            hipLaunchKernelGGL((bin_sort_persist_kernel<T>), dim3(pg), blk, 0, s, in, out, ntiles, ga, fb, nfb);
-        } else
-#endif
         hipLaunchKernelGGL((bin_sort_kernel<T, GATHER>), dim3(grid), blk, 0, s, in, out, n, tiles, ntiles, ga, fb, nfb);
         DSORT_HIP(ctx, hipGetLastError());
         // the declined tiles: a grid of at most one round of workgroups over the chip walks the
