@@ -366,6 +366,7 @@ static void abort_comm_locked(dsort_ctx *ctx) {
 // the abort flag or the deadline ends it.
 static int exch_wait(dsort_ctx *ctx, hipStream_t s, bool with_stream, double deadline, const char *what,
                      bool hold = false) {
+    PollPause pause;
     for (;;) {
         const hipError_t q0 = with_stream ? hipStreamQuery(s) : hipSuccess;
         const hipError_t q = hold && q0 == hipSuccess ? hipErrorNotReady : q0;
@@ -387,7 +388,7 @@ static int exch_wait(dsort_ctx *ctx, hipStream_t s, bool with_stream, double dea
             return set_err(ctx, DSORT_ETIMEOUT, std::string(what) + ": no progress before the deadline "
                                                     "(DSORT_OPT_COMM_TIMEOUT_MS); communicator aborted");
         }
-        usleep(4);  // (a few us: a wait on the critical path of every exchange step)
+        pause();  // (a wait on the critical path of every exchange step)
     }
 }
 
