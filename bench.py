@@ -378,11 +378,11 @@ def cpu_baseline(sample_keys, target_keys):
 # (the second level and the tile sort only the keys outside single-key buckets).
 STAGE_KERNELS = {
     4: [("bucket_hist_kernel<int>", "bucket_hist_ms", 1, "n"),
-        ("bucket_scatter_lines_kernel<int>", "bucket_scatter_ms", 2, "n"),
+        ("bucket_scatter_lines_kernel<int, false>", "bucket_scatter_ms", 2, "n"),
         ("sb_local_kernel<int>", "sub_partition_ms", 2, "tile_sort_keys"),
         ("bin_sort_kernel<int, true>", "tile_sort_kernel_ms", 2, "tile_sort_keys")],
     8: [("bucket_hist_kernel<long>", "bucket_hist_ms", 1, "n"),
-        ("bucket_scatter_lines_kernel<long>", "bucket_scatter_ms", 2, "n"),
+        ("bucket_scatter_lines_kernel<long, {ids}>", "bucket_scatter_ms", 2, "n"),
         ("sb_local_kernel<long>", "sub_partition_ms", 2, "tile_sort_keys"),
         ("bin_sort_kernel<long, true>", "tile_sort_kernel_ms", 2, "tile_sort_keys")],
 }
@@ -640,6 +640,9 @@ def stage_roofline(k, w, n, dist="uniform"):
     steps) against their algorithmic bytes, and the slowest of them."""
     stages = []
     for kernel, field, per_key, keys_field in STAGE_KERNELS[w]:
+        # (int64: the scatter variant that reads the histogram's bucket ids runs on skewed keys --
+        # the slot map chooses on the device; the bench's Zipf input takes it, uniform keys do not)
+        kernel = kernel.format(ids="true" if dist == "zipf" else "false")
         ms = k.get(field, 0.0)
         if ms <= 0:
             continue

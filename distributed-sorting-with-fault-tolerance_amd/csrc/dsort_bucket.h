@@ -43,6 +43,20 @@ template <> struct Geo<int32_t> { static constexpr int KPT = 16; };  // (14: +0.
 // int64: 48 KiB next to the 64 KiB carry (8 keys with the splitters read from global memory on
 // the lookups: C4 scatter 6.47 -> 7.09 ms)
 template <> struct Geo<int64_t> { static constexpr int KPT = 6; };
+// Bucket ids (int64, skewed keys): the histogram stores every key's bucket (2 bytes) and the
+// scatter reads it instead of repeating the lookup, when the lookup is the expensive one -- the log
+// slot map or one-key slots (BkMap.ids, set by bucket_slotmap_kernel): at 2^30 Zipf (C4) scatter
+// 6.52 -> 5.2-5.3 ms for histogram 2.08 -> 2.33 ms.  Uniform int64 keys (the linear map, no repeated
+// splitter) keep the lookup: there the scatter gained nothing and the histogram's writes cost
+// 1.50 -> 2.08 ms.  int32's packed lookup costs less than the 2 bytes per key would
+// (DSORT_BK_IDS32 builds it for comparison).
+template <typename T> struct BkIds {
+#ifdef DSORT_BK_IDS32
+    static constexpr bool ON = true;
+#else
+    static constexpr bool ON = sizeof(T) == 8;
+#endif
+};
 
 struct TileRef {
     uint64_t base;   // first key of the tile
@@ -131,6 +145,8 @@ struct BkMap {
     uint32_t sh;    // linear shift
     uint32_t mode;  // 0 linear, 1 log
     uint64_t invn;  // 2^48 / n: index -> 16-bit fraction of the input
+    uint32_t ids;   // int64: the histogram stores the buckets for the scatter (BkIds)
+    uint32_t pad;
 };
 // log mode: mantissa bits M, the largest with (KB - M + 1) * 2^M slots in the table
 template <typename T, int SB>
@@ -301,8 +317,10 @@ __global__ void __launch_bounds__(BK_MAXB) bucket_slotmap_kernel(const typename 
     const int j = threadIdx.x, nsp = B - 1;
     for (int i = j; i < 2 * BK_SLOTS; i += blockDim.x) cnt[i / BK_SLOTS][i % BK_SLOTS] = 0;
     if (j < 2) crowd[j] = 0;
+    __shared__ uint32_t dup;  // two adjacent splitters of one key: one-key slots
+    if (j == 0) dup = 0;
     const uint64_t invn = ((uint64_t)1 << 48) / (n > 0 ? n : 1);
-    BkMap mm[2] = {{0, (uint32_t)(CT::KB - BK_SLOTB), 0, invn}, {0, 0, 1, invn}};
+    BkMap mm[2] = {{0, (uint32_t)(CT::KB - BK_SLOTB), 0, invn, 0, 0}, {0, 0, 1, invn, 0, 0}};
     if (!CT::ADAPT) {
         if (j == 0) *out = mm[0];
         return;
@@ -312,11 +330,12 @@ __global__ void __launch_bounds__(BK_MAXB) bucket_slotmap_kernel(const typename 
         const U r = hi - lo;
         const int bits = r == 0 ? 0 : (int)(sizeof(U) * 8) - (sizeof(U) == 8 ? __builtin_clzll((uint64_t)r)
                                                                                : __builtin_clz((uint32_t)r));
-        mm[0] = BkMap{(uint64_t)lo, (uint32_t)(bits > BK_SLOTB ? bits - BK_SLOTB : 0), 0, invn};
-        mm[1] = BkMap{(uint64_t)lo, 0, 1, invn};
+        mm[0] = BkMap{(uint64_t)lo, (uint32_t)(bits > BK_SLOTB ? bits - BK_SLOTB : 0), 0, invn, 0, 0};
+        mm[1] = BkMap{(uint64_t)lo, 0, 1, invn, 0, 0};
     }
     __syncthreads();
     // count the distinct splitter keys of every slot under both maps
+    if (j > 0 && j < nsp && CT::key_of(spl[j]) == CT::key_of(spl[j - 1])) dup = 1;
     if (j < nsp && (j == 0 || CT::key_of(spl[j]) != CT::key_of(spl[j - 1]))) {
         const T k = CT::key_of(spl[j]);
         atomicAdd(&cnt[0][slot_at<T>(mm[0], k)], 1u);
@@ -325,7 +344,11 @@ __global__ void __launch_bounds__(BK_MAXB) bucket_slotmap_kernel(const typename 
     __syncthreads();
     for (int i = j; i < 2 * BK_SLOTS; i += blockDim.x) atomicMax(&crowd[i / BK_SLOTS], cnt[i / BK_SLOTS][i % BK_SLOTS]);
     __syncthreads();
-    if (j == 0) *out = crowd[1] < crowd[0] ? mm[1] : mm[0];
+    if (j == 0) {
+        BkMap r = crowd[1] < crowd[0] ? mm[1] : mm[0];
+        r.ids = BkIds<T>::ON && (r.mode == 1 || dup) ? 1u : 0u;
+        *out = r;
+    }
 }
 
 template <typename T>
@@ -431,7 +454,7 @@ __global__ void __launch_bounds__(BK_T, 2) bucket_hist_kernel(const T *__restric
                                                               const typename Comp<T>::C *__restrict__ spl_g,
                                                               const BkMap *__restrict__ map, int B, int BP,
                                                               int subs, uint32_t *__restrict__ counts,
-                                                              uint64_t ioff) {
+                                                              uint64_t ioff, uint16_t *__restrict__ ids) {
     using CT = Comp<T>;
     constexpr int KPT = Geo<T>::KPT, SUB = BK_T * KPT;
     __shared__ typename CT::C spl[BK_MAXB + 1];
@@ -471,14 +494,22 @@ __global__ void __launch_bounds__(BK_T, 2) bucket_hist_kernel(const T *__restric
             for (int k = 0; k < KPT; ++k) {
                 const uint64_t i = b0 + (uint64_t)k * BK_T;
                 const uint32_t sl = slot_mode<T, BK_SLOTB, 0>(m, key[k]);
-                if (i < n) atomicAdd(&hist[bucket_fast<T, false>(spl, rng, sl, key[k], CT::make(key[k], i + ioff))], 1u);
+                if (i < n) {
+                    const int b = bucket_fast<T, false>(spl, rng, sl, key[k], CT::make(key[k], i + ioff));
+                    atomicAdd(&hist[b], 1u);
+                    if (BkIds<T>::ON && m.ids) ids[i] = (uint16_t)b;
+                }
             }
         } else {
 #pragma unroll
             for (int k = 0; k < KPT; ++k) {
                 const uint64_t i = b0 + (uint64_t)k * BK_T;
                 const uint32_t sl = slot_mode<T, BK_SLOTB, 1>(m, key[k]);
-                if (i < n) atomicAdd(&hist[bucket_fast<T, false>(spl, rng, sl, key[k], CT::make(key[k], i + ioff))], 1u);
+                if (i < n) {
+                    const int b = bucket_fast<T, false>(spl, rng, sl, key[k], CT::make(key[k], i + ioff));
+                    atomicAdd(&hist[b], 1u);
+                    if (BkIds<T>::ON && m.ids) ids[i] = (uint16_t)b;
+                }
             }
         }
     }
@@ -640,14 +671,18 @@ __device__ unsigned long long g_bkstamps[8192 * 16];
     do {        \
     } while (0)
 #endif
-template <typename T>
+// IDS: the variant that reads the histogram's buckets (BkIds).  The host launches both variants for
+// int64 (it does not know the map's choice); the one that does not match m.ids returns at once
+// (one kernel with a run-time branch: uniform int64 scatter 5.29 -> 5.84 ms).
+template <typename T, bool IDS>
 __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__restrict__ in, uint64_t n,
                                                                     const typename Comp<T>::C *__restrict__ spl_g,
                                                                     const BkMap *__restrict__ map, int B, int BP, int subs,
                                                                     const uint32_t *__restrict__ offs,
                                                                     T *__restrict__ out, T *__restrict__ out2,
-                                                                    uint64_t ioff) {
+                                                                    uint64_t ioff, const uint16_t *__restrict__ ids) {
     using CT = Comp<T>;
+    static_assert(!IDS || BkIds<T>::ON, "bucket ids of this key width");
     using G = LineGeo<T>;
     using V = typename std::conditional<sizeof(T) == 4, int4, longlong2>::type;
     constexpr int KPT = Geo<T>::KPT, SUB = G::SUB, LK = G::LK, KPL = G::KPL;
@@ -656,8 +691,8 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
     // int32: the splitters are staged in lk for the slot table only (the packed lookup reads them
     // from global memory on its rare slow path), which leaves lk room for 16 keys per thread
     constexpr bool SPL_LK = !CT::ADAPT;
-    __shared__ typename CT::C spl_own[SPL_LK ? 1 : BK_MAXB + 1];
-    __shared__ uint32_t rng[BK_SLOTS];
+    __shared__ typename CT::C spl_own[SPL_LK || IDS ? 1 : BK_MAXB + 1];
+    __shared__ uint32_t rng[IDS ? 1 : BK_SLOTS];
     __shared__ uint32_t hist[BK_MAXB];               // sub-tile histogram, then the LDS starts
     __shared__ uint2 st[BK_MAXB];                    // per bucket: LDS start | first line << 16, vc|ph|pure|L
     __shared__ uint32_t sgb[BK_MAXB];                // per bucket: global index of stream entry 0
@@ -686,20 +721,27 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
         gb = o - ph;
         hist[tb] = 0;
     }
-    load_splitters<T>(spl_g, BP, spl);
     const BkMap m = *map;
-    __syncthreads();
-    build_slots<T, true>(spl, BP, m, rng);
+#ifndef DSORT_IDS_ONLY
+    if (BkIds<T>::ON && (m.ids != 0) != IDS) return;  // (workgroup-uniform: the other variant's sort)
+#endif
+    if (!IDS) {
+        load_splitters<T>(spl_g, BP, spl);
+        __syncthreads();
+        build_slots<T, true>(spl, BP, m, rng);
+    }
     __syncthreads();
     const uint64_t g0 = (uint64_t)g * subs * SUB;
 #ifdef DSORT_STAMPS
     uint64_t bk_acc[8] = {}, bk_t0 = __builtin_amdgcn_s_memtime();
 #endif
     T nxt[KPT];
+    uint16_t nid[KPT];
 #pragma unroll
     for (int k = 0; k < KPT; ++k) {
         const uint64_t i = g0 + tb + (uint64_t)k * BK_T;
         nxt[k] = i < n ? in[i] : T(0);
+        if (IDS) nid[k] = i < n ? ids[i] : (uint16_t)0;
     }
 #pragma unroll 1
     for (int sub = 0; sub < subs; ++sub) {
@@ -708,15 +750,21 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
         const bool last = sub + 1 == subs || s0 + SUB >= n;
         T key[KPT];
         uint32_t pk[KPT];  // rank | bucket << 16; ~0 past the input
+        uint32_t sl[KPT];  // (the lookup's slots, or the stored buckets)
 #pragma unroll
         for (int k = 0; k < KPT; ++k) key[k] = nxt[k];
-        uint32_t sl[KPT];
-        slots_at<T, KPT>(m, key, sl);
+        if constexpr (IDS) {
+#pragma unroll
+            for (int k = 0; k < KPT; ++k) sl[k] = nid[k];
+        } else {
+            slots_at<T, KPT>(m, key, sl);
+        }
         if (!last) {
 #pragma unroll
             for (int k = 0; k < KPT; ++k) {
                 const uint64_t i = s0 + SUB + tb + (uint64_t)k * BK_T;
                 nxt[k] = i < n ? in[i] : T(0);
+                if (IDS) nid[k] = i < n ? ids[i] : (uint16_t)0;
             }
         }
 #pragma unroll
@@ -724,7 +772,7 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
             const uint64_t i = s0 + tb + (uint64_t)k * BK_T;
             pk[k] = ~0u;
             if (i < n) {
-                const int b = bucket_fast<T, true>(spl_look, rng, sl[k], key[k], CT::make(key[k], i + ioff));
+                const int b = IDS ? (int)sl[k] : bucket_fast<T, true>(spl_look, rng, sl[k], key[k], CT::make(key[k], i + ioff));
                 pk[k] = atomicAdd(&hist[b], 1u) | (uint32_t)b << 16;
             }
         }

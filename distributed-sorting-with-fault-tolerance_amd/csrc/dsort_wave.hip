@@ -2026,6 +2026,7 @@ struct BkLayout {
     uint64_t *part, *bst;
     bk::TileRef *tt;
     bk::BkMap *map;
+    uint16_t *ids;  // every key's bucket (bk::BkIds), else null
 };
 template <typename T>
 static int bk_layout(dsort_ctx *ctx, uint64_t n, int B, size_t smp_bytes, BkLayout<T> &L) {
@@ -2042,7 +2043,7 @@ static int bk_layout(dsort_ctx *ctx, uint64_t n, int B, size_t smp_bytes, BkLayo
     const size_t o_smp = take(smp_bytes), o_spl = take((size_t)L.BP * sizeof(C)), o_cnt = take((size_t)L.G * B * 4),
                  o_part = take((size_t)L.nchunk * B * 8), o_offs = take((size_t)L.G * B * 4),
                  o_bst = take((size_t)(B + 1) * 8), o_tt = take((size_t)L.tmax * sizeof(TileRef)), o_nt = take(4),
-                 o_map = take(sizeof(BkMap));
+                 o_map = take(sizeof(BkMap)), o_ids = take(BkIds<T>::ON ? (size_t)n * 2 : 0);
     int rc = ensure(ctx, &ctx->bucket, &ctx->bucket_bytes, off, "bucket partition");
     if (rc) return rc;
     char *a = static_cast<char *>(ctx->bucket);
@@ -2055,6 +2056,7 @@ static int bk_layout(dsort_ctx *ctx, uint64_t n, int B, size_t smp_bytes, BkLayo
     L.tt = reinterpret_cast<TileRef *>(a + o_tt);
     L.ntl = reinterpret_cast<uint32_t *>(a + o_nt);
     L.map = reinterpret_cast<BkMap *>(a + o_map);
+    L.ids = BkIds<T>::ON ? reinterpret_cast<uint16_t *>(a + o_ids) : nullptr;
     const size_t hbytes = (size_t)(BK_MAXB + 1) * 8 + (size_t)BK_MAXB * 16;  // starts, then the splitters
     if (ctx->bucket_host_bytes < hbytes) {
         if (ctx->bucket_host) (void)hipHostFree(ctx->bucket_host);
@@ -2085,7 +2087,7 @@ static int first_level(dsort_ctx *ctx, const T *d_in, uint64_t n, uint64_t ioff,
     hipLaunchKernelGGL(bucket_slotmap_kernel<T>, dim3(1), dim3(BK_MAXB), 0, s, L.spl, B, n, L.map);
     if ((rc = stage_event(ctx, s, timed, 9))) return rc;
     hipLaunchKernelGGL(bucket_hist_kernel<T>, dim3((unsigned)L.G), dim3(BK_T), 0, s, d_in, n, L.spl, L.map, B, BP,
-                       L.subs, L.cnt, ioff);
+                       L.subs, L.cnt, ioff, L.ids);
     if ((rc = stage_event(ctx, s, timed, 10))) return rc;
     hipLaunchKernelGGL(bucket_colsum_kernel, dim3((unsigned)L.nchunk), dim3(BK_MAXB), 0, s, L.cnt, (uint32_t)L.G, B,
                        L.part);
@@ -2104,8 +2106,14 @@ static int first_level(dsort_ctx *ctx, const T *d_in, uint64_t n, uint64_t ioff,
     if (B > 1) DSORT_HIP(ctx, hipMemcpyAsync(hspl, L.spl, (size_t)(B - 1) * sizeof(C), hipMemcpyDeviceToHost, ctx->side));
     DSORT_HIP(ctx, hipEventRecord(ctx->bucket_ev, ctx->side));
     if ((rc = stage_event(ctx, s, timed, 11))) return rc;
-    hipLaunchKernelGGL(bucket_scatter_lines_kernel<T>, dim3((unsigned)L.G), dim3(BK_T), 0, s, d_in, n, L.spl, L.map, B,
-                       BP, L.subs, L.offs, part_out, direct, ioff);
+#ifdef DSORT_IDS_ONLY
+    if constexpr (!BkIds<T>::ON)
+#endif
+    hipLaunchKernelGGL((bucket_scatter_lines_kernel<T, false>), dim3((unsigned)L.G), dim3(BK_T), 0, s, d_in, n, L.spl,
+                       L.map, B, BP, L.subs, L.offs, part_out, direct, ioff, L.ids);
+    if constexpr (BkIds<T>::ON)  // (the variant the slot map did not choose returns at once)
+        hipLaunchKernelGGL((bucket_scatter_lines_kernel<T, true>), dim3((unsigned)L.G), dim3(BK_T), 0, s, d_in, n, L.spl,
+                           L.map, B, BP, L.subs, L.offs, part_out, direct, ioff, L.ids);
     DSORT_HIP(ctx, hipGetLastError());
     if ((rc = stage_event(ctx, s, timed, 12))) return rc;
     fault_point(ctx, s, 0);  // first-level partition done
