@@ -406,7 +406,8 @@ struct GTile {
     uint64_t src;          // first key of the bucket's first chunk (chunk c0 + k at src + k * SB_LCH)
     uint32_t valid, b, j0, j1;
     uint32_t c0, nch;      // the bucket's chunks [c0, c0 + nch)
-    uint32_t nsub, flags;  // the bucket's sub-buckets; bit 0: gathered key by key (no vector room)
+    uint32_t nsub, flags;  // the bucket's sub-buckets; bit 0: gathered key by key (no vector room);
+                           // bits 8-31: a split tile's start inside its first chunk's piece
 };
 
 // What the gathering tile sort needs (block_sort_w_kernel<T, true>): its tiles, the chunk and
@@ -440,29 +441,60 @@ struct Gather {
 // *ntiles > trec and takes the scatter path.
 //
 // Split of sub-bucket j (LOCAL, above a tile): greedy over the bucket's chunks, a tile taking
-// consecutive chunks' pieces while its keys plus cpad per piece fit `full`.  Calls f(ca, cb, valid)
-// per tile in order; returns the tile count.  Any one chunk's piece fits (a chunk holds fewer keys
-// than a tile).
+// consecutive chunks' pieces while its keys plus cpad per piece fit `full`.  A piece larger than a
+// tile's room (a chunk holds more keys than an int32 tile: 15360 vs 8192) is cut: the tiles that
+// start inside it take `full - cpad` keys of it each.  Calls f(ca, aoff, cb, valid) per tile in
+// order -- chunks [ca, cb), the first one's piece from offset aoff (GTile.flags >> 8); a one-chunk
+// tile takes `valid` keys from there -- and returns the tile count.
 template <typename F>
 __device__ __forceinline__ uint32_t split_tiles(const uint32_t *counts, int SS, uint32_t c0, uint32_t c1, int j,
                                                 uint32_t full, uint32_t cpad, F &&f) {
-    uint32_t nt = 0, ca = c0, v = 0;
+    uint32_t nt = 0, ca = c0, aoff = 0, v = 0, np = 0;
     for (uint32_t c = c0; c < c1; ++c) {
         const uint32_t *pc = counts + (uint64_t)c * (SS + 1);
         const uint32_t piece = pc[j + 1] - pc[j];
-        if (c > ca && v + piece + cpad * (c - ca + 1) > full) {
-            f(ca, c, v);
+        uint32_t off = 0;
+        while (off < piece) {
+            const uint32_t r = piece - off, used = v + cpad * (np + 1);
+            const uint32_t cap = full > used ? full - used : 0;
+            if (r <= cap) {  // the rest of the piece fits the open tile
+                v += r;
+                ++np;
+                break;
+            }
+            if (np == 0) {  // an empty tile: a cut of this piece alone
+                f(c, off, c + 1, cap);
+                ++nt;
+                off += cap;
+                ca = c;
+                aoff = off;
+                continue;
+            }
+            f(ca, aoff, c, v);  // the open tile ends before this chunk
             ++nt;
             ca = c;
+            aoff = off;
             v = 0;
+            np = 0;
         }
-        v += piece;
+        if (piece == 0 && np == 0 && v == 0) {  // (an empty piece at the open tile's start)
+            ca = c + 1;
+            aoff = 0;
+        }
     }
-    if (c1 > ca) {
-        f(ca, c1, v);
+    if (np) {
+        f(ca, aoff, c1, v);
         ++nt;
     }
     return nt;
+}
+// The piece of a gathered tile in chunk c (global key indices): [pref[c][j0], pref[c][j1]) of the
+// chunk, from offset flags >> 8 in the tile's first chunk; a one-chunk tile takes `valid` keys.
+__device__ __forceinline__ uint2 tile_piece(const uint32_t *counts, int SS, uint32_t base, uint32_t c, uint32_t c0,
+                                            uint32_t nch, uint32_t j0, uint32_t j1, uint32_t valid, uint32_t flags) {
+    const uint32_t *pc = counts + (uint64_t)c * (SS + 1);
+    const uint32_t lo = base + pc[j0] + (c == c0 ? flags >> 8 : 0u);
+    return make_uint2(lo, nch == 1 ? lo + valid : base + pc[j1]);
 }
 
 template <bool LOCAL>
@@ -559,7 +591,8 @@ __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restric
         room = (uint32_t)tile - ((p + mis) & (uint32_t)(align - 1));
         over = len > (LOCAL ? (uint32_t)full : room);
         if (LOCAL && over)  // (i1 == i0 + 1: a lone sub-bucket) cut by chunks
-            nt = split_tiles(counts, SS, b.c0, b.c1, (int)i0, (uint32_t)full, cpad, [](uint32_t, uint32_t, uint32_t) {});
+            nt = split_tiles(counts, SS, b.c0, b.c1, (int)i0, (uint32_t)full, cpad,
+                             [](uint32_t, uint32_t, uint32_t, uint32_t) {});
         else
             nt = len == 0 ? 0 : over ? 1 + (len - room + tile - 1) / tile : 1;
     }
@@ -581,14 +614,12 @@ __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restric
                 // piece tables like any tile's
                 uint32_t q = p;
                 split_tiles(counts, SS, b.c0, b.c1, (int)i0, (uint32_t)full, cpad,
-                            [&](uint32_t ca, uint32_t cb, uint32_t v) {
+                            [&](uint32_t ca, uint32_t aoff, uint32_t cb, uint32_t v) {
                                 if (k < trec)
-                                    gt[k] = GTile{q, b.start, v, blockIdx.x, i0, i1, ca, cb - ca, b.nsub, 0u};
-                                for (uint32_t c = ca; pieces && c < cb && k < tcap; ++c) {
-                                    const uint32_t *pc = counts + (uint64_t)c * (SS + 1);
-                                    const uint32_t base = (uint32_t)ch[c].start;
-                                    pieces[(uint64_t)k * PS + (c - ca)] = make_uint2(base + pc[i0], base + pc[i1]);
-                                }
+                                    gt[k] = GTile{q, b.start, v, blockIdx.x, i0, i1, ca, cb - ca, b.nsub, aoff << 8};
+                                for (uint32_t c = ca; pieces && c < cb && k < tcap; ++c)
+                                    pieces[(uint64_t)k * PS + (c - ca)] =
+                                        tile_piece(counts, SS, (uint32_t)ch[c].start, c, ca, cb - ca, i0, i1, v, aoff << 8);
                                 q += v;
                                 ++k;
                             });
@@ -636,11 +667,9 @@ __global__ void __launch_bounds__(256) sb_pieces_kernel(const GTile *__restrict_
     const uint32_t k = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (k >= *ntiles || k >= tcap) return;  // (wave-uniform; the host fails a sort past tcap)
     const GTile t = tiles[k];
-    for (uint32_t c = lane; c < t.nch; c += 64) {
-        const uint32_t *pc = counts + (uint64_t)(t.c0 + c) * (SS + 1);
-        const uint32_t base = (uint32_t)ch[t.c0 + c].start;
-        pieces[(uint64_t)k * PS + c] = make_uint2(base + pc[t.j0], base + pc[t.j1]);
-    }
+    for (uint32_t c = lane; c < t.nch; c += 64)
+        pieces[(uint64_t)k * PS + c] = tile_piece(counts, SS, (uint32_t)ch[t.c0 + c].start, t.c0 + c, t.c0, t.nch, t.j0,
+                                                  t.j1, t.valid, t.flags);
 }
 
 // Local partition (the default second level).  Chunk c (<= SB_LCH keys of one bucket) is loaded

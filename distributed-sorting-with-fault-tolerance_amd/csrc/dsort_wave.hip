@@ -61,8 +61,14 @@ constexpr int kWaveMaxF = 1 << kWaveMaxLogF;
 // Per key type: waves of the tile sort and of the merge tile, and the occupancy they are
 // compiled for (waves per SIMD: two workgroups per CU).
 template <typename T> struct WG;
+// int32 tile sort: 8192-key tiles of 512 threads, four workgroups per CU (40 KiB of LDS each):
+// while one workgroup gathers its tile another sorts (16384-key tiles, two per CU: bin sort 2.47
+// -> 2.05 ms at 2^30; round 4).
+#ifndef DSORT_I32_WAVES
+#define DSORT_I32_WAVES 8
+#endif
 template <> struct WG<int32_t> {
-    static constexpr int WAVES = 16, MWAVES = 16, OCC = 8, MAXLOGF = 5;
+    static constexpr int WAVES = DSORT_I32_WAVES, MWAVES = 16, OCC = 8, MAXLOGF = 5;
 };
 template <> struct WG<int64_t> {
     // F = 32 would need 32 run heads of 64-bit keys per lane next to the window: it spills, so
@@ -1591,10 +1597,14 @@ static int wave_merge(dsort_ctx *ctx, const T *d_in, const size_t *lens, int k, 
 
 // ---- second partition level (dsort_sub.h) -------------------------------------------------
 // Nominal keys per sub-bucket: TILE / 8 unless DSORT_OPT_SUB_KEYS says otherwise (0 = off).
+#ifndef DSORT_SUB_NOM_16THS
+#define DSORT_SUB_NOM_16THS 3
+#endif
+constexpr uint64_t SUB_NOM_16THS = DSORT_SUB_NOM_16THS;  // nominal sub-bucket: 3/16 of a tile
 template <typename T>
 static uint64_t sub_keys(const dsort_opts &opt) {
     const int64_t v = opt.sub_keys;
-    return v < 0 ? (uint64_t)TILE_OF<T> / 8 : (uint64_t)v;
+    return v < 0 ? (uint64_t)TILE_OF<T> * SUB_NOM_16THS / 16 : (uint64_t)v;
 }
 template <typename T>
 static uint64_t sub_keys(const dsort_ctx *ctx) { return sub_keys<T>(ctx->opt); }
@@ -1722,14 +1732,19 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
     const uint64_t CH = local ? SB_LCH<T> : SB_CH<T>;
     // samples per sub-bucket; a bucket's samples (<= SB_MAXS * 8) fit one int64 tile
     constexpr int kMaxOs = TILE_OF<int64_t> / SB_MAXS;
-    int os = ctx->opt.sub_os > 0 ? (ctx->opt.sub_os < kMaxOs ? (int)ctx->opt.sub_os : kMaxOs) : 4;
-    // buckets so large that even SB_MAXS sub-buckets average above an eighth of a tile: sample at
-    // the maximum rate, so the size spread (about 1/sqrt(os)) keeps every sub-bucket below a tile
+    // (nominal sub-buckets above an eighth of a tile -- the default 3/16 -- sample at the maximum
+    // rate: at 4 samples 10 of 16 sorts of 2^30 int32 met a sub-bucket above a tile, each costing
+    // 0.1-0.7 ms of split merge)
+    int os = ctx->opt.sub_os > 0 ? (ctx->opt.sub_os < kMaxOs ? (int)ctx->opt.sub_os : kMaxOs)
+                                 : (m > (uint64_t)TILE / 8 ? kMaxOs : 4);
+    // buckets so large that even SB_MAXS sub-buckets average above the nominal size (and above an
+    // eighth of a tile): sample at the maximum rate, so the size spread (about 1/sqrt(os)) keeps
+    // every sub-bucket below a tile
     // (at a quarter tile and os = 4, about one sort in 30 of two 3.3M-key buckets met a sub-bucket
     // above a tile and took the scatter path)
     if (ctx->opt.sub_os <= 0)
         for (int b = 0; b < B; ++b)
-            if (!pure[b] && hb[b + 1] - hb[b] > (uint64_t)SB_MAXS * TILE / 8) os = kMaxOs;
+            if (!pure[b] && hb[b + 1] - hb[b] > (uint64_t)SB_MAXS * std::max<uint64_t>(m, TILE / 8)) os = kMaxOs;
     // bucket and chunk tables
     std::vector<BInfo> bi((size_t)B);
     uint64_t nsmp = 0, nch = 0, nsubs = 0;

@@ -106,9 +106,10 @@ def test_sort_stages(dsort_mod):
 
     assert stages(0, 4) == 0 and stages(1, 8) == 0
     assert stages(1 << 30, 4) == 3 and stages(1 << 29, 4) == 3 and stages(1 << 25, 8) == 3
-    assert stages(16384, 4) == 1                   # one tile: the tile sort only
-    assert stages(1 << 20, 4) == 3                 # 64 tiles: tile sort + 2 merge passes (F <= 16)
-    assert stages((1 << 25) - 1, 4) == 1 + 3       # 2048 tiles: 11 bits in 3 passes
+    assert stages(8192, 4) == 1                    # one tile (8192 int32 keys): the tile sort only
+    assert stages(16384, 4) == 2                   # two tiles: + one merge pass
+    assert stages(1 << 20, 4) == 3                 # 128 tiles: tile sort + 2 merge passes (F <= 16)
+    assert stages((1 << 25) - 1, 4) == 1 + 3       # 4096 tiles: 12 bits in 3 passes
     m = ctypes.c_int()
     assert lib.dsort_sort_stages(None, 100, 2, ctypes.byref(m)) == -1
 

@@ -1,5 +1,5 @@
 """The bin sort of a tile (dsort_wave.hip bin_sort_tile) and its fall back to the bitonic tile
-sort, against numpy on the MI355X.  Inputs below 2^25 keys are sorted tile by tile (16384 int32 /
+sort, against numpy on the MI355X.  Inputs below 2^25 keys are sorted tile by tile (8192 int32 /
 8192 int64 keys, then merge passes), so each case below shapes the tiles directly:
 
 - spread keys: every tile takes the bin path;

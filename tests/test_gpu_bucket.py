@@ -11,7 +11,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 INT_MIN, INT_MAX = -(2**31), 2**31 - 1
-TILE = 16384
+TILE = 8192  # int32 tile of the tile sort (dsort_wave.hip WG<int32_t>)
 
 
 def _keys(rng, kind, n):

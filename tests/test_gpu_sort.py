@@ -16,7 +16,7 @@ CASES = json.load(open(os.path.join(GOLDEN, "cases.json")))
 INT_MIN, INT_MAX = -(2**31), 2**31 - 1
 I64_MIN, I64_MAX = -(2**63), 2**63 - 1
 TILE32, TILE64 = 8192, 4096
-WTILE = 16384  # int32 tile of the wave-register kernels (dsort_wave.hip)
+WTILE = 8192  # int32 tile of the wave-register tile sort (dsort_wave.hip; merge tiles: 16384)
 
 
 def sha(b):
