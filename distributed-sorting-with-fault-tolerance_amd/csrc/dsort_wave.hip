@@ -76,6 +76,9 @@ template <> struct WG<int64_t> {
     static constexpr int WAVES = 8, MWAVES = 8, OCC = 4, MAXLOGF = 4;
 };
 template <typename T> constexpr int TILE_OF = WK * WG<T>::WAVES;
+// The tile sort's kernels also come with W waves (W = 16: 16384-key int32 tiles, for buckets above
+// 2M keys, whose sub-buckets would come too close to an 8192-key tile; sub_sort picks).
+template <int W> constexpr int TILE_W = WK * W;
 template <typename T> constexpr int MTILE_OF = WK * WG<T>::MWAVES;
 template <typename T> constexpr int MSLACK_OF = MTILE_OF<T> / 32;      // cut tolerance of partk
 template <typename T> constexpr int MTNOM_OF = MTILE_OF<T> - 2 * MSLACK_OF<T>;
@@ -551,15 +554,15 @@ __device__ __forceinline__ T wave_max(T v) {
 
 // Bins per tile: two keys per bin on average.  The counters (16-bit, two per word) and the tile
 // fill exactly 80 KiB of LDS for int32 (64 + 16), so two workgroups share a CU.
-template <typename T> constexpr int BIN_NB = TILE_OF<T> / 2;
+template <int W> constexpr int BIN_NB = TILE_W<W> / 2;
 
 // Per-wave scratch of the bin sort; it lives at the start of the tile array s, which is free
 // until the keys are placed (step 4).
-template <typename T>
+template <typename T, int W>
 struct BinSm {
-    T mn[WG<T>::WAVES], mx[WG<T>::WAVES];
-    uint32_t wsum[WG<T>::WAVES];
-    uint32_t flag[WG<T>::WAVES];
+    T mn[W], mx[W];
+    uint32_t wsum[W];
+    uint32_t flag[W];
 };
 
 // __syncthreads_or with the caller's scratch (one word per wave): HIP's own reserves 256 bytes of
@@ -717,12 +720,12 @@ __device__ __forceinline__ void merge_halves(T (&v)[K]) {
 // the scalar path: 16 ds_read2_b32 per window at a 64-byte lane stride, 16-way bank conflicts.)
 // The last window at offset 8 would reach past the tile; its second half is empty, so the merge
 // is a no-op and it is skipped.
-template <int OFF, bool MERGE, typename T>
+template <int OFF, bool MERGE, int TILE, typename T>
 __device__ __forceinline__ void window_pass(T *s, int P, int tid) {
     using V = typename V16<T>::type;
     constexpr int N = KPC<T>;
     const int ws = 16 * tid + OFF;
-    if (ws >= P || ws + 16 > TILE_OF<T>) return;
+    if (ws >= P || ws + 16 > TILE) return;
     T v[16];
     V *p[16 / N];  // the window's 16-byte chunks (their physical slots: bsw)
 #pragma unroll
@@ -750,14 +753,14 @@ __device__ __forceinline__ void window_pass(T *s, int P, int tid) {
 //      returns false (out untouched) and the caller runs the bitonic sort.
 // About 30 operations per key on the window networks, against ~180 for the bitonic tile sort.
 // cw holds the counters (NB / 2 words); the caller has passed a barrier since its last use.
-template <typename T>
+template <typename T, int W>
 __device__ __forceinline__ bool bin_sort_tile(const T (&x)[R], int valid, T *s, uint32_t *cw, T *out,
                                               bool hot_hint, bool known, T klo, T khi, const int tid) {
     using U = typename sb::KeyU<T>::U;
-    constexpr int WAVES = WG<T>::WAVES, THREADS = 64 * WAVES, NB = BIN_NB<T>;
+    constexpr int WAVES = W, THREADS = 64 * WAVES, NB = BIN_NB<W>, TL = TILE_W<W>;
     constexpr int BPT = NB / THREADS;
     static_assert(BPT == 8, "one 16-byte word of counters per thread");
-    BinSm<T> &sm = *reinterpret_cast<BinSm<T> *>(s);
+    BinSm<T, W> &sm = *reinterpret_cast<BinSm<T, W> *>(s);
     const int lane = tid & 63, w = tid >> 6;
     // 1. range: the caller's bounds, or a reduction over the keys (which waits for all of them)
     T mn = klo, mx = khi;
@@ -795,7 +798,7 @@ __device__ __forceinline__ bool bin_sort_tile(const T (&x)[R], int valid, T *s, 
     // A tile within 3 keys of TILE keeps sh = 0 (its shifted slots would not fit) and writes keys.
     constexpr int N = KPC<T>;
     const int sh0 = (int)((reinterpret_cast<uintptr_t>(out) / sizeof(T)) & (N - 1));
-    const int sh = valid + sh0 <= TILE_OF<T> ? sh0 : 0;
+    const int sh = valid + sh0 <= TL ? sh0 : 0;
     const U range = (U)mx - (U)mn;
     BinMap<T> bm;
     bm.pre = 0;
@@ -854,7 +857,7 @@ __device__ __forceinline__ bool bin_sort_tile(const T (&x)[R], int valid, T *s, 
     // (E) and at least 24 slots past P (the windows reaching past P read them: no masking).
     const int P = (int)M + sh, E = valid + sh;
     {
-        const int F0 = E > P + 24 ? E : P + 24, F = F0 < TILE_OF<T> ? F0 : TILE_OF<T>;
+        const int F0 = E > P + 24 ? E : P + 24, F = F0 < TL ? F0 : TL;
         if (tid < sh) s[bsw<T>((uint32_t)tid)] = key_min<T>();
         for (int p = P + tid; p < F; p += THREADS) s[bsw<T>((uint32_t)p)] = key_max<T>();
     }
@@ -874,15 +877,15 @@ __device__ __forceinline__ bool bin_sort_tile(const T (&x)[R], int valid, T *s, 
     __syncthreads();
     STAMP(5);
     // 5. window passes; a descent can only be left at a boundary of the last pass's windows
-    window_pass<0, false>(s, P, tid);
+    window_pass<0, false, TL>(s, P, tid);
     __syncthreads();
     STAMP(6);
-    window_pass<8, true>(s, P, tid);
+    window_pass<8, true, TL>(s, P, tid);
     __syncthreads();
     STAMP(7);
     const int e8 = 16 * tid + 8;
     if (block_or<WAVES>(e8 < P && s[bsw<T>(e8 - 1)] > s[bsw<T>(e8)], cw)) {  // (cw is dead from step 5)
-        window_pass<0, true>(s, P, tid);
+        window_pass<0, true, TL>(s, P, tid);
         __syncthreads();
         const int e16 = 16 * tid + 16;
         if (block_or<WAVES>(e16 < P && s[bsw<T>(e16 - 1)] > s[bsw<T>(e16)], cw + WAVES)) return false;
@@ -952,11 +955,11 @@ __device__ __forceinline__ void gather_pieces(const sb::Gather &ga, uint32_t jt,
     }
 }
 // ptab: 3 kMaxPieces + 1 words of LDS for the piece table; wsum: one word per wave.
-template <typename T>
+template <typename T, int W>
 __device__ __forceinline__ void gather_tile(const sb::Gather &ga, const uint2 (&pe)[2], const sb::GTile &gt,
                                             const T *in, uint32_t *ptab, uint32_t *wsum, T (&x)[R],
                                             const int tid = threadIdx.x) {
-    constexpr int WAVES = WG<T>::WAVES, THREADS = 64 * WAVES, N = KPC<T>, KP = kMaxPieces<T>;
+    constexpr int WAVES = W, THREADS = 64 * WAVES, N = KPC<T>, KP = kMaxPieces<T>;
     using V = typename V16<T>::type;
     static_assert(2 * THREADS >= KP + 1, "two pieces per thread");
     uint32_t *voff = ptab, *plo = ptab + KP + 1, *phi = plo + KP;  // vector offsets, piece bounds
@@ -1061,11 +1064,11 @@ __device__ __forceinline__ void gather_tile(const sb::Gather &ga, const uint2 (&
 
 // Tile j's keys into x (any order; slots past `valid` are key_max).  Returns false when j is
 // past the tile count (the grid is an upper bound).
-template <typename T, bool GATHER>
+template <typename T, bool GATHER, int W>
 __device__ __forceinline__ bool load_tile(const T *in, uint64_t n, const uint4 *tiles, const uint32_t *ntiles,
                                           const sb::Gather &ga, uint32_t j, uint32_t *poff, uint32_t *wsum,
                                           T (&x)[R], uint64_t &base, int &valid, const int tid = threadIdx.x) {
-    constexpr int TILE = TILE_OF<T>, N = KPC<T>;
+    constexpr int TILE = TILE_W<W>, N = KPC<T>;
     using V = typename V16<T>::type;
     const int t = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform
@@ -1076,7 +1079,7 @@ __device__ __forceinline__ bool load_tile(const T *in, uint64_t n, const uint4 *
         valid = (int)gt.valid;
         uint2 pe[2];
         gather_pieces(ga, j, pe, tid);
-        gather_tile<T>(ga, pe, gt, in, poff, wsum, x, tid);
+        gather_tile<T, W>(ga, pe, gt, in, poff, wsum, x, tid);
         return true;
     } else if (tiles) {
         if (j >= *ntiles) return false;
@@ -1123,14 +1126,14 @@ __device__ __forceinline__ bool load_tile(const T *in, uint64_t n, const uint4 *
 
 // The bin sort of every tile (bin_sort_tile); a tile it declines is appended to fb (*nfb) for
 // the bitonic kernel.  Separate from the bitonic kernel so that each keeps its own registers.
-template <typename T, bool GATHER>
-__global__ void __launch_bounds__(64 * WG<T>::WAVES, WG<T>::OCC) bin_sort_kernel(const T *in, T *out, uint64_t n,
+template <typename T, bool GATHER, int W>
+__global__ void __launch_bounds__(64 * W, WG<T>::OCC) bin_sort_kernel(const T *in, T *out, uint64_t n,
                                                                      const uint4 *tiles, const uint32_t *ntiles,
                                                                      sb::Gather ga, uint32_t *fb, uint32_t *nfb) {
-    constexpr int TILE = TILE_OF<T>;
+    constexpr int TILE = TILE_W<W>;
     static_assert(128 + 3 * kMaxPieces<T> + 1 <= TILE * (int)sizeof(T) / 4, "the piece table fits in the tile");
     __shared__ __attribute__((aligned(16))) T s[TILE];
-    __shared__ __attribute__((aligned(16))) uint32_t cw[BIN_NB<T> / 2];
+    __shared__ __attribute__((aligned(16))) uint32_t cw[BIN_NB<W> / 2];
     // the counters are zeroed before the gather's barriers; the piece table of a gathered tile and
     // its scan words live in the tile array (free until the keys are placed), past BinSm
     reinterpret_cast<uint4 *>(cw)[threadIdx.x] = make_uint4(0u, 0u, 0u, 0u);
@@ -1175,25 +1178,25 @@ __global__ void __launch_bounds__(64 * WG<T>::WAVES, WG<T>::OCC) bin_sort_kernel
         const int jj = jl + lane_id();
         if (jj < jh && jj + 1 < nspl) hint = sp[jj].k == sp[jj + 1].k;
         hint = __ballot(hint) != 0;
-        gather_tile<T>(ga, pe, gt, in, s32 + 128, s32 + 96, x, threadIdx.x);
+        gather_tile<T, W>(ga, pe, gt, in, s32 + 128, s32 + 96, x, threadIdx.x);
     } else {
         j = blockIdx.x;
-        if (!load_tile<T, false>(in, n, tiles, ntiles, ga, j, nullptr, nullptr, x, base, valid)) return;
+        if (!load_tile<T, false, W>(in, n, tiles, ntiles, ga, j, nullptr, nullptr, x, base, valid)) return;
         if (valid == 0) return;
     }
     STAMP(1);
-    if (!bin_sort_tile<T>(x, valid, s, cw, out + base, hint, known, klo, khi, threadIdx.x) && threadIdx.x == 0)
+    if (!bin_sort_tile<T, W>(x, valid, s, cw, out + base, hint, known, klo, khi, threadIdx.x) && threadIdx.x == 0)
         fb[atomicAdd(nfb, 1u)] = j;
 }
 
 // The bitonic tile sort of the bin sort's declined tiles fb[i], i < *nfb, each workgroup taking
 // i = blockIdx.x, blockIdx.x + gridDim.x, ... (the count stays on the device: the host never
 // waits for the bin sort, and with no declined tile every workgroup exits at once).
-template <typename T, bool GATHER>
-__global__ void __launch_bounds__(64 * WG<T>::WAVES, WG<T>::OCC) block_sort_w_kernel(
+template <typename T, bool GATHER, int W>
+__global__ void __launch_bounds__(64 * W, WG<T>::OCC) block_sort_w_kernel(
     const T *in, T *out, uint64_t n, const uint4 *tiles, const uint32_t *ntiles, sb::Gather ga,
     const uint32_t *fb, const uint32_t *nfb) {
-    constexpr int TILE = TILE_OF<T>, N = KPC<T>;
+    constexpr int TILE = TILE_W<W>, N = KPC<T>;
     using V = typename V16<T>::type;
     // `in` may alias `out`: every workgroup reads its tile before it writes it
     __shared__ __attribute__((aligned(16))) T s[TILE + WK];  // + slack read by load_window
@@ -1210,7 +1213,7 @@ __global__ void __launch_bounds__(64 * WG<T>::WAVES, WG<T>::OCC) block_sort_w_ke
     int valid;
     const uint32_t j = fb[i];
     // (the piece table of a gathered tile sits in the runs' space: a barrier before they are written)
-    if (!load_tile<T, GATHER>(in, n, tiles, ntiles, ga, j, reinterpret_cast<uint32_t *>(s) + 64,
+    if (!load_tile<T, GATHER, W>(in, n, tiles, ntiles, ga, j, reinterpret_cast<uint32_t *>(s) + 64,
                               reinterpret_cast<uint32_t *>(s), x, base, valid))
         return;
     if (GATHER) __syncthreads();
@@ -1495,29 +1498,43 @@ static int tile_sort_event(dsort_ctx *ctx, hipStream_t s, bool timed, int which)
 // The tile sort of `grid` tiles (an upper bound when the count lives on the device): the bin
 // sort first, then the bitonic sort of the tiles it declined.  Events 7 / 8 around both.
 constexpr uint32_t kFallbackWgs = 512;  // two workgroups per CU
+template <typename T, bool GATHER, int W>
+static int tile_sort_w(dsort_ctx *ctx, const T *in, T *out, uint64_t n, const uint4 *tiles, const uint32_t *ntiles,
+                       const sb::Gather &ga, uint32_t grid, hipStream_t s) {
+    const dim3 blk(64 * W);
+    int rc = ensure(ctx, &ctx->tfb, &ctx->tfb_bytes, ((size_t)grid + 1) * 4, "tile fallback list");
+    if (rc) return rc;
+    uint32_t *fb = static_cast<uint32_t *>(ctx->tfb), *nfb = fb + grid;
+    DSORT_HIP(ctx, hipMemsetAsync(nfb, 0, 4, s));
+    hipLaunchKernelGGL((bin_sort_kernel<T, GATHER, W>), dim3(grid), blk, 0, s, in, out, n, tiles, ntiles, ga, fb, nfb);
+    DSORT_HIP(ctx, hipGetLastError());
+    // the declined tiles: a grid of at most one round of workgroups over the chip walks the
+    // list, whose length stays on the device (round 2 read it back: the host waited for the
+    // bin sort, and the GPU idled about 70 us per sort until the next work arrived)
+    const uint32_t fgrid = grid < kFallbackWgs ? grid : kFallbackWgs;
+    hipLaunchKernelGGL((block_sort_w_kernel<T, GATHER, W>), dim3(fgrid), blk, 0, s, in, out, n, tiles, ntiles, ga,
+                       static_cast<const uint32_t *>(fb), static_cast<const uint32_t *>(nfb));
+    DSORT_HIP(ctx, hipGetLastError());
+    return DSORT_OK;
+}
+// tile: the tile size in keys (TILE_OF<T>, or 16384 for int32's large buckets: sub_sort)
 template <typename T, bool GATHER>
 static int tile_sort(dsort_ctx *ctx, const T *in, T *out, uint64_t n, const uint4 *tiles, const uint32_t *ntiles,
-                     const sb::Gather &ga, uint32_t grid, hipStream_t s, bool timed) {
-    const dim3 blk(64 * WG<T>::WAVES);
+                     const sb::Gather &ga, uint32_t grid, hipStream_t s, bool timed, int tile = TILE_OF<T>) {
     int rc = tile_sort_event(ctx, s, timed, 0);
     if (rc) return rc;
     // (The library's own small sorts, the splitter samples, take the same path: nothing is read
     // back, and a tile of a bucket's 2048 samples costs the bin sort a quarter of what the bitonic
     // sort spends on the whole padded tile.)
     if (grid) {
-        rc = ensure(ctx, &ctx->tfb, &ctx->tfb_bytes, ((size_t)grid + 1) * 4, "tile fallback list");
+        rc = DSORT_EINVAL;
+        if (tile == TILE_OF<T>) {
+            rc = tile_sort_w<T, GATHER, WG<T>::WAVES>(ctx, in, out, n, tiles, ntiles, ga, grid, s);
+        } else if constexpr (sizeof(T) == 4) {
+            if (tile == TILE_W<16>) rc = tile_sort_w<T, GATHER, 16>(ctx, in, out, n, tiles, ntiles, ga, grid, s);
+        }
+        if (rc == DSORT_EINVAL) return set_err(ctx, DSORT_EINVAL, "tile sort: no kernel for this tile size");
         if (rc) return rc;
-        uint32_t *fb = static_cast<uint32_t *>(ctx->tfb), *nfb = fb + grid;
-        DSORT_HIP(ctx, hipMemsetAsync(nfb, 0, 4, s));
-        hipLaunchKernelGGL((bin_sort_kernel<T, GATHER>), dim3(grid), blk, 0, s, in, out, n, tiles, ntiles, ga, fb, nfb);
-        DSORT_HIP(ctx, hipGetLastError());
-        // the declined tiles: a grid of at most one round of workgroups over the chip walks the
-        // list, whose length stays on the device (round 2 read it back: the host waited for the
-        // bin sort, and the GPU idled about 70 us per sort until the next work arrived)
-        const uint32_t fgrid = grid < kFallbackWgs ? grid : kFallbackWgs;
-        hipLaunchKernelGGL((block_sort_w_kernel<T, GATHER>), dim3(fgrid), blk, 0, s, in, out, n, tiles, ntiles, ga,
-                           static_cast<const uint32_t *>(fb), static_cast<const uint32_t *>(nfb));
-        DSORT_HIP(ctx, hipGetLastError());
     }
     return tile_sort_event(ctx, s, timed, 1);
 }
@@ -1709,11 +1726,21 @@ __global__ void __launch_bounds__(256) fill_segments_kernel(T *out, const FillSe
 }
 
 template <typename T>
-static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_t *hb, int B, uint64_t m,
+static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_t *hb, int B, uint64_t m_in,
                     hipStream_t s, bool timed, bool local, const uint8_t *pure, bool pure_done, const void *bspl,
                     bool retry = false, const PieceMap<T> *pm = nullptr) {
     using namespace sb;
-    constexpr int TILE = TILE_OF<T>;
+    // The tile: int32 buckets above 2M keys take 16384-key tiles -- their sub-buckets (at most
+    // SB_MAXS per bucket) would average above a quarter of an 8192-key tile, and sampled 8 per
+    // sub-bucket many would overflow it (a 2^29-key rank of C3 has 4M-key buckets: 115 ms of split
+    // merges per sort on 8192-key tiles).  The nominal sub-bucket (DSORT_OPT_SUB_KEYS unset): 3/16 of
+    // an 8192-key tile, an eighth of a 16384-key one.
+    uint64_t maxlen = 0;
+    for (int b = 0; b < B; ++b)
+        if (!pure[b]) maxlen = std::max<uint64_t>(maxlen, hb[b + 1] - hb[b]);
+    const int TILE = sizeof(T) == 4 && maxlen > (uint64_t)SB_MAXS * TILE_OF<T> / 4 ? TILE_W<16> : TILE_OF<T>;
+    const uint64_t m = ctx->opt.sub_keys < 0 && TILE != TILE_OF<T> ? (uint64_t)TILE / 8 : m_in;
+    ctx->stats.tile_keys = TILE;
     constexpr uint64_t ALIGN = KPC<T>;
     const bool asked_local = local;
     const uint64_t LCH = SB_LCH<T>;
@@ -1949,7 +1976,7 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         // 3. tile sort: gathered from the chunks into d_keys
         if (ntiles) {
             const Gather ga{static_cast<const GTile *>(tt), dch, dbi, cnt, pcs, PS, SS, spl, bspl, B};
-            rc = tile_sort<T, true>(ctx, src, d_keys, n, nullptr, num, ga, ntiles, s, timed);
+            rc = tile_sort<T, true>(ctx, src, d_keys, n, nullptr, num, ga, ntiles, s, timed, TILE);
             if (rc) return rc;
         }
         if ((rc = stage_event(ctx, s, timed, 1))) return rc;
@@ -1992,7 +2019,7 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
     ctx->stats.merge_passes = 0;
     if (ntiles) {
         rc = tile_sort<T, false>(ctx, d_keys, d_keys, n, static_cast<const uint4 *>(tt), num, Gather{}, ntiles, s,
-                                 timed);
+                                 timed, TILE);
         if (rc) return rc;
     }
     if (timed && ctx->ev_ok) {
