@@ -20,9 +20,15 @@ def run(rank, world, port, n_total, dtype, dist, out_path, transport="rccl", dev
 
     import dsort
 
+    import datetime
+
+    def step(what):  # (progress on stdout: a hung rank shows where it stopped)
+        print(f"rank {rank}: {what}", flush=True)
+
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    tdist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
+    step("rendezvous done")
     ctx = dsort.Context(device)
     if transport == "host":  # ranks share one GPU: exchanges through gloo
         ctx.comm_init_transport(world, rank, dsort.torch_dist_transport(world))
@@ -45,8 +51,10 @@ def run(rank, world, port, n_total, dtype, dist, out_path, transport="rccl", dev
         if dist == "few":  # 8 distinct keys: whole buckets of one key on every rank
             t.copy_(t >> (29 if dtype == "i32" else 61))
     torch.cuda.synchronize()
+    step(f"input ready ({sz} keys)")
     ptr, nout = ctx.sample_sort_dev(t)
     ctx.synchronize()
+    step(f"sample sort done ({nout} keys)")
     host = np.zeros(nout, np.int32 if dtype == "i32" else np.int64)
     if nout:
         ctx.copy_d2h(host, ptr, host.nbytes)
@@ -58,6 +66,7 @@ def run(rank, world, port, n_total, dtype, dist, out_path, transport="rccl", dev
         json.dump(res, f)
     ctx.comm_destroy()
     ctx.close()
+    step("done")
     tdist.barrier()
     tdist.destroy_process_group()
 

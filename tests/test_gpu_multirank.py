@@ -32,7 +32,13 @@ def run_ranks(tmp_path, world, n, dtype="i32", dist="uniform", transport="host")
         except subprocess.TimeoutExpired:
             for q in procs:
                 q.kill()
-            raise
+            tails = list(logs)
+            for q in procs[len(logs):]:
+                try:
+                    tails.append(q.communicate(timeout=10)[0].decode(errors="replace"))
+                except (subprocess.TimeoutExpired, ValueError, OSError):
+                    tails.append("(no output)")
+            pytest.fail("ranks timed out; their last output:\n" + "\n---\n".join(t[-600:] for t in tails))
         logs.append(o.decode(errors="replace"))
     for p, lg in zip(procs, logs):
         assert p.returncode == 0, lg[-3000:]
