@@ -49,7 +49,8 @@ template <> struct Geo<int64_t> { static constexpr int KPT = 6; };
 // 6.52 -> 5.2-5.3 ms for histogram 2.08 -> 2.33 ms.  Uniform int64 keys (the linear map, no repeated
 // splitter) keep the lookup: there the scatter gained nothing and the histogram's writes cost
 // 1.50 -> 2.08 ms.  int32's packed lookup costs less than the 2 bytes per key would
-// (DSORT_BK_IDS32 builds it for comparison).
+// (DSORT_BK_IDS32 builds it for comparison: histogram 0.77 -> 1.23 ms, scatter 2.67 -> 3.25 ms at
+// 2^30, profiles/r4_ab_bucket_ids_int32.log).
 template <typename T> struct BkIds {
 #ifdef DSORT_BK_IDS32
     static constexpr bool ON = true;
@@ -322,7 +323,11 @@ __global__ void __launch_bounds__(BK_MAXB) bucket_slotmap_kernel(const typename 
     const uint64_t invn = ((uint64_t)1 << 48) / (n > 0 ? n : 1);
     BkMap mm[2] = {{0, (uint32_t)(CT::KB - BK_SLOTB), 0, invn, 0, 0}, {0, 0, 1, invn, 0, 0}};
     if (!CT::ADAPT) {
-        if (j == 0) *out = mm[0];
+        if (j == 0) {
+            BkMap r = mm[0];
+            r.ids = BkIds<T>::ON ? 1u : 0u;  // (int32 with DSORT_BK_IDS32: always)
+            *out = r;
+        }
         return;
     }
     if (nsp >= 1) {
