@@ -459,9 +459,10 @@ __global__ void __launch_bounds__(BK_T, 2) bucket_hist_kernel(const T *__restric
                                                               const typename Comp<T>::C *__restrict__ spl_g,
                                                               const BkMap *__restrict__ map, int B, int BP,
                                                               int subs, uint32_t *__restrict__ counts,
-                                                              uint64_t ioff, uint16_t *__restrict__ ids) {
+                                                              uint64_t ioff, uint32_t *__restrict__ ids) {
     using CT = Comp<T>;
     constexpr int KPT = Geo<T>::KPT, SUB = BK_T * KPT;
+    static_assert(!BkIds<T>::ON || KPT % 2 == 0, "bucket ids two per word");
     __shared__ typename CT::C spl[BK_MAXB + 1];
     __shared__ uint32_t rng[BK_SLOTS];
     const BkMap m = *map;
@@ -493,6 +494,8 @@ __global__ void __launch_bounds__(BK_T, 2) bucket_hist_kernel(const T *__restric
                 nxt[k] = i < n ? in[i] : T(0);
             }
         }
+        // the buckets of the thread's keys, two per word (bucket ids: BkIds)
+        uint32_t idw[KPT / 2] = {};
         // (the mode branch outside the key loop: a slot array would cost the second workgroup)
         if (!CT::ADAPT || m.mode == 0) {
 #pragma unroll
@@ -502,7 +505,7 @@ __global__ void __launch_bounds__(BK_T, 2) bucket_hist_kernel(const T *__restric
                 if (i < n) {
                     const int b = bucket_fast<T, false>(spl, rng, sl, key[k], CT::make(key[k], i + ioff));
                     atomicAdd(&hist[b], 1u);
-                    if (BkIds<T>::ON && m.ids) ids[i] = (uint16_t)b;
+                    idw[k / 2] |= (uint32_t)b << (16 * (k & 1));
                 }
             }
         } else {
@@ -513,9 +516,17 @@ __global__ void __launch_bounds__(BK_T, 2) bucket_hist_kernel(const T *__restric
                 if (i < n) {
                     const int b = bucket_fast<T, false>(spl, rng, sl, key[k], CT::make(key[k], i + ioff));
                     atomicAdd(&hist[b], 1u);
-                    if (BkIds<T>::ON && m.ids) ids[i] = (uint16_t)b;
+                    idw[k / 2] |= (uint32_t)b << (16 * (k & 1));
                 }
             }
+        }
+        // thread-major: the KPT ids of thread t of a sub-tile at words (sub-tile start + KPT t) / 2,
+        // i.e. a thread stores (and the scatter's thread loads) KPT / 2 consecutive words -- one
+        // 2-byte access per key measured slower than the lookup it replaces (int32)
+        if (BkIds<T>::ON && m.ids) {
+            uint32_t *dst = ids + (b0 - threadIdx.x) / 2 + (uint64_t)threadIdx.x * (KPT / 2);
+#pragma unroll
+            for (int w = 0; w < KPT / 2; ++w) dst[w] = idw[w];
         }
     }
     __syncthreads();
@@ -685,7 +696,7 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
                                                                     const BkMap *__restrict__ map, int B, int BP, int subs,
                                                                     const uint32_t *__restrict__ offs,
                                                                     T *__restrict__ out, T *__restrict__ out2,
-                                                                    uint64_t ioff, const uint16_t *__restrict__ ids) {
+                                                                    uint64_t ioff, const uint32_t *__restrict__ ids) {
     using CT = Comp<T>;
     static_assert(!IDS || BkIds<T>::ON, "bucket ids of this key width");
     using G = LineGeo<T>;
@@ -741,12 +752,15 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
     uint64_t bk_acc[8] = {}, bk_t0 = __builtin_amdgcn_s_memtime();
 #endif
     T nxt[KPT];
-    uint16_t nid[KPT];
+    uint32_t nid[IDS ? KPT / 2 : 1];  // (the histogram's thread-major bucket ids, two per word)
 #pragma unroll
     for (int k = 0; k < KPT; ++k) {
         const uint64_t i = g0 + tb + (uint64_t)k * BK_T;
         nxt[k] = i < n ? in[i] : T(0);
-        if (IDS) nid[k] = i < n ? ids[i] : (uint16_t)0;
+    }
+    if constexpr (IDS) {
+#pragma unroll
+        for (int w = 0; w < KPT / 2; ++w) nid[w] = g0 < n ? ids[g0 / 2 + (uint64_t)tb * (KPT / 2) + w] : 0u;
     }
 #pragma unroll 1
     for (int sub = 0; sub < subs; ++sub) {
@@ -760,7 +774,7 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
         for (int k = 0; k < KPT; ++k) key[k] = nxt[k];
         if constexpr (IDS) {
 #pragma unroll
-            for (int k = 0; k < KPT; ++k) sl[k] = nid[k];
+            for (int k = 0; k < KPT; ++k) sl[k] = (nid[k / 2] >> (16 * (k & 1))) & 0xFFFFu;
         } else {
             slots_at<T, KPT>(m, key, sl);
         }
@@ -769,7 +783,10 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
             for (int k = 0; k < KPT; ++k) {
                 const uint64_t i = s0 + SUB + tb + (uint64_t)k * BK_T;
                 nxt[k] = i < n ? in[i] : T(0);
-                if (IDS) nid[k] = i < n ? ids[i] : (uint16_t)0;
+            }
+            if constexpr (IDS) {
+#pragma unroll
+                for (int w = 0; w < KPT / 2; ++w) nid[w] = ids[(s0 + SUB) / 2 + (uint64_t)tb * (KPT / 2) + w];
             }
         }
 #pragma unroll

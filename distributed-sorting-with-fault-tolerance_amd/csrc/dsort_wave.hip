@@ -2068,7 +2068,7 @@ struct BkLayout {
     uint64_t *part, *bst;
     bk::TileRef *tt;
     bk::BkMap *map;
-    uint16_t *ids;  // every key's bucket (bk::BkIds), else null
+    uint32_t *ids;  // every key's bucket (bk::BkIds: two per word, thread-major per sub-tile), else null
 };
 template <typename T>
 static int bk_layout(dsort_ctx *ctx, uint64_t n, int B, size_t smp_bytes, BkLayout<T> &L) {
@@ -2085,7 +2085,7 @@ static int bk_layout(dsort_ctx *ctx, uint64_t n, int B, size_t smp_bytes, BkLayo
     const size_t o_smp = take(smp_bytes), o_spl = take((size_t)L.BP * sizeof(C)), o_cnt = take((size_t)L.G * B * 4),
                  o_part = take((size_t)L.nchunk * B * 8), o_offs = take((size_t)L.G * B * 4),
                  o_bst = take((size_t)(B + 1) * 8), o_tt = take((size_t)L.tmax * sizeof(TileRef)), o_nt = take(4),
-                 o_map = take(sizeof(BkMap)), o_ids = take(BkIds<T>::ON ? (size_t)n * 2 : 0);
+                 o_map = take(sizeof(BkMap)), o_ids = take(BkIds<T>::ON ? (size_t)L.G * L.subs * BK_T * Geo<T>::KPT * 2 : 0);
     int rc = ensure(ctx, &ctx->bucket, &ctx->bucket_bytes, off, "bucket partition");
     if (rc) return rc;
     char *a = static_cast<char *>(ctx->bucket);
@@ -2098,7 +2098,7 @@ static int bk_layout(dsort_ctx *ctx, uint64_t n, int B, size_t smp_bytes, BkLayo
     L.tt = reinterpret_cast<TileRef *>(a + o_tt);
     L.ntl = reinterpret_cast<uint32_t *>(a + o_nt);
     L.map = reinterpret_cast<BkMap *>(a + o_map);
-    L.ids = BkIds<T>::ON ? reinterpret_cast<uint16_t *>(a + o_ids) : nullptr;
+    L.ids = BkIds<T>::ON ? reinterpret_cast<uint32_t *>(a + o_ids) : nullptr;
     const size_t hbytes = (size_t)(BK_MAXB + 1) * 8 + (size_t)BK_MAXB * 16;  // starts, then the splitters
     if (ctx->bucket_host_bytes < hbytes) {
         if (ctx->bucket_host) (void)hipHostFree(ctx->bucket_host);
