@@ -322,3 +322,23 @@ def test_oversized_subbuckets_split_on_local_path(gpu_ctx, dtype, kind, sub_keys
     assert st["sub_scatter_fallback"] == 0
     if kind != "few":  # (few distinct keys: most buckets hold one key and skip the second level)
         assert st["sub_split_subbuckets"] > 0 and st["merge_passes"] >= 1
+
+
+@pytest.mark.parametrize("kind", ["uniform", "sorted", "few"])
+def test_large_buckets_take_16k_tiles(gpu_ctx, kind):
+    """int32 buckets above 2M keys (C3's 4M-key buckets per rank) are tile-sorted on 16384-key
+    tiles with sub-buckets of an eighth of a tile (sub_sort): exact output, the tile size in the
+    stats, no over-tile split and no scatter fallback on uniform keys."""
+    import torch
+    n = (1 << 23) + 777  # two buckets of about 4.2M keys
+    a = _keys(np.random.default_rng(23 + len(kind)), kind, n)
+    t = torch.from_numpy(a).cuda()
+    out = torch.empty_like(t)
+    with gpu_ctx.options(buckets=2):
+        gpu_ctx.sort_dev(t, out)
+        torch.cuda.synchronize()
+        st = gpu_ctx.stats()
+    assert np.array_equal(out.cpu().numpy(), np.sort(a))
+    assert st["sub_scatter_fallback"] == 0
+    if kind == "uniform":
+        assert st["tile_keys"] == 2 * TILE and st["sub_split_subbuckets"] == 0
