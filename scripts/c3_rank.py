@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--c3-buckets", type=int, default=128, help="global buckets of the one-rank bucket exchange")
     ap.add_argument("--only-bx", action="store_true", help="skip the sort-then-merge design (profiling)")
+    ap.add_argument("--opt", action="append", default=[], help="extra dsort option name=value for the bucket "
+                                                               "exchange (repeatable)")
     args = ap.parse_args()
 
     import torch
@@ -106,7 +108,8 @@ def main():
     # ---- B. bucket exchange on one rank with C3's bucket size
     ctx.comm_init(1, 0, dsort.Context.unique_id())
     acc = {}
-    with ctx.options(buckets=args.c3_buckets):
+    extra = {kv.split("=")[0]: int(eval(kv.split("=")[1], {}, {})) for kv in args.opt}
+    with ctx.options(buckets=args.c3_buckets, **extra):
         for _ in range(args.warmup):
             ctx.sample_sort_dev(chunk)
         ctx.synchronize()
