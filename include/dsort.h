@@ -62,7 +62,8 @@ typedef struct dsort_stats {
     double merge_kernel_ms; /* sum of the merge kernel's own launch durations (HIP events) */
     int merge_kernel_launches;
     int merge_passes;       /* number of global merge passes executed                     */
-    int tile_keys;          /* keys per block-sort tile                                   */
+    int tile_keys;          /* keys per tile of the tile sort (int32 8192, or 16384 when a */
+                            /* bucket exceeds 2M keys; int64 8192)                         */
     size_t keys_in;         /* keys handed to the call                                    */
     size_t keys_out;        /* keys produced (multi-GPU: this rank's key range)           */
     double alltoall_ms;     /* multi-GPU: the key all-to-all alone (grouped send/recv)    */
