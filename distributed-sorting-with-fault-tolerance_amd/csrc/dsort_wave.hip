@@ -25,8 +25,9 @@
 //     window is min(A[a0 + e], B[b0 + 1023 - e]) -- two ascending LDS reads and a min per key,
 //     a bitonic sequence -- sorted by the 10-stage half-cleaner network.  Windows are held in
 //     registers across a barrier, so the level merges in place in one LDS buffer.
-//   Key types: int32 tiles of 16 waves (16384 keys, 64 KiB LDS, two workgroups per CU); int64
-//   tiles of 8 waves (8192 keys, 64 KiB).
+//   Key types: int32 tiles of 8 waves (8192 keys, 32 KiB LDS, four workgroups per CU; 16 waves and
+//   16384 keys for buckets above 2M keys), merge tiles of 16 waves; int64 tiles of 8 waves (8192
+//   keys, 64 KiB).
 //
 // Algorithmic HBM traffic: 2 * sizeof(key) bytes per key for the tile sort and for every pass.
 #include <hip/hip_runtime.h>
@@ -59,7 +60,7 @@ constexpr int kWaveMaxLogF = 5;    // fan-in cap of one merge pass
 constexpr int kWaveMaxF = 1 << kWaveMaxLogF;
 
 // Per key type: waves of the tile sort and of the merge tile, and the occupancy they are
-// compiled for (waves per SIMD: two workgroups per CU).
+// compiled for (waves per SIMD).
 template <typename T> struct WG;
 // int32 tile sort: 8192-key tiles of 512 threads, four workgroups per CU (40 KiB of LDS each):
 // while one workgroup gathers its tile another sorts (16384-key tiles, two per CU: bin sort 2.47
@@ -1577,10 +1578,9 @@ static int launch_pass_w(dsort_ctx *ctx, const T *src, T *dst, const PassDesc &p
 // ---- bucketed sort (dsort_bucket.h) ------------------------------------------------------
 // Buckets of about 2^20 keys: at most 1024, and none below 2^25 keys (DSORT_OPT_BUCKETS = 0
 // turns the partition off, B forces B buckets, DSORT_OPT_BUCKET_KEYS sets the nominal bucket
-// size).  int32 at 2^30 keys: 1024 buckets of about 64 16K-key tiles; the largest stays below 128
-// tiles (7 merge levels: F = 16, then F = 8), and the buckets of <= 64 runs take F = 8 twice
-// (per-bucket fan-in, below).  int64: 1024 buckets of about 128 8K-key tiles.  A nested sort (the
-// splitter samples) never buckets.
+// size).  Without the second level (DSORT_OPT_SUB_KEYS = 0) every bucket is tile-sorted and
+// merged with a per-bucket fan-in (int32 at 2^30 keys: 1024 buckets of about 128 8K-key tiles).
+// A nested sort (the splitter samples) never buckets.
 static int bucket_count(const dsort_opts &opt, uint64_t n) {
     const int64_t forced = opt.buckets;
     if (forced == 0) return 0;
