@@ -125,11 +125,33 @@ __device__ __forceinline__ bool below(const Spl<T> &s, T key, uint32_t pos) {
 // slot are below it iff their slot is lower (slot_of is monotone), so only the slot's own
 // splitters are searched -- usually none or one.
 // The part after the reads: r = the key's slot entry, a and b = the slot's first two splitters.
+// One-key slots (bit 15 of the entry: three or more splitters, all of one key K -- a duplicate
+// run of a skewed bucket, int64 Zipf): a key other than K lies below or above all of them, with no
+// search.  A copy of K positioned before the first of them or from the last one on goes to the
+// outer sub-bucket the (key, position) order gives it, so those stay as full as sampled; the
+// copies in between may go to any sub-bucket between the first and the last K splitter (each holds
+// only K), and a hash of the position spreads them evenly -- instead of a divergent binary search
+// (C4: second level 3.0 -> 2.3 ms).  (In proportion to the position, the first level's rule, the
+// sub-buckets came out uneven -- a bucket at the edge of a heavy key's run holds that key's copies
+// from one end of the input only -- and one overflowed a tile in most sorts.)  Only this function
+// places keys on the local path; the scatter path's two passes both call it.
+constexpr uint32_t SB_ONEKEY = 0x8000u;
 template <typename T>
 __device__ __forceinline__ int sub_pick(const Spl<T> *spl, uint32_t r, const Spl<T> &a, const Spl<T> &b, T key,
                                         uint32_t pos) {
-    int lo = (int)(r & 0xFFFF);
+    int lo = (int)(r & 0x7FFF);
     const int hi = (int)(r >> 16);
+    if (r & SB_ONEKEY) {
+        if (key != a.k) return key < a.k ? lo : hi;
+        if (pos < a.p) return lo;
+        const Spl<T> z = spl[hi - 1];
+        if (pos >= z.p) return hi;
+        // (any sub-bucket in [lo + 1, hi - 1] holds only K: spread the copies by a hash of the
+        // position, which balances them whatever their positions are)
+        const float f = (float)((pos * 2654435761u) >> 8) * 0x1p-24f;
+        const int jj = (int)(f * (float)(hi - lo - 1));
+        return lo + 1 + (jj < hi - lo - 2 ? jj : hi - lo - 2);
+    }
     const int j = lo + (lo < hi && below<T>(a, key, pos) ? 1 + (lo + 1 < hi && below<T>(b, key, pos)) : 0);
     if (j < lo + 2 || j >= hi) return j;
     lo = j;
@@ -148,7 +170,7 @@ __device__ __forceinline__ int sub_of(const Spl<T> *spl, const uint32_t *rng, T 
     // none in about 60 % of the keys' cases at 2^30 uniform: fewer lanes in every random LDS read,
     // fewer bank conflicts), then the rare crowded slot
     const uint32_t r = rng[slot_of<T>(key, klo, sh)];
-    const int lo = (int)(r & 0xFFFF), hi = (int)(r >> 16);
+    const int lo = (int)(r & 0x7FFF), hi = (int)(r >> 16);
     Spl<T> a{}, b{};
     if (lo < hi) a = spl[lo];
     if (lo + 1 < hi) b = spl[lo + 1];
@@ -279,6 +301,7 @@ __global__ void __launch_bounds__(SB_MAXS) sb_splitter_kernel(const int64_t *__r
                                                               SlotFn<T> *__restrict__ sfn) {
     using U = typename KeyU<T>::U;
     __shared__ uint32_t sslot[SB_MAXS];
+    __shared__ T skey[SB_MAXS];
     const BInfo b = bi[blockIdx.x];
     const int tid = threadIdx.x;
     const int nspl = (int)b.nsub - 1;
@@ -297,6 +320,7 @@ __global__ void __launch_bounds__(SB_MAXS) sb_splitter_kernel(const int64_t *__r
             sp.p = (uint32_t)bucket_src_pos(b, ch, sample_pos(b, g - b.soff));
             spl[(uint64_t)blockIdx.x * SS + tid] = sp;
             sslot[tid] = slot_of<T>(K, klo, sh);
+            skey[tid] = K;
         }
     }
     __syncthreads();
@@ -313,7 +337,8 @@ __global__ void __launch_bounds__(SB_MAXS) sb_splitter_kernel(const int64_t *__r
             if (sslot[mid] <= (uint32_t)s) lo2 = mid + 1;
             else hi2 = mid;
         }
-        rng[(uint64_t)blockIdx.x * SB_SLOTS + s] = lo | (lo2 << 16);
+        const bool one = lo2 >= lo + 3 && skey[lo] == skey[lo2 - 1];
+        rng[(uint64_t)blockIdx.x * SB_SLOTS + s] = lo | (one ? SB_ONEKEY : 0u) | (lo2 << 16);
     }
     if (tid == 0) sfn[blockIdx.x] = SlotFn<T>{klo, sh, 0};
 }
@@ -796,7 +821,7 @@ __global__ void __launch_bounds__(SB_LT<T>, SB_LT<T> / 128) sb_local_kernel(T *_
 #pragma unroll
         for (int u = 0; u < G; ++u)
             if (g0 + u < KPT) {
-                const uint32_t lo = r[u] & 0xFFFF, hi = r[u] >> 16;
+                const uint32_t lo = r[u] & 0x7FFF, hi = r[u] >> 16;
                 sa[u] = Spl<T>{};
                 sb[u] = Spl<T>{};
                 if (lo < hi) sa[u] = spl[lo];
