@@ -380,11 +380,11 @@ STAGE_KERNELS = {
     4: [("bucket_hist_kernel<int>", "bucket_hist_ms", 1, "n"),
         ("bucket_scatter_lines_kernel<int, false>", "bucket_scatter_ms", 2, "n"),
         ("sb_local_kernel<int>", "sub_partition_ms", 2, "tile_sort_keys"),
-        ("bin_sort_kernel<int, true>", "tile_sort_kernel_ms", 2, "tile_sort_keys")],
+        ("bin_sort_kernel<int, true, 8>", "tile_sort_kernel_ms", 2, "tile_sort_keys")],
     8: [("bucket_hist_kernel<long>", "bucket_hist_ms", 1, "n"),
         ("bucket_scatter_lines_kernel<long, {ids}>", "bucket_scatter_ms", 2, "n"),
         ("sb_local_kernel<long>", "sub_partition_ms", 2, "tile_sort_keys"),
-        ("bin_sort_kernel<long, true>", "tile_sort_kernel_ms", 2, "tile_sort_keys")],
+        ("bin_sort_kernel<long, true, 8>", "tile_sort_kernel_ms", 2, "tile_sort_keys")],
 }
 # the generator and runtime copies are not part of the sort
 NOT_SORT = ("gen_uniform", "gen_zipf", "__amd_rocclr", "fingerprint", "descents")
