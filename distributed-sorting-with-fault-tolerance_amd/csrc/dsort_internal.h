@@ -51,14 +51,17 @@ struct PassDesc {
 struct dsort_opts {
     int64_t buckets = -1;           // DSORT_OPT_BUCKETS: -1 auto, 0 off, B forced
     int64_t bucket_keys = 1 << 20;  // DSORT_OPT_BUCKET_KEYS
-    int64_t bucket_os = 256;        // DSORT_OPT_BUCKET_OVERSAMPLE
+#ifndef DSORT_BUCKET_OS_DEFAULT
+#define DSORT_BUCKET_OS_DEFAULT 256
+#endif
+    int64_t bucket_os = DSORT_BUCKET_OS_DEFAULT;  // DSORT_OPT_BUCKET_OVERSAMPLE
     int64_t max_logf = -1;          // DSORT_OPT_MAX_FANIN_LOG2: -1 = per key type default
     int64_t kill_after_pass = -1;   // DSORT_OPT_KILL_AFTER_STAGE
     int64_t kill_in_exchange = -1;  // DSORT_OPT_KILL_IN_EXCHANGE
     int64_t comm_timeout_ms = 0;    // DSORT_OPT_COMM_TIMEOUT_MS
     int64_t test_hold_exchange = 0; // DSORT_OPT_TEST_HOLD_EXCHANGE
-    int64_t sub_keys = -1;          // DSORT_OPT_SUB_KEYS: -1 = TILE / 8, 0 = no second level
-    int64_t sub_os = -1;            // DSORT_OPT_SUB_OVERSAMPLE: -1 = 4
+    int64_t sub_keys = -1;          // DSORT_OPT_SUB_KEYS: -1 = 3/16 of a tile, 0 = no second level
+    int64_t sub_os = -1;            // DSORT_OPT_SUB_OVERSAMPLE: -1 = 8 (4 at sub-buckets <= TILE/8)
     int64_t sub_gather = 1;         // DSORT_OPT_SUB_GATHER
 };
 
