@@ -147,8 +147,40 @@ struct BkMap {
     uint32_t mode;  // 0 linear, 1 log
     uint64_t invn;  // 2^48 / n: index -> 16-bit fraction of the input
     uint32_t ids;   // int64: the histogram stores the buckets for the scatter (BkIds)
-    uint32_t pad;
+    uint32_t hot;   // runs of one bucket in the input (sorted, reversed, few keys): a wave's keys
+                    // that share its first key's bucket count with one atomic (bucket_bump)
 };
+
+// The splitters say whether a wave's consecutive keys will mostly share a bucket: the input is
+// sorted or reversed when the splitters' input indices run (nearly) monotone with their order, and
+// has few distinct keys when a quarter of the neighbouring splitters share a key.  Then 64 lanes
+// incrementing one LDS counter serialise (2^30 sorted int32: histogram 3.7 ms, scatter 5.4 ms, 5x and
+// 2x uniform input), and the first level aggregates them; uniform input keeps its plain atomics.
+template <typename T>
+__device__ __forceinline__ uint32_t bucket_runs_hint(uint32_t nasc, uint32_t ndup, int nsp) {
+    if (nsp < 16) return 0;
+    const uint32_t pairs = (uint32_t)(nsp - 1);
+    (void)ndup;  // (few distinct keys or Zipf: a wave holds several such runs -- not aggregated)
+    return (8 * nasc >= 7 * pairs || 8 * nasc <= pairs) ? 1u : 0u;
+}
+// Count (rank) of bucket b for the active lanes of a wave: the lanes in the first active lane's
+// bucket with one atomic, the others one each.  RANK: returns the key's rank in its bucket.
+template <bool RANK>
+__device__ __forceinline__ uint32_t bucket_bump(uint32_t *hist, int b, bool act) {
+    const uint64_t am = __ballot(act);
+    if (!am) return 0u;
+    const int lane = (int)(threadIdx.x & 63), first = (int)__ffsll((long long)am) - 1;
+    const int b0 = __shfl(b, first);
+    const uint64_t same = __ballot(act && b == b0);
+    uint32_t pos = 0, base = 0;
+    if (act && b != b0) pos = atomicAdd(&hist[b], 1u);
+    if (lane == first) base = atomicAdd(&hist[b0], (uint32_t)__popcll(same));
+    if (RANK) {
+        base = (uint32_t)__shfl((int)base, first);
+        if (act && b == b0) pos = base + (uint32_t)__popcll(same & ((1ull << lane) - 1));
+    }
+    return pos;
+}
 // log mode: mantissa bits M, the largest with (KB - M + 1) * 2^M slots in the table
 template <typename T, int SB>
 __host__ __device__ constexpr int log_m() {
@@ -319,13 +351,21 @@ __global__ void __launch_bounds__(BK_MAXB) bucket_slotmap_kernel(const typename 
     for (int i = j; i < 2 * BK_SLOTS; i += blockDim.x) cnt[i / BK_SLOTS][i % BK_SLOTS] = 0;
     if (j < 2) crowd[j] = 0;
     __shared__ uint32_t dup;  // two adjacent splitters of one key: one-key slots
-    if (j == 0) dup = 0;
+    __shared__ uint32_t nasc, ndup;  // neighbouring splitters with ascending input index / one key
+    if (j == 0) dup = nasc = ndup = 0;
+    __syncthreads();
+    if (j + 1 < nsp) {
+        if (CT::idx_of(spl[j]) < CT::idx_of(spl[j + 1])) atomicAdd(&nasc, 1u);
+        if (CT::key_of(spl[j]) == CT::key_of(spl[j + 1])) atomicAdd(&ndup, 1u);
+    }
     const uint64_t invn = ((uint64_t)1 << 48) / (n > 0 ? n : 1);
     BkMap mm[2] = {{0, (uint32_t)(CT::KB - BK_SLOTB), 0, invn, 0, 0}, {0, 0, 1, invn, 0, 0}};
     if (!CT::ADAPT) {
+        __syncthreads();
         if (j == 0) {
             BkMap r = mm[0];
             r.ids = BkIds<T>::ON ? 1u : 0u;  // (int32 with DSORT_BK_IDS32: always)
+            r.hot = bucket_runs_hint<T>(nasc, ndup, nsp);
             *out = r;
         }
         return;
@@ -352,6 +392,7 @@ __global__ void __launch_bounds__(BK_MAXB) bucket_slotmap_kernel(const typename 
     if (j == 0) {
         BkMap r = crowd[1] < crowd[0] ? mm[1] : mm[0];
         r.ids = BkIds<T>::ON && (r.mode == 1 || dup) ? 1u : 0u;
+        r.hot = bucket_runs_hint<T>(nasc, ndup, nsp);
         *out = r;
     }
 }
@@ -497,7 +538,16 @@ __global__ void __launch_bounds__(BK_T, 2) bucket_hist_kernel(const T *__restric
         // the buckets of the thread's keys, two per word (bucket ids: BkIds)
         uint32_t idw[KPT / 2] = {};
         // (the mode branch outside the key loop: a slot array would cost the second workgroup)
-        if (!CT::ADAPT || m.mode == 0) {
+        if (m.hot) {  // (runs of one bucket: aggregated increments, bucket_runs_hint)
+#pragma unroll
+            for (int k = 0; k < KPT; ++k) {
+                const uint64_t i = b0 + (uint64_t)k * BK_T;
+                const uint32_t sl = m.mode == 0 ? slot_mode<T, BK_SLOTB, 0>(m, key[k]) : slot_mode<T, BK_SLOTB, 1>(m, key[k]);
+                const int b = bucket_fast<T, false>(spl, rng, sl, key[k], CT::make(key[k], i + ioff));
+                bucket_bump<false>(hist, b, i < n);
+                if (i < n) idw[k / 2] |= (uint32_t)b << (16 * (k & 1));
+            }
+        } else if (!CT::ADAPT || m.mode == 0) {
 #pragma unroll
             for (int k = 0; k < KPT; ++k) {
                 const uint64_t i = b0 + (uint64_t)k * BK_T;
@@ -789,13 +839,27 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
                 for (int w = 0; w < KPT / 2; ++w) nid[w] = ids[(s0 + SUB) / 2 + (uint64_t)tb * (KPT / 2) + w];
             }
         }
+#ifndef DSORT_HOT_SCATTER
+#define DSORT_HOT_SCATTER 1
+#endif
+        if (DSORT_HOT_SCATTER && m.hot) {  // (runs of one bucket: aggregated ranks, bucket_runs_hint)
 #pragma unroll
-        for (int k = 0; k < KPT; ++k) {
-            const uint64_t i = s0 + tb + (uint64_t)k * BK_T;
-            pk[k] = ~0u;
-            if (i < n) {
+            for (int k = 0; k < KPT; ++k) {
+                const uint64_t i = s0 + tb + (uint64_t)k * BK_T;
+                const bool act = i < n;
                 const int b = IDS ? (int)sl[k] : bucket_fast<T, true>(spl_look, rng, sl[k], key[k], CT::make(key[k], i + ioff));
-                pk[k] = atomicAdd(&hist[b], 1u) | (uint32_t)b << 16;
+                const uint32_t r = bucket_bump<true>(hist, b, act);
+                pk[k] = act ? r | (uint32_t)b << 16 : ~0u;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < KPT; ++k) {
+                const uint64_t i = s0 + tb + (uint64_t)k * BK_T;
+                pk[k] = ~0u;
+                if (i < n) {
+                    const int b = IDS ? (int)sl[k] : bucket_fast<T, true>(spl_look, rng, sl[k], key[k], CT::make(key[k], i + ioff));
+                    pk[k] = atomicAdd(&hist[b], 1u) | (uint32_t)b << 16;
+                }
             }
         }
         __syncthreads();  // A

@@ -185,8 +185,13 @@ __device__ __forceinline__ int sub_of(const Spl<T> *spl, const uint32_t *rng, T 
 // quantile.  Sample g (global index, bucket b's samples at [soff, soff + ns)) is written as the
 // key (smp) and, for int32, as the composite key * 2^32 + g (cmp), whose sort orders the samples
 // by (key, position).  A bucket whose ns is not a multiple of SB_RUN (DSORT_OPT_SUB_OVERSAMPLE
-// not a multiple of 4) samples single keys.
-constexpr uint32_t SB_RUN = 4;
+// not a multiple of 8) samples single keys.  Runs of 8 keys (round 4, at 8 samples per
+// sub-bucket): the kernel fetches a line per run, half the lines of runs of 4 (-0.05 ms per sort
+// at 2^30 int32; no over-tile sub-bucket in 24 sorts).
+#ifndef DSORT_SB_RUN
+#define DSORT_SB_RUN 8
+#endif
+constexpr uint32_t SB_RUN = DSORT_SB_RUN;
 constexpr uint32_t SB_SMP_CH = 1024;  // chunks of a several-piece bucket staged in LDS for its sampling
 __host__ __device__ __forceinline__ uint32_t sample_run(const BInfo &b) { return b.single || b.ns % SB_RUN ? 1u : SB_RUN; }
 // (positions relative to the bucket: bucket_src_pos maps them to the source)
