@@ -143,6 +143,7 @@ struct dsort_ctx {
     size_t small_host_bytes = 0;
     void *bxs = nullptr;    // bucket exchange: this rank's and every rank's splitter samples
     size_t bxs_bytes = 0;
+    const uint32_t *bk_hot = nullptr;  // the last first level's runs flag (device, BkMap.hot)
     hipStream_t xs = nullptr;     // bucket exchange: the comm stream of its sends and receives
     hipEvent_t xev[3] = {};       // ... a wave's receives done (0, 1), the partition done (2)
     int ev_off = 0;               // stage events 1, 7, 8, 13, 14 of the bucket exchange's first

@@ -736,7 +736,7 @@ __global__ void __launch_bounds__(SB_LT<T>, SB_LT<T> / 128) sb_local_kernel(T *_
                                                          const Spl<T> *__restrict__ spl_g,
                                                          const uint32_t *__restrict__ rng_g,
                                                          const SlotFn<T> *__restrict__ sfn,
-                                                         uint32_t *__restrict__ pref) {
+                                                         uint32_t *__restrict__ pref, const uint32_t *__restrict__ hotp) {
     constexpr int LT = SB_LT<T>, KPT = SB_LKPT<T>, CHL = SB_LCH<T>, PER = SB_MAXS / LT;
     static_assert(SB_MAXS % LT == 0, "sub-buckets per thread");
     __shared__ Spl<T> spl[SB_MAXS + 1];
@@ -787,6 +787,9 @@ __global__ void __launch_bounds__(SB_LT<T>, SB_LT<T> / 128) sb_local_kernel(T *_
 #pragma unroll
     for (int q = 0; q < PER; ++q) hist[PER * tid + q] = 0;
     const SlotFn<T> f = sfn[c.b];
+    // sorted or reversed input (the first level's bk::BkMap.hot): a wave's consecutive keys share
+    // a sub-bucket, counted with one atomic (bk::bucket_bump); 2^30 sorted int32 sub level 4.3 -> 2.1 ms
+    const bool hotf = hotp != nullptr && *hotp != 0;
     __syncthreads();
     SBST(0);
     uint32_t pk[KPT];  // sub-bucket | rank << 10
@@ -797,7 +800,15 @@ __global__ void __launch_bounds__(SB_LT<T>, SB_LT<T> / 128) sb_local_kernel(T *_
     // a whole chunk: only the first and last slot rows can fall outside it
     const bool whole = c.len == (uint32_t)CHL;
     if constexpr (G == 1) {
-        if (whole) {  // (no per-key branch in the middle rows)
+        if (hotf) {
+#pragma unroll
+            for (int k = 0; k < KPT; ++k) {
+                const uint32_t s = tid + k * LT;
+                const bool act = s - m < c.len;
+                const int j = act ? sub_of<T>(spl, rng, f.klo, f.sh, key[k], (uint32_t)(c.start + s - m)) : 0;
+                pk[k] = (uint32_t)j | bk::bucket_bump<true>(hist, j, act) << 10;
+            }
+        } else if (whole) {  // (no per-key branch in the middle rows)
 #pragma unroll
             for (int k = 0; k < KPT; ++k) {
                 const uint32_t s = tid + k * LT;
@@ -838,7 +849,8 @@ __global__ void __launch_bounds__(SB_LT<T>, SB_LT<T> / 128) sb_local_kernel(T *_
                 const uint32_t s = tid + (g0 + u) * LT, i = s - m;
                 const int j = sub_pick<T>(spl, r[u], sa[u], sb[u], key[g0 + u], (uint32_t)(c.start + i));
                 // (a key past the chunk adds 0 to a lane-spread counter, not all to one)
-                pk[g0 + u] = (uint32_t)j | atomicAdd(&hist[i < c.len ? j : lane], i < c.len ? 1u : 0u) << 10;
+                if (hotf) pk[g0 + u] = (uint32_t)j | bk::bucket_bump<true>(hist, j, i < c.len) << 10;
+                else pk[g0 + u] = (uint32_t)j | atomicAdd(&hist[i < c.len ? j : lane], i < c.len ? 1u : 0u) << 10;
             }
     }
     }

@@ -1941,7 +1941,7 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         if (nch) {
             if ((rc = stage_event(ctx, s, timed, 13))) return rc;
             hipLaunchKernelGGL(sb_local_kernel<T>, dim3((unsigned)nch), dim3(SB_LT<T>), 0, s, src, dch, dbi, SS, spl, rng,
-                               sfn, cnt);
+                               sfn, cnt, ctx->bk_hot);
             DSORT_HIP(ctx, hipGetLastError());
             if ((rc = stage_event(ctx, s, timed, 14))) return rc;
         }
@@ -2127,6 +2127,7 @@ static int first_level(dsort_ctx *ctx, const T *d_in, uint64_t n, uint64_t ioff,
     hb = static_cast<uint64_t *>(ctx->bucket_host);
     hspl = reinterpret_cast<C *>(hb + BK_MAXB + 1);
     hipLaunchKernelGGL(bucket_slotmap_kernel<T>, dim3(1), dim3(BK_MAXB), 0, s, L.spl, B, n, L.map);
+    ctx->bk_hot = &L.map->hot;
     if ((rc = stage_event(ctx, s, timed, 9))) return rc;
     hipLaunchKernelGGL(bucket_hist_kernel<T>, dim3((unsigned)L.G), dim3(BK_T), 0, s, d_in, n, L.spl, L.map, B, BP,
                        L.subs, L.cnt, ioff, L.ids);
@@ -2166,6 +2167,7 @@ static int first_level(dsort_ctx *ctx, const T *d_in, uint64_t n, uint64_t ioff,
 
 // The stats and events of a bucketed sort start after its nested splitter sort.
 static int bucketed_stats_start(dsort_ctx *ctx, uint64_t n, int tile, hipStream_t s, bool timed) {
+    ctx->bk_hot = nullptr;  // (set by this sort's first level, if it runs one)
     ctx->stats = dsort_stats{};
     ctx->stats.keys_in = ctx->stats.keys_out = n;
     ctx->stats.tile_sort_keys = n;
