@@ -342,3 +342,32 @@ def test_large_buckets_take_16k_tiles(gpu_ctx, kind):
     assert st["sub_scatter_fallback"] == 0
     if kind == "uniform":
         assert st["tile_keys"] == 2 * TILE and st["sub_split_subbuckets"] == 0
+
+
+@pytest.mark.parametrize("dtype", [np.int32, np.int64])
+@pytest.mark.parametrize("kind", ["sorted", "reverse", "noisy", "sawtooth", "sorted_dups"])
+@pytest.mark.parametrize("mode", ["local", "scatter"])
+def test_runs_hint_inputs(gpu_ctx, dtype, kind, mode):
+    """Presorted inputs turn on the runs hint (BkMap.hot, from the splitters' input indices): the
+    histogram, the scatter and the second level's sub-bucket counts (sb_local_kernel) then count a
+    wave's run of one (sub-)bucket with one atomic (bk::bucket_bump).  The hint is only a hint, so
+    inputs that set it but break the runs (1 % of the keys moved, sorted blocks in falling order,
+    long runs of equal keys) must sort exactly too."""
+    rng = np.random.default_rng(len(kind) * 17 + (5 if dtype == np.int64 else 0))
+    info = np.iinfo(dtype)
+    n = (1 << 21) + 333
+    if kind == "sorted_dups":
+        a = np.sort(rng.integers(-40, 40, n)).astype(dtype)
+    else:
+        a = np.sort(rng.integers(info.min, info.max, n, dtype=dtype, endpoint=True))
+    if kind == "reverse":
+        a = a[::-1].copy()
+    elif kind == "noisy":
+        i = rng.integers(0, n, n // 100)
+        a[i] = rng.integers(info.min, info.max, i.size, dtype=dtype, endpoint=True)
+    elif kind == "sawtooth":  # ascending blocks of 2^17 keys, the blocks in descending order
+        blocks = [a[s:s + (1 << 17)] for s in range(0, n, 1 << 17)]
+        a = np.concatenate(blocks[::-1])
+    opts = {"local": dict(), "scatter": dict(sub_gather=0)}[mode]
+    with gpu_ctx.options(buckets=256, **opts):
+        assert np.array_equal(_sort(gpu_ctx, a, False), np.sort(a))
