@@ -91,7 +91,7 @@ template <> struct Comp<int32_t> {
     using U = uint32_t;
     __host__ __device__ static U flip(int32_t key) { return (uint32_t)key ^ 0x80000000u; }
     static constexpr int KB = 32;  // key bits
-    static constexpr bool ADAPT = false;  // fixed top-bit slots, no one-key slots (see BkMap)
+    static constexpr bool ADAPT = false;  // fixed top-bit slots (see BkMap)
 };
 template <> struct Comp<int64_t> {
     using C = Pair;
@@ -136,7 +136,7 @@ __device__ __forceinline__ int bucket_of(const typename Comp<T>::C *spl, int BP,
 //                    skewed keys (Zipf's small heavy integers) get a slot per heavy key and the
 //                    sparse tail shares wide slots.  Under the linear map they all fall in one
 //                    slot and every key binary-searches hundreds of splitters.
-// int32 keeps the fixed map (the top SLOTB bits, ulo = 0) and no one-key slots: its histogram
+// int32 keeps the fixed map (the top SLOTB bits, ulo = 0), one-key slots included: its histogram
 // runs at the HBM rate and the extra lookup work measured +0.5 ms there at 2^30 uniform keys.
 constexpr int BK_SLOTB = 11;
 constexpr int BK_SLOTS = 1 << BK_SLOTB;
@@ -149,6 +149,8 @@ struct BkMap {
     uint32_t ids;   // int64: the histogram stores the buckets for the scatter (BkIds)
     uint32_t hot;   // runs of one bucket in the input (sorted, reversed, few keys): a wave's keys
                     // that share its first key's bucket count with one atomic (bucket_bump)
+    uint32_t one;   // int32: neighbouring splitters share a key, so one-key slots may exist; the
+                    // histogram's usual loop leaves their check out (2^30 uniform: 0.85 -> 0.78 ms)
 };
 
 // The splitters say whether a wave's consecutive keys will mostly share a bucket: the input is
@@ -268,12 +270,14 @@ __device__ __forceinline__ void build_slots(const typename Comp<T>::C *spl, int 
             // int32: lo (bits 0-9), splitters in the slot (bits 10-11: 0, 1, 2 = two or more) and
             // bits 20..1 of the flipped key of the slot's one splitter, or the number of splitters
             // of a crowded slot (bits 12-31): see bucket_fast
+            // (3: a one-key slot of that many splitters)
             const uint32_t in = cnt[1] - cnt[0];
             const uint32_t kb = in == 1 ? ((uint32_t)CT::key_of(spl[cnt[0]]) ^ 0x80000000u) << 11 >> 12 : in;
-            rng[i] = cnt[0] | (in > 2 ? 2u : in) << 10 | kb << 12;
+            const bool one = in >= 2 && CT::key_of(spl[cnt[0]]) == CT::key_of(spl[cnt[1] - 1]);
+            rng[i] = cnt[0] | (one ? 3u : in > 2 ? 2u : in) << 10 | kb << 12;
         } else {
             // a slot whose (>= 2) splitters all hold one key K: see bucket_fast
-            const bool one = CT::ADAPT && cnt[1] >= cnt[0] + 2 && CT::key_of(spl[cnt[0]]) == CT::key_of(spl[cnt[1] - 1]);
+            const bool one = cnt[1] >= cnt[0] + 2 && CT::key_of(spl[cnt[0]]) == CT::key_of(spl[cnt[1] - 1]);
             rng[i] = cnt[0] | (uint32_t)one << 15 | (cnt[1] << 16);
         }
     }
@@ -295,7 +299,25 @@ __device__ __forceinline__ void build_slots(const typename Comp<T>::C *spl, int 
 // to that splitter in bits 31..1 compares its composite; a slot of two or more splitters searches
 // them (their number is in the entry).  (Round 2 read the splitter for every key of a slot
 // that had one: half of the keys, a dependent 8-byte LDS read on the way to the rank atomic.)
-template <typename T, bool PACK>
+template <typename T>
+__device__ __forceinline__ int bucket_onekey(const typename Comp<T>::C *spl, int lo, int hi, T key,
+                                             const typename Comp<T>::C &c) {
+    const typename Comp<T>::C a = spl[lo], z = spl[hi - 1];
+    const T K = Comp<T>::key_of(a);
+    const uint32_t i = Comp<T>::idx_of(c), ia = Comp<T>::idx_of(a), iz = Comp<T>::idx_of(z);
+    if (key != K || i <= ia) return key <= K ? lo : hi;
+    if (i > iz) return hi;
+    // hi - lo - 1 inner buckets over the indices (ia, iz] (the hardware reciprocal: the same
+    // instruction in the histogram and the scatter; IEEE division measured 0.25 ms slower)
+    const float q = (float)(i - ia - 1) * ((float)(hi - lo - 1) * __builtin_amdgcn_rcpf((float)(iz - ia)));
+    const int j = (int)q;
+    return lo + 1 + (j < hi - lo - 2 ? j : hi - lo - 2);
+}
+// int32 (round 4): one-key slots as well -- 16 distinct keys spread over the range put 64
+// splitters of one key in a slot, and every key searched them (2^30: histogram 4.96 ms, scatter
+// 9.0 ms).  The packed entry marks them with splitter count field 3.
+// ONE = false: the caller knows the table has no one-key slot (BkMap.one).
+template <typename T, bool PACK, bool ONE = true>
 __device__ __forceinline__ int bucket_fast(const typename Comp<T>::C *spl, const uint32_t *rng, uint32_t slot,
                                            T key, const typename Comp<T>::C &c) {
     const uint32_t r = rng[slot];
@@ -310,6 +332,7 @@ __device__ __forceinline__ int bucket_fast(const typename Comp<T>::C *spl, const
         if (__builtin_expect(__ballot(slow) == 0, 1)) return j;
         if (!slow) return j;
         int hi = lo + (in == 1 ? 1 : (int)sb);  // (the splitters searched: those of the slot)
+        if (in == 3) return bucket_onekey<T>(spl, lo, hi, key, c);
         while (lo < hi) {
             const int mid = (lo + hi) >> 1;
             if (Comp<T>::lt(spl[mid], c)) lo = mid + 1;
@@ -318,18 +341,7 @@ __device__ __forceinline__ int bucket_fast(const typename Comp<T>::C *spl, const
         return lo;
     }
     int lo = (int)(r & 0x7FFF), hi = (int)(r >> 16);
-    if (Comp<T>::ADAPT && (r & 0x8000)) {
-        const typename Comp<T>::C a = spl[lo], z = spl[hi - 1];
-        const T K = Comp<T>::key_of(a);
-        const uint32_t i = Comp<T>::idx_of(c), ia = Comp<T>::idx_of(a), iz = Comp<T>::idx_of(z);
-        if (key != K || i <= ia) return key <= K ? lo : hi;
-        if (i > iz) return hi;
-        // hi - lo - 1 inner buckets over the indices (ia, iz] (the hardware reciprocal: the same
-        // instruction in the histogram and the scatter; IEEE division measured 0.25 ms slower)
-        const float q = (float)(i - ia - 1) * ((float)(hi - lo - 1) * __builtin_amdgcn_rcpf((float)(iz - ia)));
-        const int j = (int)q;
-        return lo + 1 + (j < hi - lo - 2 ? j : hi - lo - 2);
-    }
+    if (ONE && (r & 0x8000)) return bucket_onekey<T>(spl, lo, hi, key, c);
     while (lo < hi) {  // lower bound among the splitters of the slot
         const int mid = (lo + hi) >> 1;
         if (Comp<T>::lt(spl[mid], c)) lo = mid + 1;
@@ -366,6 +378,7 @@ __global__ void __launch_bounds__(BK_MAXB) bucket_slotmap_kernel(const typename 
             BkMap r = mm[0];
             r.ids = BkIds<T>::ON ? 1u : 0u;  // (int32 with DSORT_BK_IDS32: always)
             r.hot = bucket_runs_hint<T>(nasc, ndup, nsp);
+            r.one = ndup != 0;
             *out = r;
         }
         return;
@@ -393,6 +406,7 @@ __global__ void __launch_bounds__(BK_MAXB) bucket_slotmap_kernel(const typename 
         BkMap r = crowd[1] < crowd[0] ? mm[1] : mm[0];
         r.ids = BkIds<T>::ON && (r.mode == 1 || dup) ? 1u : 0u;
         r.hot = bucket_runs_hint<T>(nasc, ndup, nsp);
+        r.one = 1;
         *out = r;
     }
 }
@@ -547,18 +561,18 @@ __global__ void __launch_bounds__(BK_T, 2) bucket_hist_kernel(const T *__restric
                 bucket_bump<false>(hist, b, i < n);
                 if (i < n) idw[k / 2] |= (uint32_t)b << (16 * (k & 1));
             }
-        } else if (!CT::ADAPT || m.mode == 0) {
+        } else if (CT::ADAPT ? m.mode == 0 : !m.one) {
 #pragma unroll
             for (int k = 0; k < KPT; ++k) {
                 const uint64_t i = b0 + (uint64_t)k * BK_T;
                 const uint32_t sl = slot_mode<T, BK_SLOTB, 0>(m, key[k]);
                 if (i < n) {
-                    const int b = bucket_fast<T, false>(spl, rng, sl, key[k], CT::make(key[k], i + ioff));
+                    const int b = bucket_fast<T, false, CT::ADAPT>(spl, rng, sl, key[k], CT::make(key[k], i + ioff));
                     atomicAdd(&hist[b], 1u);
                     idw[k / 2] |= (uint32_t)b << (16 * (k & 1));
                 }
             }
-        } else {
+        } else {  // (int64 log map; int32 with one-key slots -- its slot_mode ignores the mode)
 #pragma unroll
             for (int k = 0; k < KPT; ++k) {
                 const uint64_t i = b0 + (uint64_t)k * BK_T;
