@@ -371,3 +371,31 @@ def test_runs_hint_inputs(gpu_ctx, dtype, kind, mode):
     opts = {"local": dict(), "scatter": dict(sub_gather=0)}[mode]
     with gpu_ctx.options(buckets=256, **opts):
         assert np.array_equal(_sort(gpu_ctx, a, False), np.sort(a))
+
+
+@pytest.mark.parametrize("order", ["random", "sorted", "reverse"])
+@pytest.mark.parametrize("mode", ["local", "scatter"])
+@pytest.mark.parametrize("B", [256, 1024])
+def test_int32_one_key_slots(gpu_ctx, order, mode, B):
+    """int32 one-key slots (bucket_onekey through the packed entry's field 3 in the scatter and
+    the histogram's flag, BkMap.one): 16 distinct keys spread over the whole range each own a
+    slot of the fixed 11-bit map and a run of buckets; two keys that share a slot, the type's
+    extremes and a thin uniform tail keep the searched and the plain slots busy in the same sort."""
+    rng = np.random.default_rng(B + len(order) * 3 + len(mode))
+    n = (1 << 22) + 4097
+    heavy = (np.arange(16, dtype=np.int64) * (1 << 28) - (1 << 31) + 12345).astype(np.int32)
+    a = rng.choice(heavy, n)
+    r = rng.random(n)
+    a[r < 0.05] = 77  # two keys in one slot (77 and 78)
+    a[(r >= 0.05) & (r < 0.08)] = 78
+    a[(r >= 0.08) & (r < 0.09)] = INT_MIN
+    a[(r >= 0.09) & (r < 0.10)] = INT_MAX
+    tail = r >= 0.97
+    a[tail] = rng.integers(INT_MIN, INT_MAX, int(tail.sum()), endpoint=True)
+    if order != "random":
+        a = np.sort(a)
+        if order == "reverse":
+            a = a[::-1].copy()
+    opts = {"local": dict(), "scatter": dict(sub_gather=0)}[mode]
+    with gpu_ctx.options(buckets=B, **opts):
+        assert np.array_equal(_sort(gpu_ctx, a, False), np.sort(a))
