@@ -90,16 +90,31 @@ def free_port():
     return p
 
 
-def rank_envs(n, port, base=None):
-    """The environment of each of n rank processes (torch.distributed.run's variables)."""
+def rank_envs(n, port, base=None, store=None):
+    """The environment of each of n rank processes (torch.distributed.run's variables).  `store`:
+    a file for the ranks' rendezvous (DSORT_BENCH_STORE), which then needs no TCP port: a port
+    chosen here and bound later by rank 0 can be taken in between (a multi-rank test hung on that
+    in round 4)."""
     base = dict(os.environ if base is None else base)
     out = []
     for r in range(n):
         e = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                  GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                  HSA_ENABLE_IPC_MODE_LEGACY="0")
+        if store:
+            e["DSORT_BENCH_STORE"] = store
         out.append(e)
     return out
+
+
+def init_group(dist, rank, world):
+    """The ranks' gloo group: a file rendezvous when this script spawned them, else torchrun's
+    MASTER_ADDR/MASTER_PORT (env://)."""
+    store = os.environ.get("DSORT_BENCH_STORE")
+    if store:
+        dist.init_process_group("gloo", init_method=f"file://{store}", rank=rank, world_size=world)
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
 
 
 def launch_ranks(n, argv, check_devices=True, timeout_s=1800):
@@ -114,7 +129,8 @@ def launch_ranks(n, argv, check_devices=True, timeout_s=1800):
             print(f"bench: --gpus {n} needs {n} visible GPUs (one rank per GPU), found {ndev}",
                   file=sys.stderr, flush=True)
             return 2
-    envs = rank_envs(n, free_port())
+    tmpd = tempfile.mkdtemp(prefix="dsort_bench_")
+    envs = rank_envs(n, free_port(), store=os.path.join(tmpd, "store"))
     procs = [subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), *argv], env=e) for e in envs]
     rc, t_end = 0, time.time() + timeout_s
     try:
@@ -129,6 +145,9 @@ def launch_ranks(n, argv, check_devices=True, timeout_s=1800):
             if p.poll() is None:
                 p.kill()
             p.wait()
+        import shutil
+
+        shutil.rmtree(tmpd, ignore_errors=True)
     if rc == 0:
         rc = next((p.returncode for p in procs if p.returncode), 0)
     return rc
@@ -538,10 +557,9 @@ def run_multi(args, rank, world):
 
     local = int(os.environ.get("LOCAL_RANK", rank))
     torch.cuda.set_device(local)
-    if world == 1:  # --path samplesort on one GPU without a launcher: a one-rank rendezvous
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", str(free_port()))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if world == 1 and "MASTER_PORT" not in os.environ:  # --path samplesort, one GPU, no launcher
+        os.environ.setdefault("DSORT_BENCH_STORE", os.path.join(tempfile.mkdtemp(prefix="dsort_bench_"), "store"))
+    init_group(dist, rank, world)
     ctx = dsort.Context(local)
     uid = [dsort.Context.unique_id() if rank == 0 else None]
     dist.broadcast_object_list(uid, src=0)
@@ -585,7 +603,7 @@ def run_multi(args, rank, world):
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
     # per-stage device times from as many instrumented steps again (outside the timed region)
     timed = ("exchange_ms", "alltoall_ms", "final_merge_ms", "merge_kernel_ms", "tile_sort_kernel_ms",
-             "bucket_hist_ms", "bucket_scatter_ms", "sub_partition_ms")
+             "bucket_hist_ms", "bucket_scatter_ms", "sub_partition_ms", "total_ms")
     acc = {k: 0.0 for k in timed}
     acc.update({"merge_kernel_launches": 0, "merge_passes": 0, "sent": 0, "tile_sort_keys": 0, "exchange_path": 0})
     for _ in range(args.steps):
@@ -605,7 +623,8 @@ def run_multi(args, rank, world):
     mine = torch.tensor([acc["tile_sort_kernel_ms"] / steps, acc["alltoall_ms"] / steps, acc["exchange_ms"] / steps,
                          acc["final_merge_ms"] / steps, acc["sent"] / steps, sz,
                          acc["bucket_hist_ms"] / steps, acc["bucket_scatter_ms"] / steps,
-                         acc["sub_partition_ms"] / steps, acc["tile_sort_keys"] / steps, acc["exchange_path"]],
+                         acc["sub_partition_ms"] / steps, acc["tile_sort_keys"] / steps, acc["exchange_path"],
+                         acc["total_ms"] / steps],
                         dtype=torch.float64)
     everyone = [torch.zeros_like(mine) for _ in range(world)]
     dist.all_gather(everyone, mine)
@@ -704,6 +723,33 @@ def report_single(args, elapsed, k):
     print(json.dumps(result), flush=True)
 
 
+# columns of run_multi's per-rank rows (report_multi)
+PR_TILE, PR_A2A, PR_EXCH, PR_FINAL, PR_SENT, PR_KEYS, PR_HIST, PR_SCAT, PR_SUB, PR_TKEYS, PR_PATH, PR_TOTAL = range(12)
+
+
+def multi_all_kernels(per_rank, w, world, dist):
+    """SURVEY.md §8d's primary figure at N > 1: every rank's sort kernels' HBM bytes (the PMC table
+    of the one-GPU sort, bytes per key scaled to the rank's keys: a rank runs the same kernels on its
+    chunk and on the keys it receives) plus the exchange's own HBM traffic (the bytes a rank ships
+    are read once and written once at the receiver), over the slowest rank's device time, against
+    the aggregate HBM peak (N x 8 TB/s).  None when there is no PMC table of this key width."""
+    tot, src, match = 0, None, False
+    for r in range(world):
+        pb, src, match = pmc_sort_bytes(int(per_rank[r, PR_KEYS]), w, dist)
+        if pb is None:
+            return None
+        tot += pb + 2 * w * int(per_rank[r, PR_SENT])
+    dev = float(per_rank[:, PR_TOTAL].max())
+    if dev <= 0:
+        return None
+    frac = round(tot / (dev * 1e-3) / 1e9 / (HBM_PEAK_GBS * world), 4)
+    return {"frac": frac, "measured": bool(match),
+            "detail": {"pmc_bytes_all_ranks": int(tot), "device_ms_slowest_rank": round(dev, 3), "pmc_source": src,
+                       "pmc_measured_on_this_build": bool(match),
+                       "rule": "sum over ranks of (PMC bytes per key of the one-GPU sort's kernels x the rank's keys "
+                               "+ 2 x key bytes shipped) / slowest rank's device time / (N x 8 TB/s)"}}
+
+
 def report_multi(args, world, elapsed, per_rank, w):
     result = result_header(args, world)
     n = args.keys
@@ -758,7 +804,17 @@ def report_multi(args, world, elapsed, per_rank, w):
                         "alltoall_ms": round(float(a2a[r]), 4),
                         "exchange_stage_ms": round(float(per_rank[:, 2].max()), 4),
                         ("received_buckets_sort_ms" if bx else "final_merge_ms"): round(float(per_rank[:, 3].max()), 4)}
+    ak = multi_all_kernels(per_rank, w, world, args.dist)
+    if ak:
+        # (measured when the PMC table was taken on this very build and key distribution; else an estimate)
+        roof["all_kernels_frac" if ak["measured"] else "all_kernels_frac_estimate"] = ak["frac"]
+        roof["all_kernels"] = ak["detail"]
+    roof["device_ms_per_rank"] = [round(float(x), 3) for x in per_rank[:, PR_TOTAL]]
     result["roofline"] = roof
+    if not args.no_cpu_baseline and args.dtype == "i32":
+        # the reference's CPU path beside the N-GPU number (rank 0, after the timed region and the
+        # other ranks' exit): the same leg as N = 1
+        result["cpu_baseline"] = cpu_baseline(args.cpu_sample_keys, n)
     print(json.dumps(result), flush=True)
 
 

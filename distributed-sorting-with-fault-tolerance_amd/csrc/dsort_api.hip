@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "dsort_internal.h"
+#include "dsort_tx.h"
 
 #define DSORT_VERSION_STRING "libdsort 0.1 (gfx950, HIP " DSORT_STR(HIP_VERSION_MAJOR) "." DSORT_STR(HIP_VERSION_MINOR) ")"
 #define DSORT_STR2(x) #x
@@ -40,10 +41,21 @@ int hip_err(dsort_ctx *ctx, hipError_t e, const char *what) {
 int ensure(dsort_ctx *ctx, void **buf, size_t *have, size_t need, const char *what) {
     if (need <= *have && *buf) return DSORT_OK;
     if (*buf) {
-        // the old arena may still be used by queued work on any stream of this device
-        hipError_t e = hipDeviceSynchronize();
-        if (e != hipSuccess) return hip_err(ctx, e, "hipDeviceSynchronize (arena grow)");
-        (void)hipFree(*buf);
+        // the old arena may still be used by queued work on any stream of this device.  Inside the
+        // bucket exchange's second level (ctx->poll_waits) the keys are still in flight on the comm
+        // stream, which a dead peer never completes: a device-wide synchronize would hang there, so
+        // wait for the streams that read the arenas (the sort's and the side stream) with polled
+        // waits that see the abort flag and the deadline (the comm stream touches only the
+        // partition and receive buffers, which never grow in that window)
+        if (ctx->poll_waits) {
+            int rc = sync_stream(ctx, ctx->poll_stream, "arena grow (sort stream)");
+            if (!rc && ctx->side) rc = sync_stream(ctx, ctx->side, "arena grow (side stream)");
+            if (rc) return rc;
+        } else {
+            hipError_t e = hipDeviceSynchronize();
+            if (e != hipSuccess) return hip_err(ctx, e, "hipDeviceSynchronize (arena grow)");
+        }
+        release_dev(ctx, *buf);
         *buf = nullptr;
         *have = 0;
     }
@@ -58,10 +70,27 @@ int ensure(dsort_ctx *ctx, void **buf, size_t *have, size_t need, const char *wh
     return DSORT_OK;
 }
 
+void release_dev(dsort_ctx *ctx, void *p) {
+    if (!p) return;
+    if (ctx->poll_waits) ctx->dev_later.push_back(p);
+    else (void)hipFree(p);
+}
+void release_host(dsort_ctx *ctx, void *p) {
+    if (!p) return;
+    if (ctx->poll_waits) ctx->host_later.push_back(p);
+    else (void)hipHostFree(p);
+}
+void flush_later(dsort_ctx *ctx) {
+    for (void *p : ctx->dev_later) (void)hipFree(p);
+    for (void *p : ctx->host_later) (void)hipHostFree(p);
+    ctx->dev_later.clear();
+    ctx->host_later.clear();
+}
+
 // grow-only pinned host buffer
 static int ensure_host(dsort_ctx *ctx, void **buf, size_t *have, size_t need) {
     if (need <= *have && *buf) return DSORT_OK;
-    if (*buf) (void)hipHostFree(*buf);
+    if (*buf) release_host(ctx, *buf);
     *buf = nullptr;
     *have = 0;
     if (hipHostMalloc(buf, need, hipHostMallocDefault) != hipSuccess) {
@@ -407,15 +436,27 @@ static void exchange_fault_point(dsort_ctx *ctx, int stage) {
     if (ctx->opt.kill_in_exchange == stage) raise(SIGKILL);
 }
 
+// DSORT_OPT_TEST_FAIL_EXCHANGE = k (host transport): a local error of this rank right before its
+// k-th collective (0 = the key-count all-gather), returned like any other local error -- the
+// sequence's guard reports it to the peers at the next gate (dsort_tx.h)
+static int tx_fault_point(dsort_ctx *ctx) {
+    if (ctx->tx && ctx->opt.test_fail_exchange >= 0 && ctx->opt.test_fail_exchange == ctx->tx->collectives_done())
+        return set_err(ctx, DSORT_EHIP, "injected local failure before collective " +
+                                            std::to_string(ctx->opt.test_fail_exchange) +
+                                            " of the exchange (DSORT_OPT_TEST_FAIL_EXCHANGE)");
+    return DSORT_OK;
+}
+
 // All-gather of `count` uint64 per rank (RCCL through the context's small device buffer, or the
 // host transport): out[r * count + i] = rank r's src[i].
 static int allgather_u64(dsort_ctx *ctx, const uint64_t *src, size_t count, uint64_t *out, hipStream_t s,
                          double deadline, const char *what) {
     const int P = ctx->nranks;
     if (ctx->has_transport) {
-        if (ctx->transport.allgather(ctx->transport.user, src, out, count * 8))
-            return set_err(ctx, DSORT_ECOMM, std::string("host transport allgather (") + what + ") failed");
-        return DSORT_OK;
+        if (!ctx->tx) return set_err(ctx, DSORT_EINVAL, std::string(what) + ": no sample sort running");
+        if (int rc_ = tx_fault_point(ctx)) return rc_;
+        const int rc = ctx->tx->allgather(src, out, count * 8, what);
+        return rc ? set_err(ctx, rc, ctx->tx->error()) : DSORT_OK;
     }
     const size_t bytes = count * 8 * (size_t)(P + 1);
     int rc = ensure(ctx, &ctx->small, &ctx->small_bytes, bytes, "sample-sort small buffers");
@@ -465,6 +506,9 @@ static int sample_sort_bx(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, T **d
                           double deadline) {
     const int P = pl.P, me = pl.me, Bl = pl.Bl, Bt = pl.Btot;
     const bool host_tx = ctx->has_transport;
+    // The exchange in W waves of this rank's buckets (two or more buckets: W = 2), see step 4
+    const int W = Bl >= 2 ? 2 : 1;
+    if (host_tx) ctx->tx->plan(2 + W);  // samples, bucket starts, the waves (dsort_tx.h)
     const size_t rec = (size_t)pl.s_max * sizeof(BxSample);
     int rc = ensure(ctx, &ctx->bxs, &ctx->bxs_bytes, rec * (size_t)(P + 1), "bucket-exchange samples");
     if (rc) return rc;
@@ -482,8 +526,8 @@ static int sample_sort_bx(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, T **d
         DSORT_HIP(ctx, hipMemcpyAsync(hm, mine, rec, hipMemcpyDeviceToHost, s));
         rc = exch_wait(ctx, s, true, deadline, "samples");
         if (rc) return rc;
-        if (ctx->transport.allgather(ctx->transport.user, hm, ha, rec))
-            return set_err(ctx, DSORT_ECOMM, "host transport allgather (samples) failed");
+        if ((rc = tx_fault_point(ctx))) return rc;
+        if ((rc = ctx->tx->allgather(hm, ha, rec, "samples all-gather"))) return set_err(ctx, rc, ctx->tx->error());
         DSORT_HIP(ctx, hipMemcpyAsync(all, ha, rec * (size_t)P, hipMemcpyHostToDevice, s));
     }
     exchange_fault_point(ctx, 1);
@@ -509,7 +553,6 @@ static int sample_sort_bx(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, T **d
     // while wave 1's keys are on the links (the sends and receives go on the comm stream; the sort
     // stream waits for each wave's event).  (The host transport and a single rank run the same waves
     // one after the other: the same layout and second-level calls as the 8-GPU run.)
-    const int W = Bl >= 2 ? 2 : 1;
     const int jb[3] = {0, W == 2 ? Bl / 2 : Bl, Bl};
     const uint64_t *hme = hb_all.data() + (size_t)me * (Bt + 1);
     auto hof = [&](int r) { return hb_all.data() + (size_t)r * (Bt + 1); };
@@ -609,9 +652,10 @@ static int sample_sort_bx(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, T **d
                     hi = std::max<uint64_t>(hi, rpos[k] + rcnt[k]);
                 }
             }
-            if (ctx->transport.alltoallv(ctx->transport.user, ctx->xfer, sc.data(), sd.data(), ctx->xfer2, rcn.data(),
-                                         rd.data()))
-                return set_err(ctx, DSORT_ECOMM, "host transport alltoallv (keys) failed");
+            if ((rc = tx_fault_point(ctx))) return rc;
+            if ((rc = ctx->tx->alltoallv(ctx->xfer, sc.data(), sd.data(), ctx->xfer2, rcn.data(), rd.data(),
+                                         w ? "key all-to-all (wave 1)" : "key all-to-all (wave 0)")))
+                return set_err(ctx, rc, ctx->tx->error());
             if (hi > lo)
                 DSORT_HIP(ctx, hipMemcpyAsync(rb + lo, static_cast<char *>(ctx->xfer2) + (lo - shift) * sizeof(T),
                                               (hi - lo) * sizeof(T), hipMemcpyHostToDevice, s));
@@ -624,6 +668,7 @@ static int sample_sort_bx(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, T **d
     T *outp = static_cast<T *>(ctx->recv2);
     ctx->poll_waits = !host_tx;
     ctx->poll_deadline = deadline;
+    ctx->poll_stream = s;
     uint64_t out_off = 0;
     for (int w = 0; w < W && !rc; ++w) {
         if (!host_tx) {
@@ -649,6 +694,7 @@ static int sample_sort_bx(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, T **d
     // the receives have landed (and the test hold, DSORT_OPT_TEST_HOLD_EXCHANGE, is released)
     rc = exch_wait(ctx, cs, true, deadline, "key all-to-all", ctx->opt.test_hold_exchange != 0);
     if (rc) return rc;
+    flush_later(ctx);  // (the buffers the second level replaced while the keys were in flight)
     ctx->last_stream = s;
     ctx->stats.keys_in = pl.n_local;
     ctx->stats.keys_out = nrecv;
@@ -675,6 +721,20 @@ static int sample_sort(dsort_ctx *ctx, const T *d_in, size_t n_local, T **d_out,
     const int P = ctx->nranks, me = ctx->rank, S = kSamplesPerRank;
     const bool host_tx = ctx->has_transport;
     int rc;
+    // host transport: the sequence of collectives with its gates (dsort_tx.h); leaving this call
+    // before the last collective on any error reports the failure to the peers at the next gate
+    // (the guard), so none of them blocks in a collective this rank never joins.  The first
+    // collective is the key-count all-gather (the presorted entry starts with the samples).
+    TxSeq txs(ctx->transport, P, deadline, presorted ? 3 : 1);
+    struct TxScope {
+        dsort_ctx *c;
+        ~TxScope() { c->tx = nullptr; }
+    } tx_scope{ctx};
+    TxGuard tx_guard;
+    if (host_tx) {
+        ctx->tx = &txs;
+        tx_guard.seq = &txs;
+    }
     if (!presorted) {
         // every rank's key count decides the path, the same on every rank: the bucket exchange, or
         // (small inputs, partition switched off) sort locally and merge the received runs
@@ -684,12 +744,13 @@ static int sample_sort(dsort_ctx *ctx, const T *d_in, size_t n_local, T **d_out,
         if (rc) return rc;
         BxPlan pl;
         if (bx_make_plan(ctx->opt, P, me, n_of.data(), (int)sizeof(T), pl)) {
-            ctx->stats = dsort_stats{};
+            ctx->stats = fresh_stats();
             return sample_sort_bx<T>(ctx, d_in, pl, d_out, n_out, s, deadline);
         }
+        if (host_tx) txs.plan(3);  // samples, count matrix, keys
     }
     const T *d_keys;
-    dsort_stats st{};
+    dsort_stats st = fresh_stats();
     if (presorted) {
         // the caller already holds a sorted local run (fault recovery: a survivor merged the
         // chunks it sorted)
@@ -761,8 +822,8 @@ static int sample_sort(dsort_ctx *ctx, const T *d_in, size_t n_local, T **d_out,
         rc = exch_wait(ctx, s, true, deadline, "local sort");
         if (rc) return rc;
         memcpy(mine + (size_t)S * sizeof(T), &nl, 8);
-        if (ctx->transport.allgather(ctx->transport.user, mine, all, rec))
-            return set_err(ctx, DSORT_ECOMM, "host transport allgather (samples) failed");
+        if ((rc = tx_fault_point(ctx))) return rc;
+        if ((rc = txs.allgather(mine, all, rec, "samples all-gather"))) return set_err(ctx, rc, txs.error());
         for (int r = 0; r < P; ++r) {
             memcpy(hsm + off_all + (size_t)r * S * sizeof(T), all + (size_t)r * rec, (size_t)S * sizeof(T));
             memcpy(hsm + off_n + (size_t)r * 8, all + (size_t)r * rec + (size_t)S * sizeof(T), 8);
@@ -804,8 +865,9 @@ static int sample_sort(dsort_ctx *ctx, const T *d_in, size_t n_local, T **d_out,
         DSORT_HIP(ctx, hipMemcpyAsync(hsm + off_mat, dsm + off_mat, (size_t)P * P * 8, hipMemcpyDeviceToHost, s));
         rc = exch_wait(ctx, s, true, deadline, "count all-gather");
         if (rc) return rc;
-    } else if (ctx->transport.allgather(ctx->transport.user, hcnt, hsm + off_mat, (size_t)P * 8)) {
-        return set_err(ctx, DSORT_ECOMM, "host transport allgather (counts) failed");
+    } else {
+        if ((rc = tx_fault_point(ctx))) return rc;
+        if ((rc = txs.allgather(hcnt, hsm + off_mat, (size_t)P * 8, "count all-gather"))) return set_err(ctx, rc, txs.error());
     }
     const uint64_t *mat = reinterpret_cast<const uint64_t *>(hsm + off_mat);  // mat[src*P + dst]
     std::vector<size_t> rlen(P);
@@ -862,9 +924,9 @@ static int sample_sort(dsort_ctx *ctx, const T *d_in, size_t n_local, T **d_out,
             rcn[r] = rlen[r] * sizeof(T);
             rd[r] = roff[r] * sizeof(T);
         }
-        if (ctx->transport.alltoallv(ctx->transport.user, ctx->xfer, sc.data(), sd.data(), ctx->xfer2,
-                                     rcn.data(), rd.data()))
-            return set_err(ctx, DSORT_ECOMM, "host transport alltoallv (keys) failed");
+        if ((rc = tx_fault_point(ctx))) return rc;
+        if ((rc = txs.alltoallv(ctx->xfer, sc.data(), sd.data(), ctx->xfer2, rcn.data(), rd.data(), "key all-to-all")))
+            return set_err(ctx, rc, txs.error());
         if (nrecv) DSORT_HIP(ctx, hipMemcpyAsync(rb, ctx->xfer2, nrecv * sizeof(T), hipMemcpyHostToDevice, s));
         if (ctx->ev_ok) {
             DSORT_HIP(ctx, hipEventRecord(ctx->ev[6], s));
@@ -946,6 +1008,8 @@ int dsort_finalize(dsort_ctx *ctx) {
         ncclCommAbort(ctx->comm);  // peers may be gone: never wait for them here
         ctx->comm = nullptr;
     }
+    ctx->poll_waits = false;
+    flush_later(ctx);
     void *bufs[] = {ctx->scratch, ctx->scratch2, ctx->splits, ctx->groups, ctx->io, ctx->io2, ctx->red,
                     ctx->local, ctx->recv, ctx->recv2, ctx->small, ctx->text_status,
                     ctx->bucket, ctx->sub, ctx->sub_alt, ctx->stmp, ctx->bxs, ctx->tfb};
@@ -1027,6 +1091,10 @@ int dsort_set_option(dsort_ctx *ctx, int option, int64_t v) {
             if (v != 0 && v != 1) return set_err(ctx, DSORT_EINVAL, "DSORT_OPT_TEST_HOLD_EXCHANGE: 0 or 1");
             o.test_hold_exchange = v;
             return DSORT_OK;
+        case DSORT_OPT_TEST_FAIL_EXCHANGE:
+            if (v < -1) return set_err(ctx, DSORT_EINVAL, "DSORT_OPT_TEST_FAIL_EXCHANGE: -1 or a collective index");
+            o.test_fail_exchange = v;
+            return DSORT_OK;
         default:
             return set_err(ctx, DSORT_EINVAL, "unknown option " + std::to_string(option));
     }
@@ -1044,6 +1112,7 @@ int dsort_get_option(const dsort_ctx *ctx, int option, int64_t *v) {
         case DSORT_OPT_KILL_IN_EXCHANGE: *v = o.kill_in_exchange; return DSORT_OK;
         case DSORT_OPT_COMM_TIMEOUT_MS: *v = o.comm_timeout_ms; return DSORT_OK;
         case DSORT_OPT_TEST_HOLD_EXCHANGE: *v = o.test_hold_exchange; return DSORT_OK;
+        case DSORT_OPT_TEST_FAIL_EXCHANGE: *v = o.test_fail_exchange; return DSORT_OK;
         case DSORT_OPT_SUB_KEYS: *v = o.sub_keys; return DSORT_OK;
         case DSORT_OPT_SUB_OVERSAMPLE: *v = o.sub_os; return DSORT_OK;
         case DSORT_OPT_SUB_GATHER: *v = o.sub_gather; return DSORT_OK;
@@ -1212,6 +1281,12 @@ int dsort_comm_init_transport(dsort_ctx *ctx, int nranks, int rank, const dsort_
     ctx->has_transport = true;
     ctx->nranks = nranks;
     ctx->rank = rank;
+    return DSORT_OK;
+}
+
+int dsort_comm_deadline_ms(const dsort_ctx *ctx, int64_t *remaining_ms) {
+    if (!ctx || !remaining_ms) return DSORT_EINVAL;
+    *remaining_ms = ctx->tx ? ctx->tx->remaining_ms() : -1;
     return DSORT_OK;
 }
 

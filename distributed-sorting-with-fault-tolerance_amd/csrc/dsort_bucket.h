@@ -151,6 +151,10 @@ struct BkMap {
                     // that share its first key's bucket count with one atomic (bucket_bump)
     uint32_t one;   // int32: neighbouring splitters share a key, so one-key slots may exist; the
                     // histogram's usual loop leaves their check out (2^30 uniform: 0.85 -> 0.78 ms)
+    uint32_t ad;    // int32 (round 5): the adaptive map (ulo, sh, mode as int64's) instead of the fixed
+                    // top-11-bit slots, when those crowd many splitters of several keys into one slot
+                    // (many small keys: the reference's input.txt holds only 1..100).  The host reads
+                    // it back and launches the kernels' adaptive instances (first_level)
 };
 
 // The splitters say whether a wave's consecutive keys will mostly share a bucket: the input is
@@ -191,12 +195,13 @@ __host__ __device__ constexpr int log_m() {
     return m;
 }
 
-template <typename T, int SB, int MODE>
+// ADP: the map of the sort is adaptive (int64 always; int32 when BkMap.ad, see bucket_slotmap_kernel)
+template <typename T, int SB, int MODE, bool ADP = Comp<T>::ADAPT>
 __host__ __device__ __forceinline__ uint32_t slot_mode(const BkMap &m, T key) {
     using U = typename Comp<T>::U;
     constexpr uint32_t NS = 1u << SB;
     constexpr int M = log_m<T, SB>();
-    if (!Comp<T>::ADAPT) return Comp<T>::slot_of(key, SB);
+    if (!ADP) return Comp<T>::slot_of(key, SB);
     const U u = Comp<T>::flip(key);
     const U d = u < (U)m.ulo ? (U)0 : (U)(u - (U)m.ulo);
     if (MODE == 0) {
@@ -207,19 +212,19 @@ __host__ __device__ __forceinline__ uint32_t slot_mode(const BkMap &m, T key) {
     const int e = (int)(sizeof(U) * 8) - (sizeof(U) == 8 ? __builtin_clzll((uint64_t)d) : __builtin_clz((uint32_t)d));
     return (uint32_t)(e - M) << M | ((uint32_t)(d >> (e - 1 - M)) & ((1u << M) - 1));
 }
-template <typename T, int SB = BK_SLOTB>
+template <typename T, int SB = BK_SLOTB, bool ADP = Comp<T>::ADAPT>
 __host__ __device__ __forceinline__ uint32_t slot_at(const BkMap &m, T key) {
-    return m.mode == 0 ? slot_mode<T, SB, 0>(m, key) : slot_mode<T, SB, 1>(m, key);
+    return m.mode == 0 ? slot_mode<T, SB, 0, ADP>(m, key) : slot_mode<T, SB, 1, ADP>(m, key);
 }
 // the slots of K keys, the (workgroup-uniform) mode branch taken once
-template <typename T, int K>
+template <typename T, int K, bool ADP = Comp<T>::ADAPT>
 __device__ __forceinline__ void slots_at(const BkMap &m, const T (&key)[K], uint32_t (&sl)[K]) {
-    if (!Comp<T>::ADAPT || m.mode == 0) {
+    if (!ADP || m.mode == 0) {
 #pragma unroll
-        for (int k = 0; k < K; ++k) sl[k] = slot_mode<T, BK_SLOTB, 0>(m, key[k]);
+        for (int k = 0; k < K; ++k) sl[k] = slot_mode<T, BK_SLOTB, 0, ADP>(m, key[k]);
     } else {
 #pragma unroll
-        for (int k = 0; k < K; ++k) sl[k] = slot_mode<T, BK_SLOTB, 1>(m, key[k]);
+        for (int k = 0; k < K; ++k) sl[k] = slot_mode<T, BK_SLOTB, 1, ADP>(m, key[k]);
     }
 }
 
@@ -246,8 +251,8 @@ __host__ __device__ __forceinline__ bool slot_first(const BkMap &m, uint32_t i, 
     return true;
 }
 
-// PACK (int32 only): the packed entry of bucket_fast's first branch (the scatter's table)
-template <typename T, bool PACK, int SB = BK_SLOTB>
+// PACK (int32 on the fixed map only): the packed entry of bucket_fast's first branch (the scatter's table)
+template <typename T, bool PACK, int SB = BK_SLOTB, bool ADP = Comp<T>::ADAPT>
 __device__ __forceinline__ void build_slots(const typename Comp<T>::C *spl, int BP, const BkMap &m,
                                             uint32_t *rng) {
     using CT = Comp<T>;
@@ -266,7 +271,7 @@ __device__ __forceinline__ void build_slots(const typename Comp<T>::C *spl, int 
                 cnt[e] = (uint32_t)bucket_of<T>(spl, BP, c);
             }
         }
-        if constexpr (!CT::ADAPT && PACK) {
+        if constexpr (!ADP && PACK) {
             // int32: lo (bits 0-9), splitters in the slot (bits 10-11: 0, 1, 2 = two or more) and
             // bits 20..1 of the flipped key of the slot's one splitter, or the number of splitters
             // of a crowded slot (bits 12-31): see bucket_fast
@@ -317,11 +322,11 @@ __device__ __forceinline__ int bucket_onekey(const typename Comp<T>::C *spl, int
 // splitters of one key in a slot, and every key searched them (2^30: histogram 4.96 ms, scatter
 // 9.0 ms).  The packed entry marks them with splitter count field 3.
 // ONE = false: the caller knows the table has no one-key slot (BkMap.one).
-template <typename T, bool PACK, bool ONE = true>
+template <typename T, bool PACK, bool ONE = true, bool ADP = Comp<T>::ADAPT>
 __device__ __forceinline__ int bucket_fast(const typename Comp<T>::C *spl, const uint32_t *rng, uint32_t slot,
                                            T key, const typename Comp<T>::C &c) {
     const uint32_t r = rng[slot];
-    if constexpr (!Comp<T>::ADAPT && PACK) {
+    if constexpr (!ADP && PACK) {
         // branch-free on the usual path; the rare keys that search take one wave-uniform branch
         // (per-key early returns doubled the histogram's branches and cost it 0.2 ms at 2^30)
         int lo = (int)(r & 1023);
@@ -372,13 +377,49 @@ __global__ void __launch_bounds__(BK_MAXB) bucket_slotmap_kernel(const typename 
     }
     const uint64_t invn = ((uint64_t)1 << 48) / (n > 0 ? n : 1);
     BkMap mm[2] = {{0, (uint32_t)(CT::KB - BK_SLOTB), 0, invn, 0, 0}, {0, 0, 1, invn, 0, 0}};
-    if (!CT::ADAPT) {
+    if constexpr (!CT::ADAPT) {
+        // int32: the fixed map (the packed lookup) unless it puts more than AD_MIX splitters of
+        // several keys into one slot -- every key there binary-searches them, from global memory in
+        // the scatter (2^30 keys of 1..100: 19.8 ms).  Then the adaptive map of int64 (linear over
+        // the splitters' range, or log) with one-key slots, if its most crowded such slot is smaller.
+        // The cost of a map: its largest slot of splitters of at least two keys (a slot of one key is
+        // a one-key slot: no search).
+        constexpr uint32_t AD_MIX = 8;
+        __shared__ uint32_t tot[3][BK_SLOTS], dst[3][BK_SLOTS];
+        __shared__ uint32_t cost[3];
+        for (int i = j; i < 3 * BK_SLOTS; i += blockDim.x) tot[i / BK_SLOTS][i % BK_SLOTS] = dst[i / BK_SLOTS][i % BK_SLOTS] = 0;
+        if (j < 3) cost[j] = 0;
+        BkMap am[3] = {mm[0], mm[0], mm[1]};  // fixed, adaptive linear, adaptive log
+        if (nsp >= 1) {
+            const uint32_t lo = CT::flip(CT::key_of(spl[0])), hi = CT::flip(CT::key_of(spl[nsp - 1]));
+            const uint32_t r = hi - lo;
+            const int bits = r == 0 ? 0 : 32 - __builtin_clz(r);
+            am[1] = BkMap{(uint64_t)lo, (uint32_t)(bits > BK_SLOTB ? bits - BK_SLOTB : 0), 0, invn, 0, 0};
+            am[2] = BkMap{(uint64_t)lo, 0, 1, invn, 0, 0};
+        }
+        __syncthreads();
+        if (j < nsp) {
+            const T k = CT::key_of(spl[j]);
+            const bool first = j == 0 || CT::key_of(spl[j - 1]) != k;
+            const uint32_t sl[3] = {slot_mode<T, BK_SLOTB, 0, false>(am[0], k), slot_mode<T, BK_SLOTB, 0, true>(am[1], k),
+                                    slot_mode<T, BK_SLOTB, 1, true>(am[2], k)};
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                atomicAdd(&tot[q][sl[q]], 1u);
+                if (first) atomicAdd(&dst[q][sl[q]], 1u);
+            }
+        }
+        __syncthreads();
+        for (int i = j; i < 3 * BK_SLOTS; i += blockDim.x)
+            if (dst[i / BK_SLOTS][i % BK_SLOTS] >= 2) atomicMax(&cost[i / BK_SLOTS], tot[i / BK_SLOTS][i % BK_SLOTS]);
         __syncthreads();
         if (j == 0) {
-            BkMap r = mm[0];
+            const int q = cost[0] <= AD_MIX ? 0 : cost[2] < cost[1] ? 2 : 1;
+            BkMap r = q == 0 || cost[q] < cost[0] ? am[q] : am[0];
+            r.ad = r.ulo != 0 || r.mode != 0 || r.sh != (uint32_t)(CT::KB - BK_SLOTB) ? 1u : 0u;
             r.ids = BkIds<T>::ON ? 1u : 0u;  // (int32 with DSORT_BK_IDS32: always)
             r.hot = bucket_runs_hint<T>(nasc, ndup, nsp);
-            r.one = ndup != 0;
+            r.one = r.ad ? 1u : (ndup != 0);
             *out = r;
         }
         return;
@@ -508,14 +549,16 @@ __host__ __forceinline__ int bucket_wg_subs(uint64_t n) {
 
 // counts[g * B + b] = keys of workgroup g's subs sub-tiles in bucket b.  (The same slot table as
 // the scatter's: the one-key slots must agree.)  ioff: the composite index of in[0] (the multi-GPU
-// path: this rank's first key in the global order; 0 on one GPU).
-template <typename T>
+// path: this rank's first key in the global order; 0 on one GPU).  AD (int32): the instance of the
+// adaptive map (BkMap.ad; the host launches the one the slot map chose).
+template <typename T, bool AD = false>
 __global__ void __launch_bounds__(BK_T, 2) bucket_hist_kernel(const T *__restrict__ in, uint64_t n,
                                                               const typename Comp<T>::C *__restrict__ spl_g,
                                                               const BkMap *__restrict__ map, int B, int BP,
                                                               int subs, uint32_t *__restrict__ counts,
                                                               uint64_t ioff, uint32_t *__restrict__ ids) {
     using CT = Comp<T>;
+    constexpr bool ADP = CT::ADAPT || AD;
     constexpr int KPT = Geo<T>::KPT, SUB = BK_T * KPT;
     static_assert(!BkIds<T>::ON || KPT % 2 == 0, "bucket ids two per word");
     __shared__ typename CT::C spl[BK_MAXB + 1];
@@ -525,7 +568,7 @@ __global__ void __launch_bounds__(BK_T, 2) bucket_hist_kernel(const T *__restric
     load_splitters<T>(spl_g, BP, spl);
     for (int b = threadIdx.x; b < B; b += BK_T) hist[b] = 0;
     __syncthreads();
-    build_slots<T, false>(spl, BP, m, rng);  // (the packed table measured 0.78 -> 0.93 ms here)
+    build_slots<T, false, BK_SLOTB, ADP>(spl, BP, m, rng);  // (the packed table measured 0.78 -> 0.93 ms here)
     __syncthreads();
     const uint64_t g0 = (uint64_t)blockIdx.x * subs * SUB;
     // the next sub-tile's keys are loaded while the current one is counted (two workgroups per CU
@@ -556,18 +599,18 @@ __global__ void __launch_bounds__(BK_T, 2) bucket_hist_kernel(const T *__restric
 #pragma unroll
             for (int k = 0; k < KPT; ++k) {
                 const uint64_t i = b0 + (uint64_t)k * BK_T;
-                const uint32_t sl = m.mode == 0 ? slot_mode<T, BK_SLOTB, 0>(m, key[k]) : slot_mode<T, BK_SLOTB, 1>(m, key[k]);
-                const int b = bucket_fast<T, false>(spl, rng, sl, key[k], CT::make(key[k], i + ioff));
+                const uint32_t sl = m.mode == 0 ? slot_mode<T, BK_SLOTB, 0, ADP>(m, key[k]) : slot_mode<T, BK_SLOTB, 1, ADP>(m, key[k]);
+                const int b = bucket_fast<T, false, true, ADP>(spl, rng, sl, key[k], CT::make(key[k], i + ioff));
                 bucket_bump<false>(hist, b, i < n);
                 if (i < n) idw[k / 2] |= (uint32_t)b << (16 * (k & 1));
             }
-        } else if (CT::ADAPT ? m.mode == 0 : !m.one) {
+        } else if (ADP ? m.mode == 0 : !m.one) {
 #pragma unroll
             for (int k = 0; k < KPT; ++k) {
                 const uint64_t i = b0 + (uint64_t)k * BK_T;
-                const uint32_t sl = slot_mode<T, BK_SLOTB, 0>(m, key[k]);
+                const uint32_t sl = slot_mode<T, BK_SLOTB, 0, ADP>(m, key[k]);
                 if (i < n) {
-                    const int b = bucket_fast<T, false, CT::ADAPT>(spl, rng, sl, key[k], CT::make(key[k], i + ioff));
+                    const int b = bucket_fast<T, false, ADP, ADP>(spl, rng, sl, key[k], CT::make(key[k], i + ioff));
                     atomicAdd(&hist[b], 1u);
                     idw[k / 2] |= (uint32_t)b << (16 * (k & 1));
                 }
@@ -576,9 +619,9 @@ __global__ void __launch_bounds__(BK_T, 2) bucket_hist_kernel(const T *__restric
 #pragma unroll
             for (int k = 0; k < KPT; ++k) {
                 const uint64_t i = b0 + (uint64_t)k * BK_T;
-                const uint32_t sl = slot_mode<T, BK_SLOTB, 1>(m, key[k]);
+                const uint32_t sl = slot_mode<T, BK_SLOTB, 1, ADP>(m, key[k]);
                 if (i < n) {
-                    const int b = bucket_fast<T, false>(spl, rng, sl, key[k], CT::make(key[k], i + ioff));
+                    const int b = bucket_fast<T, false, true, ADP>(spl, rng, sl, key[k], CT::make(key[k], i + ioff));
                     atomicAdd(&hist[b], 1u);
                     idw[k / 2] |= (uint32_t)b << (16 * (k & 1));
                 }
@@ -754,7 +797,7 @@ __device__ unsigned long long g_bkstamps[8192 * 16];
 // IDS: the variant that reads the histogram's buckets (BkIds).  The host launches both variants for
 // int64 (it does not know the map's choice); the one that does not match m.ids returns at once
 // (one kernel with a run-time branch: uniform int64 scatter 5.29 -> 5.84 ms).
-template <typename T, bool IDS>
+template <typename T, bool IDS, bool AD = false>
 __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__restrict__ in, uint64_t n,
                                                                     const typename Comp<T>::C *__restrict__ spl_g,
                                                                     const BkMap *__restrict__ map, int B, int BP, int subs,
@@ -762,6 +805,7 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
                                                                     T *__restrict__ out, T *__restrict__ out2,
                                                                     uint64_t ioff, const uint32_t *__restrict__ ids) {
     using CT = Comp<T>;
+    constexpr bool ADP = CT::ADAPT || AD;  // (AD: int32's adaptive-map instance, BkMap.ad)
     static_assert(!IDS || BkIds<T>::ON, "bucket ids of this key width");
     using G = LineGeo<T>;
     using V = typename std::conditional<sizeof(T) == 4, int4, longlong2>::type;
@@ -808,7 +852,7 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
     if (!IDS) {
         load_splitters<T>(spl_g, BP, spl);
         __syncthreads();
-        build_slots<T, true>(spl, BP, m, rng);
+        build_slots<T, true, BK_SLOTB, ADP>(spl, BP, m, rng);
     }
     __syncthreads();
     const uint64_t g0 = (uint64_t)g * subs * SUB;
@@ -840,7 +884,7 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
 #pragma unroll
             for (int k = 0; k < KPT; ++k) sl[k] = (nid[k / 2] >> (16 * (k & 1))) & 0xFFFFu;
         } else {
-            slots_at<T, KPT>(m, key, sl);
+            slots_at<T, KPT, ADP>(m, key, sl);
         }
         if (!last) {
 #pragma unroll
@@ -861,7 +905,7 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
             for (int k = 0; k < KPT; ++k) {
                 const uint64_t i = s0 + tb + (uint64_t)k * BK_T;
                 const bool act = i < n;
-                const int b = IDS ? (int)sl[k] : bucket_fast<T, true>(spl_look, rng, sl[k], key[k], CT::make(key[k], i + ioff));
+                const int b = IDS ? (int)sl[k] : bucket_fast<T, true, true, ADP>(spl_look, rng, sl[k], key[k], CT::make(key[k], i + ioff));
                 const uint32_t r = bucket_bump<true>(hist, b, act);
                 pk[k] = act ? r | (uint32_t)b << 16 : ~0u;
             }
@@ -871,7 +915,7 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
                 const uint64_t i = s0 + tb + (uint64_t)k * BK_T;
                 pk[k] = ~0u;
                 if (i < n) {
-                    const int b = IDS ? (int)sl[k] : bucket_fast<T, true>(spl_look, rng, sl[k], key[k], CT::make(key[k], i + ioff));
+                    const int b = IDS ? (int)sl[k] : bucket_fast<T, true, true, ADP>(spl_look, rng, sl[k], key[k], CT::make(key[k], i + ioff));
                     pk[k] = atomicAdd(&hist[b], 1u) | (uint32_t)b << 16;
                 }
             }

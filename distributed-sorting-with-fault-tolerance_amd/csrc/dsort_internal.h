@@ -14,6 +14,9 @@
 #include "dsort.h"
 
 struct ncclComm;
+namespace dsort {
+class TxSeq;
+}
 
 namespace dsort {
 
@@ -60,6 +63,7 @@ struct dsort_opts {
     int64_t kill_in_exchange = -1;  // DSORT_OPT_KILL_IN_EXCHANGE
     int64_t comm_timeout_ms = 0;    // DSORT_OPT_COMM_TIMEOUT_MS
     int64_t test_hold_exchange = 0; // DSORT_OPT_TEST_HOLD_EXCHANGE
+    int64_t test_fail_exchange = -1; // DSORT_OPT_TEST_FAIL_EXCHANGE
     int64_t sub_keys = -1;          // DSORT_OPT_SUB_KEYS: -1 = 3/16 of a tile, 0 = no second level
     int64_t sub_os = -1;            // DSORT_OPT_SUB_OVERSAMPLE: -1 = 8 (4 at sub-buckets <= TILE/8)
     int64_t sub_gather = 1;         // DSORT_OPT_SUB_GATHER
@@ -125,6 +129,7 @@ struct dsort_ctx {
     ncclComm *comm = nullptr;
     bool has_transport = false;   // host transport instead of RCCL (dsort_comm_init_transport)
     dsort_transport transport = {};
+    dsort::TxSeq *tx = nullptr;   // the running sample sort's host-transport sequence (dsort_tx.h)
     void *xfer = nullptr;         // pinned host staging of the host transport
     size_t xfer_bytes = 0;
     void *xfer2 = nullptr;
@@ -155,6 +160,11 @@ struct dsort_ctx {
     // would never complete (sync_event / sync_stream, dsort_wave.hip).
     bool poll_waits = false;
     double poll_deadline = 0.0;  // ms on the CLOCK_MONOTONIC scale, 0 = none
+    hipStream_t poll_stream = nullptr;  // the sort stream of those waits (ensure() polls it, and the
+                                        // side stream, instead of a device-wide synchronize)
+    // buffers replaced while poll_waits is set: hipFree / hipHostFree synchronize the device, which
+    // would wait for the comm stream, so they are released once the exchange is over (flush_later)
+    std::vector<void *> dev_later, host_later;
     // stage timing
     hipEvent_t ev[30] = {};  // 0 start, 1 tile sort done, 2 local sort done, 3 exchange done,
                              // 4 final merge done, 5/6 around the key all-to-all, 7/8 around the
@@ -183,11 +193,22 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
     return v;
 }
 
+// The statistics of a call before it records anything (first_level_map -1: no bucketed sort ran).
+inline dsort_stats fresh_stats() {
+    dsort_stats s{};
+    s.first_level_map = -1;
+    return s;
+}
+
 int set_err(dsort_ctx *ctx, int code, const std::string &msg);
 // the stream argument of the C-ABI: NULL = the context's stream, DSORT_NULL_STREAM = stream 0
 hipStream_t pick_stream(dsort_ctx *ctx, void *stream);
 int hip_err(dsort_ctx *ctx, hipError_t e, const char *what);
 int ensure(dsort_ctx *ctx, void **buf, size_t *have, size_t need, const char *what);
+// hipFree / hipHostFree of a replaced buffer, deferred while ctx->poll_waits (see dsort_ctx)
+void release_dev(dsort_ctx *ctx, void *p);
+void release_host(dsort_ctx *ctx, void *p);
+void flush_later(dsort_ctx *ctx);
 
 // The sort and the k-way merge (dsort_wave.hip), both key widths.  All asynchronous on `s`.
 // sort_device sorts d_in[0..n) into d_keys (d_in may equal d_keys).  merge_device with

@@ -1836,16 +1836,16 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
     const size_t h_num = h_stl + B * sizeof(bk::TileRef) + 16;
     const size_t h_fill = h_num + 16;
     const size_t hbytes = h_fill + (pm ? B * sizeof(FillSeg<T>) : 0);
-    if (ctx->sub_host_bytes < hbytes) {
-        if (ctx->sub_host) (void)hipHostFree(ctx->sub_host);
+    if (!ctx->sub_ev && hipEventCreateWithFlags(&ctx->sub_ev, hipEventDisableTiming) != hipSuccess)
+        return set_err(ctx, DSORT_EHIP, "hipEventCreate");
+    if (int rc_ = sync_event(ctx, ctx->sub_ev, "tile count")) return rc_;  // the previous call's read-back is done with the staging
+    if (ctx->sub_host_bytes < hbytes) {  // (after that wait: the previous call's uploads are done with it)
+        release_host(ctx, ctx->sub_host);
         ctx->sub_host = nullptr;
         ctx->sub_host_bytes = 0;
         DSORT_HIP(ctx, hipHostMalloc(&ctx->sub_host, hbytes, hipHostMallocDefault));
         ctx->sub_host_bytes = hbytes;
     }
-    if (!ctx->sub_ev && hipEventCreateWithFlags(&ctx->sub_ev, hipEventDisableTiming) != hipSuccess)
-        return set_err(ctx, DSORT_EHIP, "hipEventCreate");
-    if (int rc_ = sync_event(ctx, ctx->sub_ev, "tile count")) return rc_;  // the previous call's read-back is done with the staging
     char *h = static_cast<char *>(ctx->sub_host);
     std::memcpy(h, bi.data(), B * sizeof(BInfo));
     Chunk *hc = reinterpret_cast<Chunk *>(h + h_ch);
@@ -2027,19 +2027,27 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         ctx->ev_mask |= 2u;
     }
     fault_point(ctx, s, 2);  // tile sort done (the oversized sub-buckets' merges follow)
-    // 4. oversized sub-buckets: their tile-sorted pieces merged (src is free scratch now)
+    // 4. oversized sub-buckets: their tile-sorted pieces merged into a buffer of their own, then
+    //    copied back.  (Not into src: in the bucket exchange src is the partition buffer, which
+    //    still holds this rank's later waves' buckets and, over RCCL, buckets the comm stream is
+    //    still sending -- as merge_split_subbuckets does on the local path.)
     if (novf) {
         std::vector<Ovf> ov(novf);
         DSORT_HIP(ctx, hipMemcpyAsync(ov.data(), ovf, novf * sizeof(Ovf), hipMemcpyDeviceToHost, s));
         if (int rc_ = sync_stream(ctx, s, "sort stream")) return rc_;
-        T *tmp = src;
+        uint64_t mx = 0;
+        for (const Ovf &o : ov) mx = o.len > mx ? o.len : mx;
+        if (int rc_ = ensure(ctx, &ctx->stmp, &ctx->stmp_bytes, mx * sizeof(T) + 16, "oversized sub-bucket merge"))
+            return rc_;
+        // (the merge output keeps the sub-bucket's misalignment inside a 16-byte chunk)
+        T *tmp = static_cast<T *>(ctx->stmp);
         int lv = 0;
         for (const Ovf &o : ov) {
             const std::vector<size_t> runs = sub_tile_runs(o.start, o.len, TILE, ALIGN, mis);
-            rc = wave_merge<T>(ctx, d_keys + o.start, runs.data(), (int)runs.size(), tmp + o.start, s, true);
+            T *to = tmp + ((o.start + mis) & (ALIGN - 1));
+            rc = wave_merge<T>(ctx, d_keys + o.start, runs.data(), (int)runs.size(), to, s, true);
             if (rc) return rc;
-            DSORT_HIP(ctx, hipMemcpyAsync(d_keys + o.start, tmp + o.start, o.len * sizeof(T),
-                                          hipMemcpyDeviceToDevice, s));
+            DSORT_HIP(ctx, hipMemcpyAsync(d_keys + o.start, to, o.len * sizeof(T), hipMemcpyDeviceToDevice, s));
             int l = 0;
             for (uint64_t r = runs.size(); r > 1; r = ceil_div(r, (uint64_t)1 << WG<T>::MAXLOGF)) ++l;
             lv = l > lv ? l : lv;
@@ -2099,9 +2107,10 @@ static int bk_layout(dsort_ctx *ctx, uint64_t n, int B, size_t smp_bytes, BkLayo
     L.ntl = reinterpret_cast<uint32_t *>(a + o_nt);
     L.map = reinterpret_cast<BkMap *>(a + o_map);
     L.ids = BkIds<T>::ON ? reinterpret_cast<uint32_t *>(a + o_ids) : nullptr;
-    const size_t hbytes = (size_t)(BK_MAXB + 1) * 8 + (size_t)BK_MAXB * 16;  // starts, then the splitters
+    // starts, then the splitters, then the slot map (int32 reads its choice back)
+    const size_t hbytes = (size_t)(BK_MAXB + 1) * 8 + (size_t)BK_MAXB * 16 + sizeof(BkMap);
     if (ctx->bucket_host_bytes < hbytes) {
-        if (ctx->bucket_host) (void)hipHostFree(ctx->bucket_host);
+        release_host(ctx, ctx->bucket_host);
         ctx->bucket_host = nullptr;
         ctx->bucket_host_bytes = 0;
         DSORT_HIP(ctx, hipHostMalloc(&ctx->bucket_host, hbytes, hipHostMallocDefault));
@@ -2128,9 +2137,27 @@ static int first_level(dsort_ctx *ctx, const T *d_in, uint64_t n, uint64_t ioff,
     hspl = reinterpret_cast<C *>(hb + BK_MAXB + 1);
     hipLaunchKernelGGL(bucket_slotmap_kernel<T>, dim3(1), dim3(BK_MAXB), 0, s, L.spl, B, n, L.map);
     ctx->bk_hot = &L.map->hot;
+    // int32: which map did the splitters choose -- the fixed one (packed lookup) or the adaptive
+    // one (many small keys)?  Its kernels are separate instances, so the host waits for the choice
+    // (a few us of idle GPU; launching both instances and letting the other return at once costs a
+    // grid of empty workgroups each, about 40 us for the scatter's)
+    bool ad = false;
+    BkMap *hm = reinterpret_cast<BkMap *>(reinterpret_cast<char *>(hb) + (size_t)(BK_MAXB + 1) * 8 + (size_t)BK_MAXB * 16);
+    if constexpr (!Comp<T>::ADAPT) {
+        DSORT_HIP(ctx, hipMemcpyAsync(hm, L.map, sizeof(BkMap), hipMemcpyDeviceToHost, s));
+        DSORT_HIP(ctx, hipEventRecord(ctx->bucket_ev, s));
+        if (int rc_ = sync_event(ctx, ctx->bucket_ev, "slot map")) return rc_;
+        ad = hm->ad != 0;
+    }
     if ((rc = stage_event(ctx, s, timed, 9))) return rc;
-    hipLaunchKernelGGL(bucket_hist_kernel<T>, dim3((unsigned)L.G), dim3(BK_T), 0, s, d_in, n, L.spl, L.map, B, BP,
-                       L.subs, L.cnt, ioff, L.ids);
+    if constexpr (!Comp<T>::ADAPT) {
+        if (ad)
+            hipLaunchKernelGGL((bucket_hist_kernel<T, true>), dim3((unsigned)L.G), dim3(BK_T), 0, s, d_in, n, L.spl,
+                               L.map, B, BP, L.subs, L.cnt, ioff, L.ids);
+    }
+    if (!ad)
+        hipLaunchKernelGGL((bucket_hist_kernel<T, false>), dim3((unsigned)L.G), dim3(BK_T), 0, s, d_in, n, L.spl, L.map,
+                           B, BP, L.subs, L.cnt, ioff, L.ids);
     if ((rc = stage_event(ctx, s, timed, 10))) return rc;
     hipLaunchKernelGGL(bucket_colsum_kernel, dim3((unsigned)L.nchunk), dim3(BK_MAXB), 0, s, L.cnt, (uint32_t)L.G, B,
                        L.part);
@@ -2147,13 +2174,23 @@ static int first_level(dsort_ctx *ctx, const T *d_in, uint64_t n, uint64_t ioff,
     DSORT_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->ready_ev, 0));
     DSORT_HIP(ctx, hipMemcpyAsync(hb, L.bst, (size_t)(B + 1) * 8, hipMemcpyDeviceToHost, ctx->side));
     if (B > 1) DSORT_HIP(ctx, hipMemcpyAsync(hspl, L.spl, (size_t)(B - 1) * sizeof(C), hipMemcpyDeviceToHost, ctx->side));
+    if constexpr (Comp<T>::ADAPT)  // (int64: the map only for the statistics)
+        DSORT_HIP(ctx, hipMemcpyAsync(hm, L.map, sizeof(BkMap), hipMemcpyDeviceToHost, ctx->side));
     DSORT_HIP(ctx, hipEventRecord(ctx->bucket_ev, ctx->side));
     if ((rc = stage_event(ctx, s, timed, 11))) return rc;
 #ifdef DSORT_IDS_ONLY
     if constexpr (!BkIds<T>::ON)
 #endif
-    hipLaunchKernelGGL((bucket_scatter_lines_kernel<T, false>), dim3((unsigned)L.G), dim3(BK_T), 0, s, d_in, n, L.spl,
-                       L.map, B, BP, L.subs, L.offs, part_out, direct, ioff, L.ids);
+    {
+        if constexpr (!Comp<T>::ADAPT) {
+            if (ad)
+                hipLaunchKernelGGL((bucket_scatter_lines_kernel<T, false, true>), dim3((unsigned)L.G), dim3(BK_T), 0, s,
+                                   d_in, n, L.spl, L.map, B, BP, L.subs, L.offs, part_out, direct, ioff, L.ids);
+        }
+        if (!ad)
+            hipLaunchKernelGGL((bucket_scatter_lines_kernel<T, false, false>), dim3((unsigned)L.G), dim3(BK_T), 0, s, d_in,
+                               n, L.spl, L.map, B, BP, L.subs, L.offs, part_out, direct, ioff, L.ids);
+    }
     if constexpr (BkIds<T>::ON)  // (the variant the slot map did not choose returns at once)
         hipLaunchKernelGGL((bucket_scatter_lines_kernel<T, true>), dim3((unsigned)L.G), dim3(BK_T), 0, s, d_in, n, L.spl,
                            L.map, B, BP, L.subs, L.offs, part_out, direct, ioff, L.ids);
@@ -2162,13 +2199,14 @@ static int first_level(dsort_ctx *ctx, const T *d_in, uint64_t n, uint64_t ioff,
     fault_point(ctx, s, 0);  // first-level partition done
     if (int rc_ = sync_event(ctx, ctx->bucket_ev, "bucket starts")) return rc_;
     if (hb[B] != n) return set_err(ctx, DSORT_EHIP, "bucket partition lost keys");
+    ctx->stats.first_level_map = !Comp<T>::ADAPT && !ad ? 0 : hm->mode == 0 ? 1 : 2;
     return DSORT_OK;
 }
 
 // The stats and events of a bucketed sort start after its nested splitter sort.
 static int bucketed_stats_start(dsort_ctx *ctx, uint64_t n, int tile, hipStream_t s, bool timed) {
     ctx->bk_hot = nullptr;  // (set by this sort's first level, if it runs one)
-    ctx->stats = dsort_stats{};
+    ctx->stats = fresh_stats();
     ctx->stats.keys_in = ctx->stats.keys_out = n;
     ctx->stats.tile_sort_keys = n;
     ctx->stats.tile_keys = tile;
@@ -2352,7 +2390,7 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
         if (ctx->groups_ev_pending) { if (int rc_ = sync_event(ctx, ctx->groups_ev, "group table")) return rc_; }
         ctx->groups_ev_pending = false;
         if (ctx->groups_host_bytes < tb_off + tbytes) {
-            if (ctx->groups_host) (void)hipHostFree(ctx->groups_host);
+            release_host(ctx, ctx->groups_host);
             ctx->groups_host = nullptr;
             ctx->groups_host_bytes = 0;
             DSORT_HIP(ctx, hipHostMalloc(&ctx->groups_host, tb_off + tbytes, hipHostMallocDefault));
@@ -2652,7 +2690,7 @@ namespace wv {
 template <typename T>
 static int wave_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipStream_t s, bool timed) {
     constexpr int TILE = TILE_OF<T>;
-    ctx->stats = dsort_stats{};
+    ctx->stats = fresh_stats();
     ctx->stats.keys_in = n;
     ctx->stats.keys_out = n;
     ctx->stats.tile_keys = TILE;
@@ -2722,7 +2760,7 @@ static int wave_merge(dsort_ctx *ctx, const T *d_in, const size_t *lens, int k, 
                       bool keep_stats) {
     constexpr int MAXF = 1 << WG<T>::MAXLOGF;
     if (!keep_stats) {
-        ctx->stats = dsort_stats{};
+        ctx->stats = fresh_stats();
         ctx->kev_used = 0;
     }
     ctx->last_stream = s;
@@ -2762,7 +2800,7 @@ static int wave_merge(dsort_ctx *ctx, const T *d_in, const size_t *lens, int k, 
         if (ctx->groups_ev_pending) { if (int rc_ = sync_event(ctx, ctx->groups_ev, "group table")) return rc_; }
         ctx->groups_ev_pending = false;
         if (ctx->groups_host_bytes < gbytes) {
-            if (ctx->groups_host) (void)hipHostFree(ctx->groups_host);
+            release_host(ctx, ctx->groups_host);
             ctx->groups_host = nullptr;
             ctx->groups_host_bytes = 0;
             DSORT_HIP(ctx, hipHostMalloc(&ctx->groups_host, gbytes, hipHostMallocDefault));

@@ -22,6 +22,7 @@ except Exception:  # pragma: no cover
     torch = None
 
 DSORT_OK = 0
+DSORT_ETIMEOUT = -6
 ERRORS = {-1: "EINVAL", -2: "ENOMEM", -3: "EHIP", -4: "ECOMM", -5: "ENODEV", -6: "ETIMEOUT", -7: "ESTAGE"}
 
 # every symbol include/dsort.h declares (checked by tests/test_abi.py)
@@ -31,7 +32,7 @@ EXPORTS = [
     "dsort_sort_dev_i64", "dsort_sort_dev_copy_i32", "dsort_sort_dev_copy_i64",
     "dsort_merge_i32", "dsort_merge_i64", "dsort_merge_dev_i32", "dsort_merge_dev_i64",
     "dsort_comm_unique_id", "dsort_comm_init", "dsort_comm_init_transport", "dsort_comm_abort",
-    "dsort_comm_destroy",
+    "dsort_comm_destroy", "dsort_comm_deadline_ms",
     "dsort_sample_sort_dev_i32", "dsort_sample_sort_dev_i64", "dsort_sample_merge_dev_i32",
     "dsort_sample_merge_dev_i64", "dsort_plan_splitters_i32",
     "dsort_plan_splitters_i64", "dsort_plan_cuts_i32", "dsort_plan_cuts_i64",
@@ -48,7 +49,10 @@ EXPORTS = [
 OPTIONS = {"buckets": 1, "bucket_keys": 2, "bucket_oversample": 3,
            "max_fanin_log2": 5, "kill_after_stage": 6, "kill_in_exchange": 7,
            "comm_timeout_ms": 8,
-           "sub_keys": 9, "sub_oversample": 10, "sub_gather": 11, "test_hold_exchange": 12}
+           "sub_keys": 9, "sub_oversample": 10, "sub_gather": 11, "test_hold_exchange": 12,
+           "test_fail_exchange": 13}
+# ABI 2's option name, a deprecated alias of "kill_after_stage" until ABI 6 (dsort.h)
+DEPRECATED_OPTIONS = {"kill_after_pass": "kill_after_stage"}
 
 
 class DsortError(RuntimeError):
@@ -66,7 +70,8 @@ class Stats(ctypes.Structure):
                 ("partition_ms", ctypes.c_double), ("tile_sort_keys", ctypes.c_size_t),
                 ("bucket_hist_ms", ctypes.c_double), ("bucket_scatter_ms", ctypes.c_double),
                 ("sub_partition_ms", ctypes.c_double), ("sub_split_subbuckets", ctypes.c_int),
-                ("sub_scatter_fallback", ctypes.c_int), ("exchange_path", ctypes.c_int)]
+                ("sub_scatter_fallback", ctypes.c_int), ("exchange_path", ctypes.c_int),
+                ("first_level_map", ctypes.c_int)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -85,11 +90,33 @@ class Transport(ctypes.Structure):
     _fields_ = [("user", ctypes.c_void_p), ("allgather", ALLGATHER_FN), ("alltoallv", ALLTOALLV_FN)]
 
 
-def torch_dist_transport(world, pg=None):
+def torch_dist_transport(world, pg=None, deadline_fn=None):
     """A dsort_transport over a torch.distributed process group (gloo: CPU tensors; the default
     group unless `pg` is given).  For ranks that share a GPU, where RCCL refuses to build a
-    communicator, and for the survivors' group after a fault (ftsort.py)."""
+    communicator, and for the survivors' group after a fault (ftsort.py).
+
+    Every wait is bounded by the exchange deadline: `deadline_fn()` gives the milliseconds left
+    (-1 = none).  Context.comm_init_transport sets it to dsort_comm_deadline_ms, so a collective
+    whose peer never arrives returns DSORT_ETIMEOUT (-6) at the sort's DSORT_OPT_COMM_TIMEOUT_MS
+    instead of blocking until gloo's own timeout (dsort.h, ABI 5)."""
+    import datetime
+
     import torch.distributed as dist
+
+    def _wait(work):
+        fn = t.deadline_fn
+        ms = fn() if fn is not None else -1
+        if ms is None or ms < 0:
+            work.wait()
+            return 0
+        try:
+            work.wait(timeout=datetime.timedelta(milliseconds=max(int(ms), 1)))
+        except RuntimeError as e:
+            if "timed out" in str(e).lower():
+                print("dsort host transport: no answer before the exchange deadline", flush=True)
+                return DSORT_ETIMEOUT
+            raise
+        return 0
 
     def _allgather(user, send, recv, nbytes):
         try:
@@ -97,9 +124,12 @@ def torch_dist_transport(world, pg=None):
                 if nbytes else torch.empty(0, dtype=torch.uint8)
             outs = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(world)]
             if pg is None:
-                dist.all_gather(outs, mine)
+                work = dist.all_gather(outs, mine, async_op=True)
             else:
-                pg.allgather([outs], [mine]).wait()
+                work = pg.allgather([outs], [mine])
+            rc = _wait(work)
+            if rc:
+                return rc
             if nbytes:
                 whole = torch.cat(outs).numpy()
                 ctypes.memmove(recv, whole.ctypes.data, whole.nbytes)
@@ -117,9 +147,13 @@ def torch_dist_transport(world, pg=None):
             inp = torch.frombuffer(bytearray(chunks), dtype=torch.uint8) if chunks else torch.empty(0, dtype=torch.uint8)
             out = torch.empty(sum(rcounts), dtype=torch.uint8)
             if pg is None:
-                dist.all_to_all_single(out, inp, output_split_sizes=rcounts, input_split_sizes=scounts)
+                work = dist.all_to_all_single(out, inp, output_split_sizes=rcounts, input_split_sizes=scounts,
+                                              async_op=True)
             else:
-                pg.alltoall_base(out, inp, rcounts, scounts).wait()
+                work = pg.alltoall_base(out, inp, rcounts, scounts)
+            r = _wait(work)
+            if r:
+                return r
             o = out.numpy()
             off = 0
             for i in range(world):
@@ -133,6 +167,7 @@ def torch_dist_transport(world, pg=None):
 
     t = Transport(None, ALLGATHER_FN(_allgather), ALLTOALLV_FN(_alltoallv))
     t._keep = (_allgather, _alltoallv)  # the C side holds raw function pointers
+    t.deadline_fn = deadline_fn
     return t
 
 
@@ -177,6 +212,7 @@ def load():
         "dsort_comm_init": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, P]),
         "dsort_comm_init_transport": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(Transport)]),
         "dsort_comm_abort": (ctypes.c_int, [P]),
+        "dsort_comm_deadline_ms": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_int64)]),
         "dsort_comm_destroy": (ctypes.c_int, [P]),
         "dsort_sample_sort_dev_i32": (ctypes.c_int, [P, P, SZ, ctypes.POINTER(P), ctypes.POINTER(SZ), P]),
         "dsort_sample_sort_dev_i64": (ctypes.c_int, [P, P, SZ, ctypes.POINTER(P), ctypes.POINTER(SZ), P]),
@@ -272,7 +308,9 @@ def write_text_i32(path, keys):
 def _check(ctx, rc):
     if rc != DSORT_OK:
         msg = load().dsort_last_error(ctx).decode() if ctx else ""
-        raise DsortError(f"libdsort error {rc} ({ERRORS.get(rc, '?')}): {msg}")
+        err = DsortError(f"libdsort error {rc} ({ERRORS.get(rc, '?')}): {msg}")
+        err.rc = rc
+        raise err
     return rc
 
 
@@ -310,12 +348,22 @@ class Context:
         return _check(self.h, rc)
 
     # ---------------- options (dsort_set_option) -----------------------------------------
+    @staticmethod
+    def _opt(name):
+        if name in DEPRECATED_OPTIONS:
+            import warnings
+
+            warnings.warn(f"dsort option {name!r} is deprecated (removed with ABI 6): use "
+                          f"{DEPRECATED_OPTIONS[name]!r}", DeprecationWarning, stacklevel=3)
+            name = DEPRECATED_OPTIONS[name]
+        return OPTIONS[name]
+
     def set_option(self, name, value):
-        self.check(self.lib.dsort_set_option(self.h, OPTIONS[name], int(value)))
+        self.check(self.lib.dsort_set_option(self.h, self._opt(name), int(value)))
 
     def get_option(self, name):
         v = ctypes.c_int64()
-        self.check(self.lib.dsort_get_option(self.h, OPTIONS[name], ctypes.byref(v)))
+        self.check(self.lib.dsort_get_option(self.h, self._opt(name), ctypes.byref(v)))
         return v.value
 
     @contextlib.contextmanager
@@ -476,7 +524,16 @@ class Context:
 
     def comm_init_transport(self, nranks, rank, transport):
         self._transport = transport  # keep the callbacks alive while the library may call them
+        if getattr(transport, "deadline_fn", None) is None:
+            transport.deadline_fn = self.deadline_ms  # the callbacks' waits end at the exchange deadline
         self.check(self.lib.dsort_comm_init_transport(self.h, nranks, rank, ctypes.byref(transport)))
+
+    def deadline_ms(self):
+        """Milliseconds left before the running sample sort's exchange deadline, -1 for none
+        (dsort_comm_deadline_ms; for transport callbacks on the sorting thread)."""
+        v = ctypes.c_int64()
+        self.check(self.lib.dsort_comm_deadline_ms(self.h, ctypes.byref(v)))
+        return v.value
 
     def comm_destroy(self):
         self.check(self.lib.dsort_comm_destroy(self.h))

@@ -44,6 +44,8 @@ typedef struct wk {
     uint32_t epoch;      /* epoch of the communicator in use */
     int world;           /* ranks of that epoch */
     int32_t relay_seq;   /* next relay request of this epoch */
+    int32_t want_tag;    /* the relay response awaited (-1: none): the reader drops any other, e.g. a
+                            late answer to a request abandoned at the deadline */
     int resp_ready;
     int32_t resp_tag;
     char *resp;
@@ -107,6 +109,7 @@ static void *reader_main(void *arg) {
                 }
                 break;
             case SS_RELAY_RESP:
+                if (h.status != w->want_tag) break; /* abandoned or stale: dropped (buf freed below) */
                 free(w->resp);
                 w->resp = buf;
                 buf = NULL;
@@ -159,20 +162,34 @@ static int relay(wk *w, uint16_t type, const void *a, size_t na, const void *b, 
     }
     const int32_t tag = (int32_t)((w->epoch << 20) | (uint32_t)w->relay_seq++);
     w->resp_ready = 0;
+    free(w->resp); /* (nothing else may be pending: the reader keeps only the awaited tag) */
+    w->resp = NULL;
+    w->want_tag = tag;
     pthread_mutex_unlock(&w->mu);
-    if (send_frame2(w, type, tag, a, na, b, nb)) return -1;
+    if (send_frame2(w, type, tag, a, na, b, nb)) {
+        pthread_mutex_lock(&w->mu);
+        w->want_tag = -1;
+        pthread_mutex_unlock(&w->mu);
+        return -1;
+    }
     pthread_mutex_lock(&w->mu);
-    /* a deadline like the RCCL exchange's (DSORT_OPT_COMM_TIMEOUT_MS): a hung peer never posts its
-     * part, and the master answers only when every live rank has */
+    /* the sample sort's exchange deadline (DSORT_OPT_COMM_TIMEOUT_MS, from the start of the sort,
+     * like the RCCL path's: it must cover the slowest rank's local part): a hung peer never posts
+     * its part, and the master answers only when every live rank has.  The library says how much
+     * of it is left (dsort_comm_deadline_ms); outside a sort, the option's full length. */
+    int64_t left = -1;
+    if (dsort_comm_deadline_ms(w->ctx, &left) != DSORT_OK || left < 0) left = w->comm_timeout_ms > 0 ? w->comm_timeout_ms : -1;
     struct timespec dl;
     clock_gettime(CLOCK_REALTIME, &dl);
-    dl.tv_sec += (time_t)(w->comm_timeout_ms / 1000);
-    dl.tv_nsec += (long)(w->comm_timeout_ms % 1000) * 1000000L;
-    dl.tv_sec += dl.tv_nsec / 1000000000L;
-    dl.tv_nsec %= 1000000000L;
-    int timed_out = 0;
+    if (left >= 0) {
+        dl.tv_sec += (time_t)(left / 1000);
+        dl.tv_nsec += (long)(left % 1000) * 1000000L;
+        dl.tv_sec += dl.tv_nsec / 1000000000L;
+        dl.tv_nsec %= 1000000000L;
+    }
+    int timed_out = left == 0;
     while (!(w->resp_ready && w->resp_tag == tag) && !superseded(w) && !timed_out) {
-        if (w->comm_timeout_ms > 0) timed_out = pthread_cond_timedwait(&w->cv, &w->mu, &dl) == ETIMEDOUT;
+        if (left >= 0) timed_out = pthread_cond_timedwait(&w->cv, &w->mu, &dl) == ETIMEDOUT;
         else pthread_cond_wait(&w->cv, &w->mu);
     }
     const int ok = w->resp_ready && w->resp_tag == tag;
@@ -182,15 +199,17 @@ static int relay(wk *w, uint16_t type, const void *a, size_t na, const void *b, 
         w->resp = NULL;
         w->resp_ready = 0;
     }
+    w->want_tag = -1; /* a late answer to an abandoned request is dropped by the reader */
     pthread_mutex_unlock(&w->mu);
-    return ok ? 0 : -1;
+    return ok ? 0 : (timed_out ? DSORT_ETIMEOUT : -1);
 }
 
 static int relay_allgather(void *user, const void *send, void *recv, size_t bytes) {
     wk *w = (wk *)user;
     char *r = NULL;
     size_t rl = 0;
-    if (relay(w, SS_RELAY_AG, send, bytes, NULL, 0, &r, &rl)) return 1;
+    const int rr = relay(w, SS_RELAY_AG, send, bytes, NULL, 0, &r, &rl);
+    if (rr) return rr == DSORT_ETIMEOUT ? DSORT_ETIMEOUT : 1;
     const int bad = rl != bytes * (size_t)w->world;
     if (!bad) memcpy(recv, r, rl);
     free(r);
@@ -218,7 +237,7 @@ static int relay_alltoallv(void *user, const void *send, const size_t *sc, const
     size_t rl = 0;
     const int rc = relay(w, SS_RELAY_A2A, req, off, NULL, 0, &r, &rl);
     free(req);
-    if (rc) return 1;
+    if (rc) return rc == DSORT_ETIMEOUT ? DSORT_ETIMEOUT : 1;
     int bad = rl < (size_t)P * 8;
     uint64_t pos = (uint64_t)P * 8;
     for (int s = 0; s < P && !bad; ++s) {
@@ -300,6 +319,7 @@ int samplesort_worker(const char *host, int port, int device, int verbose) {
     wire_set_nodelay(fd);
     static wk w;
     memset(&w, 0, sizeof w);
+    w.want_tag = -1;
     w.fd = fd;
     w.ctx = ctx;
     pthread_mutex_init(&w.send_mu, NULL);

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define DSORT_ABI_VERSION 4
+#define DSORT_ABI_VERSION 5
 
 #define DSORT_OK 0
 #define DSORT_EINVAL (-1)   /* bad argument */
@@ -86,6 +86,11 @@ typedef struct dsort_stats {
     int exchange_path;        /* the last sample sort: 1 = bucket exchange (partition, exchange,
                                  sort the received buckets), 2 = sort, exchange, merge the received
                                  runs (small inputs, dsort_sample_merge_dev), 0 = not a sample sort */
+    /* ABI 5 */
+    int first_level_map;      /* slot map of the last bucketed sort's first partition level: 0 the fixed
+                                 top-11-bit map (int32 only), 1 linear over the splitters' key range, 2
+                                 logarithmic (bucket_slotmap_kernel; int32 leaves the fixed map when it
+                                 crowds the splitters of several keys into one slot); -1 none */
 } dsort_stats;
 
 /* ---------------------------------------------------------------- lifecycle ---------- */
@@ -115,8 +120,12 @@ int dsort_synchronize(dsort_ctx *ctx);
                                          A stage the sort never reaches makes it return DSORT_ESTAGE
                                          (ABI 3: DSORT_EINVAL) */
 /* ABI 2's DSORT_OPT_KILL_AFTER_PASS (option 6) counted merge passes; ABI 3 renumbered option 6 as
- * stages (merge path: ABI 2's pass p is stage 1 + p; the bucketed path's stages did not exist),
- * and ABI 4 retires the old name: callers must say DSORT_OPT_KILL_AFTER_STAGE. */
+ * stages (merge path: ABI 2's pass p is stage 1 + p; the bucketed path's stages did not exist).
+ * The old name stays for one more ABI version as a deprecated alias of option 6 (with the stage
+ * meaning); it goes away in ABI 6.  Define DSORT_NO_DEPRECATED to drop it now. */
+#ifndef DSORT_NO_DEPRECATED
+#define DSORT_OPT_KILL_AFTER_PASS DSORT_OPT_KILL_AFTER_STAGE /* deprecated (ABI 5): use ..._STAGE */
+#endif
 #define DSORT_OPT_KILL_IN_EXCHANGE 7  /* fault injection: SIGKILL inside the sample-sort exchange, at
                                          stage 1 (samples all-gathered) or 2 (counts exchanged, keys
                                          about to move); -1 = off (default)                            */
@@ -135,6 +144,11 @@ int dsort_synchronize(dsort_ctx *ctx);
                                          aborted (dsort_comm_abort from another thread) or the deadline
                                          passes -- the survivor's blocked wait of a peer failure, made
                                          deterministic.  0 = off (default)                          */
+#define DSORT_OPT_TEST_FAIL_EXCHANGE 13 /* test only (ABI 5, host transport): k >= 0 = this rank fails
+                                         locally (DSORT_EHIP) right before the k-th collective of its
+                                         sample sort (0 = the key-count all-gather); its peers must
+                                         leave at the next status gate with DSORT_ECOMM instead of
+                                         blocking.  -1 = off (default)                               */
 int dsort_set_option(dsort_ctx *ctx, int option, int64_t value);
 int dsort_get_option(const dsort_ctx *ctx, int option, int64_t *value);
 
@@ -195,13 +209,19 @@ int dsort_merge_dev_i64(dsort_ctx *ctx, const int64_t *d_in, const size_t lens[]
 #define DSORT_UNIQUE_ID_BYTES 128
 int dsort_comm_unique_id(char id[DSORT_UNIQUE_ID_BYTES]);
 int dsort_comm_init(dsort_ctx *ctx, int nranks, int rank, const char id[DSORT_UNIQUE_ID_BYTES]);
-/* Host transport: the sample sort's three exchanges (samples, counts, keys) through caller
+/* Host transport: the sample sort's exchanges (counts, samples, bucket starts, keys) through caller
  * callbacks on HOST buffers instead of RCCL.  RCCL needs one GPU per rank; this serves ranks
  * that share a GPU (tests on a 1-GPU box drive it with gloo) or hosts without a usable RCCL.
- * All sizes in bytes; every callback returns 0 on success.
+ * All sizes in bytes; every callback returns 0 on success, DSORT_ETIMEOUT when it gave up at the
+ * exchange deadline (see dsort_comm_deadline_ms), anything else on a transport failure (the sort
+ * then returns DSORT_ETIMEOUT / DSORT_ECOMM and runs no further collective on this transport).
  *   allgather: rank r's `bytes` from `send` land at recv + r*bytes on every rank.
  *   alltoallv: send[sdispls[d] .. +scounts[d]) goes to rank d, which receives it at
- *              recv[rdispls[s] .. +rcounts[s]) for source s. */
+ *              recv[rdispls[s] .. +rcounts[s]) for source s.
+ * ABI 5: every collective of a sample sort after its first is preceded by an 8-byte all-gather of
+ * every rank's status (a gate): a rank that fails locally between two collectives reports it at the
+ * next gate, and every rank then returns (the failing one its own error, the others DSORT_ECOMM)
+ * instead of blocking in a collective the failed rank never joins. */
 typedef struct dsort_transport {
     void *user;
     int (*allgather)(void *user, const void *send, void *recv, size_t bytes);
@@ -209,6 +229,11 @@ typedef struct dsort_transport {
                      void *recv, const size_t *rcounts, const size_t *rdispls);
 } dsort_transport;
 int dsort_comm_init_transport(dsort_ctx *ctx, int nranks, int rank, const dsort_transport *t);
+/* ABI 5: for transport callbacks, called on the thread running the sample sort: the milliseconds
+ * left before the sort's exchange deadline (DSORT_OPT_COMM_TIMEOUT_MS; 0 = passed), or -1 when it
+ * has none or no sample sort is running.  A callback bounds its waits by it and returns
+ * DSORT_ETIMEOUT when it runs out, so a peer that hangs surfaces as a timeout, not as a hang. */
+int dsort_comm_deadline_ms(const dsort_ctx *ctx, int64_t *remaining_ms);
 /* Abort in-flight collectives (fault path: a peer died) and drop the communicator.  Safe to
  * call from another thread while this context is inside a sample sort: the call only raises the
  * abort flag, and the sample sort aborts the communicator itself and returns DSORT_ECOMM. */

@@ -140,6 +140,7 @@ int dsort_comm_init_transport(dsort_ctx *ctx, int nranks, int rank, const dsort_
     (void)ctx; g_nranks = nranks; g_rank = rank; g_tx = *t; g_has_tx = 1; g_abort = 0; return DSORT_OK;
 }
 int dsort_comm_abort(dsort_ctx *ctx) { (void)ctx; g_has_tx = 0; return DSORT_OK; }
+int dsort_comm_deadline_ms(const dsort_ctx *ctx, int64_t *ms) { (void)ctx; if (!ms) return DSORT_EINVAL; *ms = -1; return DSORT_OK; }
 int dsort_comm_destroy(dsort_ctx *ctx) { (void)ctx; g_has_tx = 0; return DSORT_OK; }
 
 /* The double's sort has the library's three bucketed-sort kill points (dsort.h,

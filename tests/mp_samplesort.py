@@ -1,10 +1,15 @@
 """Multi-process sample-sort driver used by the GPU tests (one process per rank, all ranks may
 share one GPU).  Rank 0 creates the RCCL unique id; the ids travel through a torch.distributed
-gloo store (CPU only).  Each rank generates its equal contiguous chunk of the global synthetic
-input, runs dsort_sample_sort_dev, and reports order/fingerprint/boundaries to rank 0."""
+gloo group (CPU only) whose rendezvous is a FILE store: round 4's one multi-rank hang was a TCP
+rendezvous port chosen by the test and lost before rank 0 bound it.  Each rank
+generates its equal contiguous chunk of the global synthetic input, runs dsort_sample_sort_dev,
+and saves its input and output slice.  `opts` (JSON): dsort options for every rank, and
+"rank_opts" {rank: {option: value}} for one rank (fault injection); a failing sort is reported in
+the rank's JSON ("error", "rc") instead of raising."""
 import json
 import os
 import sys
+import time
 
 import numpy as np
 
@@ -12,7 +17,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "distributed-sorting-with-fault-tolerance_amd"))
 
 
-def run(rank, world, port, n_total, dtype, dist, out_path, transport="rccl", device=0):
+def run(rank, world, store, n_total, dtype, dist, out_path, transport="rccl", opts="{}", device=0):
     import ctypes
 
     import torch
@@ -25,11 +30,15 @@ def run(rank, world, port, n_total, dtype, dist, out_path, transport="rccl", dev
     def step(what):  # (progress on stdout: a hung rank shows where it stopped)
         print(f"rank {rank}: {what}", flush=True)
 
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    tdist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
+    tdist.init_process_group("gloo", init_method=f"file://{store}", rank=rank, world_size=world,
+                             timeout=datetime.timedelta(seconds=60))
     step("rendezvous done")
     ctx = dsort.Context(device)
+    o = json.loads(opts)
+    # every wait of the exchange bounded (the transport callbacks read the remaining time)
+    ctx.set_option("comm_timeout_ms", o.pop("comm_timeout_ms", 60_000))
+    for k, v in {**o.get("all", {}), **o.get("rank_opts", {}).get(str(rank), {})}.items():
+        ctx.set_option(k, v)
     if transport == "host":  # ranks share one GPU: exchanges through gloo
         ctx.comm_init_transport(world, rank, dsort.torch_dist_transport(world))
     else:
@@ -50,10 +59,21 @@ def run(rank, world, port, n_total, dtype, dist, out_path, transport="rccl", dev
         ctx.gen_uniform(t, 0x5EED2026, first)
         if dist == "few":  # 8 distinct keys: whole buckets of one key on every rank
             t.copy_(t >> (29 if dtype == "i32" else 61))
+        elif dist == "ref100":  # the reference's input.txt shape: keys in [1, 100]
+            t.copy_((t & 0x7FFFFFFF) % 100 + 1)
     torch.cuda.synchronize()
     step(f"input ready ({sz} keys)")
-    ptr, nout = ctx.sample_sort_dev(t)
-    ctx.synchronize()
+    t0 = time.monotonic()
+    try:
+        ptr, nout = ctx.sample_sort_dev(t)
+        ctx.synchronize()
+    except dsort.DsortError as e:  # (fault-injection runs: every rank must return, with an error)
+        step(f"sample sort failed: {e}")
+        with open(out_path + f".rank{rank}.json", "w") as f:
+            json.dump({"rank": rank, "error": str(e), "rc": getattr(e, "rc", 0), "s": time.monotonic() - t0}, f)
+        ctx.close()
+        step("done")
+        os._exit(0)  # (a peer's pending gloo collective may never complete: leave without it)
     step(f"sample sort done ({nout} keys)")
     host = np.zeros(nout, np.int32 if dtype == "i32" else np.int64)
     if nout:
@@ -72,5 +92,5 @@ def run(rank, world, port, n_total, dtype, dist, out_path, transport="rccl", dev
 
 
 if __name__ == "__main__":
-    rank, world, port, n, dtype, dist, out, transport = sys.argv[1:9]
-    run(int(rank), int(world), int(port), int(n), dtype, dist, out, transport)
+    rank, world, store, n, dtype, dist, out, transport = sys.argv[1:9]
+    run(int(rank), int(world), store, int(n), dtype, dist, out, transport, sys.argv[9] if len(sys.argv) > 9 else "{}")

@@ -1,0 +1,67 @@
+"""bench.py's N > 1 result line on CPU (no GPU): report_multi fed a synthetic per-rank table (the
+rows run_multi gathers from every rank) must carry SURVEY.md §8d in full -- the slowest stage's HBM
+roofline, the xGMI figure of the key exchange, the all-kernels fraction (PMC bytes over device
+time, labelled measured only on the PMC table's own build) and the reference CPU path beside it
+(cpu_baseline, as at N = 1)."""
+import json
+import os
+import sys
+
+import numpy as np
+
+from conftest import REPO
+
+
+def _per_rank(world, n, w):
+    sys.path.insert(0, REPO)
+    import bench
+
+    rows = np.zeros((world, 12))
+    for r in range(world):
+        nk = n // world
+        rows[r, bench.PR_TILE] = 0.30 + 0.01 * r
+        rows[r, bench.PR_A2A] = 0.9
+        rows[r, bench.PR_EXCH] = 1.2
+        rows[r, bench.PR_FINAL] = 0.7
+        rows[r, bench.PR_SENT] = nk * (world - 1) / world
+        rows[r, bench.PR_KEYS] = nk
+        rows[r, bench.PR_HIST] = 0.1
+        rows[r, bench.PR_SCAT] = 0.35 + 0.01 * r
+        rows[r, bench.PR_SUB] = 0.25
+        rows[r, bench.PR_TKEYS] = nk
+        rows[r, bench.PR_PATH] = 1
+        rows[r, bench.PR_TOTAL] = 1.9 + 0.05 * r
+    return rows
+
+
+def test_report_multi_carries_roofline_all_kernels_and_cpu_baseline(capsys):
+    sys.path.insert(0, REPO)
+    import bench
+
+    world, n = 4, 1 << 30
+    args = bench.parse(["--gpus", str(world), "--steps", "5", "--cpu-sample-keys", str(1 << 16)])
+    bench.report_multi(args, world, 5 * 2.1e-3, _per_rank(world, n, 4), 4)
+    line = [ln for ln in capsys.readouterr().out.splitlines() if ln.startswith("{")][-1]
+    d = json.loads(line)
+    assert d["n_gpus"] == world and d["unit"] == "keys/s" and abs(d["value"] - n / 2.1e-3) < 1e3
+    roof = d["roofline"]
+    assert roof["bound"] == "hbm" and 0 < roof["frac"] < 1 and roof["peak"] == 8000.0
+    assert "rank 3" in roof["kernel"]  # the slowest stage of the slowest rank
+    assert roof["xgmi"]["peak"] == 3 * 153.0 and roof["xgmi"]["frac"] > 0
+    key = "all_kernels_frac" if "all_kernels_frac" in roof else "all_kernels_frac_estimate"
+    assert 0 < roof[key] < 1, roof
+    assert roof["all_kernels"]["device_ms_slowest_rank"] == 2.05
+    assert len(roof["device_ms_per_rank"]) == world
+    cb = d["cpu_baseline"]
+    assert cb["kind"] in ("reference", "port") and cb["cores"] == 4 and cb["value"] > 0
+    assert "65536" in cb["sample"]
+
+
+def test_report_multi_without_cpu_baseline(capsys):
+    sys.path.insert(0, REPO)
+    import bench
+
+    args = bench.parse(["--gpus", "2", "--no-cpu-baseline"])
+    bench.report_multi(args, 2, 10 * 4e-3, _per_rank(2, 1 << 30, 4), 4)
+    d = json.loads([ln for ln in capsys.readouterr().out.splitlines() if ln.startswith("{")][-1])
+    assert "cpu_baseline" not in d and d["n_gpus"] == 2

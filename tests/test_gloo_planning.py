@@ -14,17 +14,15 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from cluster import free_port
 from conftest import PKG
 
 
-def _rank(rank, world, port, n_total, dist_kind, outdir):
+def _rank(rank, world, store, n_total, dist_kind, outdir):
     sys.path.insert(0, PKG)
     import dsort
 
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # (a file rendezvous: no TCP port to lose between choosing it and binding it)
+    dist.init_process_group("gloo", init_method=f"file://{store}", rank=rank, world_size=world)
     rng = np.random.default_rng(1234)
     allkeys = (rng.integers(-50, 50, n_total) if dist_kind == "dups" else
                rng.integers(-(2**31), 2**31, n_total)).astype(np.int32)
@@ -60,7 +58,7 @@ def _rank(rank, world, port, n_total, dist_kind, outdir):
 @pytest.mark.parametrize("world,kind", [(2, "uniform"), (2, "dups"), (3, "dups")])
 def test_sample_sort_planning_over_gloo(tmp_path, world, kind):
     n = 40_003
-    mp.spawn(_rank, args=(world, free_port(), n, kind, str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_rank, args=(world, str(tmp_path / "store"), n, kind, str(tmp_path)), nprocs=world, join=True)
     slices = [np.load(tmp_path / f"slice{r}.npy") for r in range(world)]
     allkeys = np.load(tmp_path / "all.npy")
     assert np.array_equal(np.concatenate(slices), np.sort(allkeys))

@@ -11,19 +11,18 @@ import sys
 import numpy as np
 import pytest
 
-from cluster import free_port
 from conftest import REPO
 
 pytestmark = pytest.mark.gpu
 DRIVER = os.path.join(REPO, "tests", "mp_samplesort.py")
 
 
-def run_ranks(tmp_path, world, n, dtype="i32", dist="uniform", transport="host"):
-    port = free_port()
+def run_ranks(tmp_path, world, n, dtype="i32", dist="uniform", transport="host", opts=None, expect_fail=False):
+    store = str(tmp_path / "store")  # (a file rendezvous: no port to lose)
     out = str(tmp_path / "ss")
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
-    procs = [subprocess.Popen([sys.executable, DRIVER, str(r), str(world), str(port), str(n), dtype, dist, out,
-                               transport],
+    procs = [subprocess.Popen([sys.executable, DRIVER, str(r), str(world), store, str(n), dtype, dist, out,
+                               transport, json.dumps(opts or {})],
                               env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(world)]
     logs = []
     for p in procs:
@@ -42,6 +41,8 @@ def run_ranks(tmp_path, world, n, dtype="i32", dist="uniform", transport="host")
         logs.append(o.decode(errors="replace"))
     for p, lg in zip(procs, logs):
         assert p.returncode == 0, lg[-3000:]
+    if expect_fail:
+        return [json.load(open(out + f".rank{r}.json")) for r in range(world)]
     ins = np.concatenate([np.load(out + f".in{r}.npy") for r in range(world)])
     outs = [np.load(out + f".out{r}.npy") for r in range(world)]
     meta = [json.load(open(out + f".rank{r}.json")) for r in range(world)]
@@ -84,7 +85,7 @@ def test_sample_sort_tiny_and_empty_ranks(tmp_path):
 @pytest.mark.parametrize("world,dtype,dist", [(1, "i32", "uniform"), (2, "i32", "uniform"), (3, "i32", "uniform"),
                                               (4, "i32", "uniform"), (3, "i32", "seq"), (2, "i32", "rev"),
                                               (3, "i32", "few"), (2, "i64", "uniform"), (3, "i64", "zipf"),
-                                              (2, "i64", "few")])
+                                              (2, "i64", "few"), (3, "i32", "ref100")])
 def test_bucket_exchange_bit_exact(tmp_path, world, dtype, dist):
     """The bucket exchange (dsort_api.hip sample_sort_bx: global splitters from every rank's
     samples, the first partition level before the exchange, the received pieces finished by the
@@ -106,4 +107,33 @@ def test_small_sample_sort_takes_the_merge_path(tmp_path):
     """Below 2^22 keys per rank the sample sort sorts locally and merges the received runs."""
     ins, outs, meta = run_ranks(tmp_path, 2, 1_000_003)
     assert all(m["stats"]["exchange_path"] == 2 for m in meta)
+    assert np.array_equal(np.concatenate(outs), np.sort(ins))
+
+
+@pytest.mark.parametrize("n,fail_at", [(3 * (1 << 22) + 12_345, 3), (3 * (1 << 22) + 12_345, 1),
+                                       (3 * (1 << 22) + 12_345, 4), (1_000_003, 3)])
+def test_local_failure_in_the_exchange_fails_every_rank(tmp_path, n, fail_at):
+    """A rank failing locally right before a collective of the host-transport sample sort
+    (DSORT_OPT_TEST_FAIL_EXCHANGE; 3 = the key all-to-all of the bucket exchange's first wave, 1 =
+    the samples, 4 = the second wave; on the merge path below 2^22 keys per rank, 3 = the keys):
+    its peers meet the failure at the next status gate and return DSORT_ECOMM naming it, instead of
+    blocking in a collective it never joins (dsort_tx.h; the survivor side of server.c:421-449)."""
+    res = run_ranks(tmp_path, 3, n, opts={"rank_opts": {"1": {"test_fail_exchange": fail_at}}}, expect_fail=True)
+    assert res[1]["rc"] == -3 and "DSORT_OPT_TEST_FAIL_EXCHANGE" in res[1]["error"], res[1]
+    for r in (0, 2):
+        assert res[r]["rc"] == -4 and "rank 1 failed locally" in res[r]["error"], res[r]
+    assert max(r["s"] for r in res) < 30, res
+
+
+@pytest.mark.parametrize("world,gather", [(2, 0), (3, 0), (2, 1)])
+def test_bucket_exchange_oversized_subbuckets(tmp_path, world, gather):
+    """Sub-buckets above a tile (DSORT_OPT_SUB_KEYS forces them) in the bucket exchange, on the
+    scatter path (sub_gather = 0) and the local path: their split tiles are merged into a buffer
+    of their own.  ADVICE r4: the scatter path merged into its source -- in the bucket exchange the
+    partition buffer, which still holds this rank's second-wave buckets (and, over RCCL, buckets
+    still being sent) -- and the output of the later wave was wrong."""
+    n = world * (1 << 22) + 12_345
+    ins, outs, meta = run_ranks(tmp_path, world, n, opts={"all": {"sub_gather": gather, "sub_keys": 20_000}})
+    assert all(m["stats"]["exchange_path"] == 1 for m in meta)
+    assert any(m["stats"]["sub_split_subbuckets"] > 0 for m in meta), [m["stats"] for m in meta]
     assert np.array_equal(np.concatenate(outs), np.sort(ins))

@@ -314,3 +314,55 @@ def test_c3_receive_merge_8_runs_bit_exact(gpu_ctx):
     assert torch.equal(out, torch.sort(recv).values)
     del recv, out
     torch.cuda.empty_cache()
+
+
+def _shaped_i32(gpu_ctx, n, dist):
+    import torch
+    t = torch.empty(n, dtype=torch.int32, device="cuda")
+    gpu_ctx.gen_uniform(t, 0x5EED2026, 0)
+    if dist == "ref100":  # the shape of the reference's input.txt: keys in [1, 100]
+        t.copy_((t & 0x7FFFFFFF) % 100 + 1)
+    elif dist == "byte":  # 256 small keys
+        t.copy_(t & 255)
+    elif dist == "signed100":  # 100 keys around zero (the sign flip of the slot map)
+        t.copy_((t & 0x7FFFFFFF) % 100 - 50)
+    elif dist == "narrow16":  # 2^16 distinct keys across zero
+        t.copy_((t & 0xFFFF) - 30000)
+    elif dist == "mixed":  # half uniform, half in [1, 100]: no map separates the small keys
+        t.copy_(torch.where((t & 1) == 1, t, (t & 0x7FFFFFFF) % 100 + 1))
+    return t
+
+
+@pytest.mark.parametrize("dist,want_map", [("ref100", 1), ("byte", 1), ("signed100", 1), ("narrow16", 1),
+                                           ("mixed", None), ("uniform", 0)])
+def test_small_key_ranges_adaptive_map_bit_exact(gpu_ctx, dist, want_map):
+    """int32 keys from a narrow range (the reference's input.txt holds 10 000 keys in [1, 100]): the
+    fixed 11-bit slot map of the first partition level puts every splitter into one slot; the slot
+    map kernel then switches to the adaptive map (linear over the splitters' range, one-key slots;
+    DESIGN.md §3.3), reported as first_level_map.  2^28 keys (config C2's size) against torch.sort,
+    element for element."""
+    import torch
+    n = 1 << 28
+    t = _shaped_i32(gpu_ctx, n, dist)
+    out = torch.empty_like(t)
+    gpu_ctx.sort_dev(t, out)
+    torch.cuda.synchronize()
+    st = gpu_ctx.stats()
+    if want_map is not None:
+        assert st["first_level_map"] == want_map, st
+    assert torch.equal(out, torch.sort(t).values)
+    del t, out
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("n", [(1 << 25) + 77, 3 * (1 << 25) - 5])
+def test_small_key_ranges_other_sizes(gpu_ctx, n):
+    """The adaptive map at other bucket counts (32 and 96 buckets), odd sizes."""
+    import torch
+    for dist in ("ref100", "byte"):
+        t = _shaped_i32(gpu_ctx, n, dist)
+        out = torch.empty_like(t)
+        gpu_ctx.sort_dev(t, out)
+        torch.cuda.synchronize()
+        assert gpu_ctx.stats()["first_level_map"] == 1
+        assert torch.equal(out, torch.sort(t).values)
