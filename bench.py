@@ -396,18 +396,20 @@ def cpu_baseline(sample_keys, target_keys):
 # (w = key bytes): the histogram reads every key once, the other three read and write every key
 # (the second level and the tile sort only the keys outside single-key buckets).
 STAGE_KERNELS = {
-    4: [("bucket_hist_kernel<int>", "bucket_hist_ms", 1, "n"),
-        ("bucket_scatter_lines_kernel<int, false>", "bucket_scatter_ms", 2, "n"),
+    # (round 5: the first level's kernels carry the adaptive-map flag; uniform int32 keys take the
+    # fixed map, int64 has one map kind)
+    4: [("bucket_hist_kernel<int, false>", "bucket_hist_ms", 1, "n"),
+        ("bucket_scatter_lines_kernel<int, false, false>", "bucket_scatter_ms", 2, "n"),
         ("sb_local_kernel<int>", "sub_partition_ms", 2, "tile_sort_keys"),
         ("bin_sort_kernel<int, true, 8>", "tile_sort_kernel_ms", 2, "tile_sort_keys")],
-    8: [("bucket_hist_kernel<long>", "bucket_hist_ms", 1, "n"),
-        ("bucket_scatter_lines_kernel<long, {ids}>", "bucket_scatter_ms", 2, "n"),
+    8: [("bucket_hist_kernel<long, false>", "bucket_hist_ms", 1, "n"),
+        ("bucket_scatter_lines_kernel<long, {ids}, false>", "bucket_scatter_ms", 2, "n"),
         ("sb_local_kernel<long>", "sub_partition_ms", 2, "tile_sort_keys"),
         ("bin_sort_kernel<long, true, 8>", "tile_sort_kernel_ms", 2, "tile_sort_keys")],
 }
 # the generator and runtime copies are not part of the sort
 NOT_SORT = ("gen_uniform", "gen_zipf", "__amd_rocclr", "fingerprint", "descents")
-PMC_FILES = ("r4_pmc_traffic.json", "r3_pmc_traffic.json", "r2_pmc_traffic.json")
+PMC_FILES = ("r5_pmc_traffic.json", "r4_pmc_traffic.json", "r3_pmc_traffic.json", "r2_pmc_traffic.json")
 
 
 def lib_sha256():

@@ -318,6 +318,29 @@ __device__ __forceinline__ int bucket_onekey(const typename Comp<T>::C *spl, int
     const int j = (int)q;
     return lo + 1 + (j < hi - lo - 2 ? j : hi - lo - 2);
 }
+// The packed int32 entry (bucket_fast's first branch) split in two, for a classify that keeps
+// several keys' table reads in flight: the fast result and whether the key needs the slow path
+// (a slot of two or more splitters, or a key equal to the slot's splitter in bits 31..1).
+__device__ __forceinline__ int packed_fast(uint32_t r, int32_t key, bool &slow) {
+    const int lo = (int)(r & 1023);
+    const uint32_t in = (r >> 10) & 3, sb = r >> 12;
+    const uint32_t kb = ((uint32_t)key ^ 0x80000000u) << 11 >> 12;
+    slow = in > 1 || (in == 1 && kb == sb);
+    return lo + (int)(in == 1 && kb > sb);
+}
+__device__ __forceinline__ int packed_slow(const int64_t *spl, uint32_t r, int32_t key, int64_t c) {
+    int lo = (int)(r & 1023);
+    const uint32_t in = (r >> 10) & 3, sb = r >> 12;
+    int hi = lo + (in == 1 ? 1 : (int)sb);
+    if (in == 3) return bucket_onekey<int32_t>(spl, lo, hi, key, c);
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (spl[mid] < c) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
 // int32 (round 4): one-key slots as well -- 16 distinct keys spread over the range put 64
 // splitters of one key in a slot, and every key searched them (2^30: histogram 4.96 ms, scatter
 // 9.0 ms).  The packed entry marks them with splitter count field 3.
@@ -511,6 +534,27 @@ __global__ void __launch_bounds__(BK_MAXB) pair_splitter_kernel(const int64_t *_
     }
 }
 
+// A sub-tile's keys of one thread: in[i0 + k BK_T], k < KPT.  A whole sub-tile (the usual case,
+// workgroup-uniform) loads without bounds checks: with them every load sat in a branch of its own
+// (an exec-mask save, a conditional jump), and the loads of a thread were not issued together.
+#ifndef DSORT_NOGUARD
+#define DSORT_NOGUARD 1
+#endif
+template <typename T, int KPT>
+__device__ __forceinline__ void load_sub(const T *__restrict__ in, uint64_t i0, uint64_t n, uint64_t sub_end,
+                                         T (&x)[KPT]) {
+    if (DSORT_NOGUARD && sub_end <= n) {
+#pragma unroll
+        for (int k = 0; k < KPT; ++k) x[k] = in[i0 + (uint64_t)k * BK_T];
+    } else {
+#pragma unroll
+        for (int k = 0; k < KPT; ++k) {
+            const uint64_t i = i0 + (uint64_t)k * BK_T;
+            x[k] = i < n ? in[i] : T(0);
+        }
+    }
+}
+
 // spl holds BK_MAXB + 1 entries: the BP splitters (+inf padded), +inf up to the end (the int32
 // lookup of the last slot searches up to BK_MAXB)
 template <typename T>
@@ -574,24 +618,14 @@ __global__ void __launch_bounds__(BK_T, 2) bucket_hist_kernel(const T *__restric
     // the next sub-tile's keys are loaded while the current one is counted (two workgroups per CU
     // alone left the loads' latency exposed: 0.79 ms for 4.3 GB)
     T nxt[KPT];
-#pragma unroll
-    for (int k = 0; k < KPT; ++k) {
-        const uint64_t i = g0 + threadIdx.x + (uint64_t)k * BK_T;
-        nxt[k] = i < n ? in[i] : T(0);
-    }
+    load_sub<T, KPT>(in, g0 + threadIdx.x, n, g0 + SUB, nxt);
 #pragma unroll 1
     for (int sub = 0; sub < subs; ++sub) {
         const uint64_t b0 = g0 + (uint64_t)sub * SUB + threadIdx.x;
         T key[KPT];
 #pragma unroll
         for (int k = 0; k < KPT; ++k) key[k] = nxt[k];
-        if (sub + 1 < subs) {
-#pragma unroll
-            for (int k = 0; k < KPT; ++k) {
-                const uint64_t i = b0 + SUB + (uint64_t)k * BK_T;
-                nxt[k] = i < n ? in[i] : T(0);
-            }
-        }
+        if (sub + 1 < subs) load_sub<T, KPT>(in, b0 + SUB, n, b0 - threadIdx.x + 2 * SUB, nxt);
         // the buckets of the thread's keys, two per word (bucket ids: BkIds)
         uint32_t idw[KPT / 2] = {};
         // (the mode branch outside the key loop: a slot array would cost the second workgroup)
@@ -861,11 +895,7 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
 #endif
     T nxt[KPT];
     uint32_t nid[IDS ? KPT / 2 : 1];  // (the histogram's thread-major bucket ids, two per word)
-#pragma unroll
-    for (int k = 0; k < KPT; ++k) {
-        const uint64_t i = g0 + tb + (uint64_t)k * BK_T;
-        nxt[k] = i < n ? in[i] : T(0);
-    }
+    load_sub<T, KPT>(in, g0 + tb, n, g0 + SUB, nxt);
     if constexpr (IDS) {
 #pragma unroll
         for (int w = 0; w < KPT / 2; ++w) nid[w] = g0 < n ? ids[g0 / 2 + (uint64_t)tb * (KPT / 2) + w] : 0u;
@@ -887,11 +917,7 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
             slots_at<T, KPT, ADP>(m, key, sl);
         }
         if (!last) {
-#pragma unroll
-            for (int k = 0; k < KPT; ++k) {
-                const uint64_t i = s0 + SUB + tb + (uint64_t)k * BK_T;
-                nxt[k] = i < n ? in[i] : T(0);
-            }
+            load_sub<T, KPT>(in, s0 + SUB + tb, n, s0 + 2 * SUB, nxt);
             if constexpr (IDS) {
 #pragma unroll
                 for (int w = 0; w < KPT / 2; ++w) nid[w] = ids[(s0 + SUB) / 2 + (uint64_t)tb * (KPT / 2) + w];
@@ -899,6 +925,15 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
         }
 #ifndef DSORT_HOT_SCATTER
 #define DSORT_HOT_SCATTER 1
+#endif
+#ifndef DSORT_SCATTER_CB
+#define DSORT_SCATTER_CB 4  // keys per batch of the whole-sub-tile classify (int32, fixed map)
+#endif
+#ifndef DSORT_PLACE_PB
+#define DSORT_PLACE_PB 4    // keys per batch of the whole-sub-tile placement (0: key by key)
+#endif
+#ifndef DSORT_LINE_LU
+#define DSORT_LINE_LU 2     // line entries per lane and step of the line phase
 #endif
         if (DSORT_HOT_SCATTER && m.hot) {  // (runs of one bucket: aggregated ranks, bucket_runs_hint)
 #pragma unroll
@@ -910,6 +945,42 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
                 pk[k] = act ? r | (uint32_t)b << 16 : ~0u;
             }
         } else {
+          bool batched = false;
+          if constexpr (!ADP && !IDS && DSORT_SCATTER_CB > 0) {
+           if (s0 + SUB <= n) {
+            batched = true;
+            // (int32 on the fixed map, a whole sub-tile: no per-key bounds.)  The table reads of CB
+            // keys are issued together, then their rank atomics: one LDS round trip per batch and
+            // kind instead of two per key (the per-key form waited for each read and each atomic
+            // before the next key's, with the key's bounds check as a branch around it).  The rare
+            // slow keys of a batch (crowded slot, equal to the slot's splitter) take one
+            // wave-uniform branch.
+            constexpr int CB = DSORT_SCATTER_CB > 0 ? DSORT_SCATTER_CB : 1;
+#pragma unroll
+            for (int k0 = 0; k0 < KPT; k0 += CB) {
+                uint32_t r[CB];
+                int b[CB];
+                bool sw[CB], any = false;
+#pragma unroll
+                for (int g = 0; g < CB; ++g) r[g] = rng[sl[k0 + g]];
+#pragma unroll
+                for (int g = 0; g < CB; ++g) {
+                    b[g] = packed_fast(r[g], (int32_t)key[k0 + g], sw[g]);
+                    any = any || sw[g];
+                }
+                if (__builtin_expect(__ballot(any) != 0, 0)) {
+#pragma unroll
+                    for (int g = 0; g < CB; ++g)
+                        if (sw[g])
+                            b[g] = packed_slow(reinterpret_cast<const int64_t *>(spl_look), r[g], (int32_t)key[k0 + g],
+                                               (int64_t)CT::make(key[k0 + g], s0 + tb + (uint64_t)(k0 + g) * BK_T + ioff));
+                }
+#pragma unroll
+                for (int g = 0; g < CB; ++g) pk[k0 + g] = atomicAdd(&hist[b[g]], 1u) | (uint32_t)b[g] << 16;
+            }
+           }
+          }
+          if (!batched) {
 #pragma unroll
             for (int k = 0; k < KPT; ++k) {
                 const uint64_t i = s0 + tb + (uint64_t)k * BK_T;
@@ -919,6 +990,7 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
                     pk[k] = atomicAdd(&hist[b], 1u) | (uint32_t)b << 16;
                 }
             }
+          }
         }
         __syncthreads();  // A
         BKST(0);
@@ -948,39 +1020,79 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
         }
         __syncthreads();  // C
         BKST(2);
+        if (DSORT_PLACE_PB > 0 && s0 + SUB <= n) {
+            // (a whole sub-tile: every key placed) the LDS starts of PB keys read together, then
+            // their stores -- one round trip per batch instead of one per key behind its branch
+            constexpr int PB = DSORT_PLACE_PB > 0 ? DSORT_PLACE_PB : 1;
 #pragma unroll
-        for (int k = 0; k < KPT; ++k)
-            if (pk[k] != ~0u) lk[hist[pk[k] >> 16] + (pk[k] & 0xFFFF)] = key[k];
+            for (int k0 = 0; k0 < KPT; k0 += PB) {
+                uint32_t at[PB];
+#pragma unroll
+                for (int g = 0; g < PB; ++g) at[g] = hist[pk[k0 + g] >> 16];
+#pragma unroll
+                for (int g = 0; g < PB; ++g) lk[at[g] + (pk[k0 + g] & 0xFFFF)] = key[k0 + g];
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < KPT; ++k)
+                if (pk[k] != ~0u) lk[hist[pk[k] >> 16] + (pk[k] & 0xFFFF)] = key[k];
+        }
         __syncthreads();  // D
         BKST(3);
         if (owner) hist[tb] = 0;  // (the next sub-tile's atomics follow barrier E)
-        // whole lines: 4 lanes per line, 16 bytes per lane
-        for (uint32_t it = tb; it < 4 * C; it += BK_T) {
-            const uint32_t j = it >> 2, q = it & 3;
-            const uint32_t b = lmap[j];
-            const uint2 sb = st[b];
-            const uint32_t cv = sb.y & 31, cp = (sb.y >> 5) & 31, cL = sb.y >> 11, lb = sb.x & 0xFFFF;
-            const uint32_t e0 = (j - (sb.x >> 16)) * LK + KPL * q;
-            T v[KPL];
-            bool ok[KPL];
-            bool full = true;
+        // whole lines: 4 lanes per line, 16 bytes per lane; LU line entries per lane at a time, each
+        // stage's LDS reads (line map, bucket state, keys) issued for all of them before any is used
+        // (one entry at a time waited three LDS round trips per 16 bytes written)
+        constexpr int LU = DSORT_LINE_LU;
+        for (uint32_t it0 = tb; it0 < 4 * C; it0 += LU * BK_T) {
+            uint32_t j[LU], q[LU], b[LU];
+            bool has[LU];
 #pragma unroll
-            for (int t = 0; t < KPL; ++t) {
-                const uint32_t e = e0 + t;
-                ok[t] = e >= cp && e < cL;
-                full = full && ok[t];
-                v[t] = e < cv ? carry[b * LK + cswz(b, e)] : lk[lb + e - cv];
+            for (int u = 0; u < LU; ++u) {
+                const uint32_t it = it0 + (uint32_t)u * BK_T;
+                has[u] = it < 4 * C;
+                j[u] = (has[u] ? it : it0) >> 2;
+                q[u] = (has[u] ? it : it0) & 3;
             }
-            const uint32_t gi = sgb[b] + e0;  // mod 2^32
-            T *tgt = (sb.y >> 10) & 1 ? out2 : out;
-            if (full) {
-                V vv;
-                __builtin_memcpy(&vv, v, sizeof(V));
-                *reinterpret_cast<V *>(tgt + gi) = vv;
-            } else {
 #pragma unroll
-                for (int t = 0; t < KPL; ++t)
-                    if (ok[t]) tgt[(uint32_t)(gi + t)] = v[t];
+            for (int u = 0; u < LU; ++u) b[u] = lmap[j[u]];
+            uint2 sb[LU];
+            uint32_t gb0[LU];
+#pragma unroll
+            for (int u = 0; u < LU; ++u) {
+                sb[u] = st[b[u]];
+                gb0[u] = sgb[b[u]];
+            }
+            T v[LU][KPL];
+            bool ok[LU][KPL], full[LU];
+            uint32_t e0[LU];
+#pragma unroll
+            for (int u = 0; u < LU; ++u) {
+                const uint32_t cv = sb[u].y & 31, cp = (sb[u].y >> 5) & 31, cL = sb[u].y >> 11, lb = sb[u].x & 0xFFFF;
+                e0[u] = (j[u] - (sb[u].x >> 16)) * LK + KPL * q[u];
+                full[u] = true;
+#pragma unroll
+                for (int t = 0; t < KPL; ++t) {
+                    const uint32_t e = e0[u] + t;
+                    ok[u][t] = e >= cp && e < cL;
+                    full[u] = full[u] && ok[u][t];
+                    v[u][t] = e < cv ? carry[b[u] * LK + cswz(b[u], e)] : lk[lb + e - cv];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < LU; ++u) {
+                if (!has[u]) continue;
+                const uint32_t gi = gb0[u] + e0[u];  // mod 2^32
+                T *tgt = (sb[u].y >> 10) & 1 ? out2 : out;
+                if (full[u]) {
+                    V vv;
+                    __builtin_memcpy(&vv, v[u], sizeof(V));
+                    *reinterpret_cast<V *>(tgt + gi) = vv;
+                } else {
+#pragma unroll
+                    for (int t = 0; t < KPL; ++t)
+                        if (ok[u][t]) tgt[(uint32_t)(gi + t)] = v[u][t];
+                }
             }
         }
         if (last) break;

@@ -41,9 +41,13 @@ import os  # noqa: E402
 # the build the counters were taken on (bench.py uses the table as measured only for this build)
 LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..",
                    "distributed-sorting-with-fault-tolerance_amd", "lib", "libdsort.so")
+# (round 5: the profiling script records the sha256 of the library it ran ON THE BOX in
+# gpurun_out/pmc_lib_sha256.txt; the local file is only the fallback)
+SHA_BOX = os.path.join("gpurun_out", "pmc_lib_sha256.txt")
+sha = open(SHA_BOX).read().split()[0] if os.path.exists(SHA_BOX) else hashlib.sha256(open(LIB, "rb").read()).hexdigest()
 doc = {"source": "rocprofv3 --pmc (separate passes, scripts/dev/pmc_sub.sh) over scripts/dev/ktime.py --reps 1, "
                  "2^30 keys; converted by scripts/dev/pmc_json.py",
-       "lib_sha256": hashlib.sha256(open(LIB, "rb").read()).hexdigest(),
+       "lib_sha256": sha, "lib_sha256_from": "the box" if os.path.exists(SHA_BOX) else "the local build",
        "keys": 1 << 30, "key_bytes": 4, "dist": "uniform", "kernels": per_launch(t32),
        "int64": {"keys": 1 << 30, "key_bytes": 8, "dist": "zipf", "kernels": per_launch(t64)}}
 json.dump(doc, open(sys.argv[1] if len(sys.argv) > 1 else "profiles/r2_pmc_traffic.json", "w"), indent=1)

@@ -203,3 +203,36 @@ def test_c_master_rccl_one_gpu_with_comm_deadline():
                           extra=["--comm-timeout-ms", "60000"])
     assert r["ok"], r
     assert r["transport"] == "rccl" and r["epochs"] == 1 and r["slices"] == [(1 << 25) + 7]
+
+
+def test_c3_rank_layout_one_rccl_rank_bit_exact(gpu_ctx):
+    """One rank of config C3 (2^32 int32 over 8 GPUs) on this box's one GPU, the layout of
+    scripts/c3_rank.py: 2^29 keys (rank 3's chunk of the global synthetic input), the bucket
+    exchange over one RCCL rank with DSORT_OPT_BUCKETS = 128 -- 4M-key buckets, as 1024 global
+    buckets give each of 8 ranks -- so the second level takes its large-bucket geometry (16384-key
+    tiles).  The rank's slice equals torch.sort of its keys element for element (the rank-local
+    part of server.c:414-415 + 500-515's replacement)."""
+    import ctypes
+
+    import torch
+
+    import dsort
+    ctx = gpu_ctx
+    n = 1 << 29
+    t = torch.empty(n, dtype=torch.int32, device="cuda")
+    ctx.gen_uniform(t, SEED, 3 * n)
+    ctx.comm_init(1, 0, dsort.Context.unique_id())
+    try:
+        with ctx.options(buckets=128):
+            ptr, nout = ctx.sample_sort_dev(t)
+            ctx.synchronize()
+        st = ctx.stats()
+        assert nout == n and st["exchange_path"] == 1 and st["tile_keys"] == 16384, st
+        out = torch.empty_like(t)
+        ctx.check(ctx.lib.dsort_copy_d2d(ctx.h, ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ptr), 4 * n))
+        torch.cuda.synchronize()
+        assert torch.equal(out, torch.sort(t).values)
+    finally:
+        ctx.comm_destroy()
+    del t, out
+    torch.cuda.empty_cache()
