@@ -534,16 +534,18 @@ __global__ void __launch_bounds__(BK_MAXB) pair_splitter_kernel(const int64_t *_
     }
 }
 
-// A sub-tile's keys of one thread: in[i0 + k BK_T], k < KPT.  A whole sub-tile (the usual case,
-// workgroup-uniform) loads without bounds checks: with them every load sat in a branch of its own
-// (an exec-mask save, a conditional jump), and the loads of a thread were not issued together.
+// A sub-tile's keys of one thread: in[i0 + k BK_T], k < KPT.  UNGUARDED: a whole sub-tile (the
+// usual case, workgroup-uniform) loads without bounds checks -- with them every load sat in a
+// branch of its own (an exec-mask save, a conditional jump), and the scatter's loads were not
+// issued together (int32 scatter 2.59 -> 2.49 ms, int64 Zipf 4.53 -> 4.45 ms).  The histogram keeps
+// the checks: unguarded, its int64 instance took 2.21 -> 3.09 ms at 2^30 Zipf (int32: no change).
 #ifndef DSORT_NOGUARD
 #define DSORT_NOGUARD 1
 #endif
-template <typename T, int KPT>
+template <typename T, int KPT, bool UNGUARDED = true>
 __device__ __forceinline__ void load_sub(const T *__restrict__ in, uint64_t i0, uint64_t n, uint64_t sub_end,
                                          T (&x)[KPT]) {
-    if (DSORT_NOGUARD && sub_end <= n) {
+    if (UNGUARDED && DSORT_NOGUARD && sub_end <= n) {
 #pragma unroll
         for (int k = 0; k < KPT; ++k) x[k] = in[i0 + (uint64_t)k * BK_T];
     } else {
@@ -618,14 +620,14 @@ __global__ void __launch_bounds__(BK_T, 2) bucket_hist_kernel(const T *__restric
     // the next sub-tile's keys are loaded while the current one is counted (two workgroups per CU
     // alone left the loads' latency exposed: 0.79 ms for 4.3 GB)
     T nxt[KPT];
-    load_sub<T, KPT>(in, g0 + threadIdx.x, n, g0 + SUB, nxt);
+    load_sub<T, KPT, false>(in, g0 + threadIdx.x, n, g0 + SUB, nxt);
 #pragma unroll 1
     for (int sub = 0; sub < subs; ++sub) {
         const uint64_t b0 = g0 + (uint64_t)sub * SUB + threadIdx.x;
         T key[KPT];
 #pragma unroll
         for (int k = 0; k < KPT; ++k) key[k] = nxt[k];
-        if (sub + 1 < subs) load_sub<T, KPT>(in, b0 + SUB, n, b0 - threadIdx.x + 2 * SUB, nxt);
+        if (sub + 1 < subs) load_sub<T, KPT, false>(in, b0 + SUB, n, b0 - threadIdx.x + 2 * SUB, nxt);
         // the buckets of the thread's keys, two per word (bucket ids: BkIds)
         uint32_t idw[KPT / 2] = {};
         // (the mode branch outside the key loop: a slot array would cost the second workgroup)
@@ -929,12 +931,7 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
 #ifndef DSORT_SCATTER_CB
 #define DSORT_SCATTER_CB 4  // keys per batch of the whole-sub-tile classify (int32, fixed map)
 #endif
-#ifndef DSORT_PLACE_PB
-#define DSORT_PLACE_PB 4    // keys per batch of the whole-sub-tile placement (0: key by key)
-#endif
-#ifndef DSORT_LINE_LU
-#define DSORT_LINE_LU 2     // line entries per lane and step of the line phase
-#endif
+
         if (DSORT_HOT_SCATTER && m.hot) {  // (runs of one bucket: aggregated ranks, bucket_runs_hint)
 #pragma unroll
             for (int k = 0; k < KPT; ++k) {
@@ -1020,79 +1017,39 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
         }
         __syncthreads();  // C
         BKST(2);
-        if (DSORT_PLACE_PB > 0 && s0 + SUB <= n) {
-            // (a whole sub-tile: every key placed) the LDS starts of PB keys read together, then
-            // their stores -- one round trip per batch instead of one per key behind its branch
-            constexpr int PB = DSORT_PLACE_PB > 0 ? DSORT_PLACE_PB : 1;
 #pragma unroll
-            for (int k0 = 0; k0 < KPT; k0 += PB) {
-                uint32_t at[PB];
-#pragma unroll
-                for (int g = 0; g < PB; ++g) at[g] = hist[pk[k0 + g] >> 16];
-#pragma unroll
-                for (int g = 0; g < PB; ++g) lk[at[g] + (pk[k0 + g] & 0xFFFF)] = key[k0 + g];
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < KPT; ++k)
-                if (pk[k] != ~0u) lk[hist[pk[k] >> 16] + (pk[k] & 0xFFFF)] = key[k];
-        }
+        for (int k = 0; k < KPT; ++k)
+            if (pk[k] != ~0u) lk[hist[pk[k] >> 16] + (pk[k] & 0xFFFF)] = key[k];
         __syncthreads();  // D
         BKST(3);
         if (owner) hist[tb] = 0;  // (the next sub-tile's atomics follow barrier E)
-        // whole lines: 4 lanes per line, 16 bytes per lane; LU line entries per lane at a time, each
-        // stage's LDS reads (line map, bucket state, keys) issued for all of them before any is used
-        // (one entry at a time waited three LDS round trips per 16 bytes written)
-        constexpr int LU = DSORT_LINE_LU;
-        for (uint32_t it0 = tb; it0 < 4 * C; it0 += LU * BK_T) {
-            uint32_t j[LU], q[LU], b[LU];
-            bool has[LU];
+        // whole lines: 4 lanes per line, 16 bytes per lane
+        for (uint32_t it = tb; it < 4 * C; it += BK_T) {
+            const uint32_t j = it >> 2, q = it & 3;
+            const uint32_t b = lmap[j];
+            const uint2 sb = st[b];
+            const uint32_t cv = sb.y & 31, cp = (sb.y >> 5) & 31, cL = sb.y >> 11, lb = sb.x & 0xFFFF;
+            const uint32_t e0 = (j - (sb.x >> 16)) * LK + KPL * q;
+            T v[KPL];
+            bool ok[KPL];
+            bool full = true;
 #pragma unroll
-            for (int u = 0; u < LU; ++u) {
-                const uint32_t it = it0 + (uint32_t)u * BK_T;
-                has[u] = it < 4 * C;
-                j[u] = (has[u] ? it : it0) >> 2;
-                q[u] = (has[u] ? it : it0) & 3;
+            for (int t = 0; t < KPL; ++t) {
+                const uint32_t e = e0 + t;
+                ok[t] = e >= cp && e < cL;
+                full = full && ok[t];
+                v[t] = e < cv ? carry[b * LK + cswz(b, e)] : lk[lb + e - cv];
             }
+            const uint32_t gi = sgb[b] + e0;  // mod 2^32
+            T *tgt = (sb.y >> 10) & 1 ? out2 : out;
+            if (full) {
+                V vv;
+                __builtin_memcpy(&vv, v, sizeof(V));
+                *reinterpret_cast<V *>(tgt + gi) = vv;
+            } else {
 #pragma unroll
-            for (int u = 0; u < LU; ++u) b[u] = lmap[j[u]];
-            uint2 sb[LU];
-            uint32_t gb0[LU];
-#pragma unroll
-            for (int u = 0; u < LU; ++u) {
-                sb[u] = st[b[u]];
-                gb0[u] = sgb[b[u]];
-            }
-            T v[LU][KPL];
-            bool ok[LU][KPL], full[LU];
-            uint32_t e0[LU];
-#pragma unroll
-            for (int u = 0; u < LU; ++u) {
-                const uint32_t cv = sb[u].y & 31, cp = (sb[u].y >> 5) & 31, cL = sb[u].y >> 11, lb = sb[u].x & 0xFFFF;
-                e0[u] = (j[u] - (sb[u].x >> 16)) * LK + KPL * q[u];
-                full[u] = true;
-#pragma unroll
-                for (int t = 0; t < KPL; ++t) {
-                    const uint32_t e = e0[u] + t;
-                    ok[u][t] = e >= cp && e < cL;
-                    full[u] = full[u] && ok[u][t];
-                    v[u][t] = e < cv ? carry[b[u] * LK + cswz(b[u], e)] : lk[lb + e - cv];
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < LU; ++u) {
-                if (!has[u]) continue;
-                const uint32_t gi = gb0[u] + e0[u];  // mod 2^32
-                T *tgt = (sb[u].y >> 10) & 1 ? out2 : out;
-                if (full[u]) {
-                    V vv;
-                    __builtin_memcpy(&vv, v[u], sizeof(V));
-                    *reinterpret_cast<V *>(tgt + gi) = vv;
-                } else {
-#pragma unroll
-                    for (int t = 0; t < KPL; ++t)
-                        if (ok[u][t]) tgt[(uint32_t)(gi + t)] = v[u][t];
-                }
+                for (int t = 0; t < KPL; ++t)
+                    if (ok[t]) tgt[(uint32_t)(gi + t)] = v[t];
             }
         }
         if (last) break;

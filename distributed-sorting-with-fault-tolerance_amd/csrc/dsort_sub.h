@@ -796,10 +796,7 @@ __global__ void __launch_bounds__(SB_LT<T>, SB_LT<T> / 128) sb_local_kernel(T *_
     // In groups of G keys: the slot-table reads, then the splitter reads, then the atomics, so a
     // key's LDS round trips do not wait for the previous key's.  A key past the chunk adds 0.
     // (int32: 31 keys and their ranks are already live; batching spills and measured slower)
-#ifndef DSORT_SB_G32
-#define DSORT_SB_G32 1
-#endif
-    constexpr int G = sizeof(T) == 4 ? DSORT_SB_G32 : 8;
+    constexpr int G = sizeof(T) == 4 ? 1 : 8;
     // a whole chunk: only the first and last slot rows can fall outside it
     const bool whole = c.len == (uint32_t)CHL;
     if constexpr (G == 1) {

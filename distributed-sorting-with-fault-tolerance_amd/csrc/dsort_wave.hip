@@ -658,13 +658,7 @@ __device__ __forceinline__ void bin_put(T xv, T mn, const BinMap<T> &bm, uint32_
 // of a thread's atomics issued (in batches of 8) before any result is used.  That pays at the
 // int64 tile's 4 waves per SIMD (bin sort 8.46 -> 8.18 ms at 2^30 Zipf); at int32's 8 waves per
 // SIMD the other waves already hide the latency and one key at a time is faster (3.26 vs 3.61 ms).
-#ifndef DSORT_BIN_BATCH32
-#define DSORT_BIN_BATCH32 0
-#endif
-#ifndef DSORT_BIN_G
-#define DSORT_BIN_G 8
-#endif
-template <typename T> constexpr bool BIN_BATCH = sizeof(T) == 8 || DSORT_BIN_BATCH32;
+template <typename T> constexpr bool BIN_BATCH = sizeof(T) == 8;
 template <typename T>
 struct BinAt {
     uint32_t word, sh, inc;
@@ -687,7 +681,7 @@ __device__ __forceinline__ void bin_count(const T (&x)[R], T mn, const BinMap<T>
 }
 template <typename T>
 __device__ __forceinline__ void bin_place(const T (&x)[R], T mn, const BinMap<T> &bm, uint32_t *cw, T *s) {
-    constexpr int G = DSORT_BIN_G;  // atomics in flight per thread (more spill at 64 registers)
+    constexpr int G = 8;  // atomics in flight per thread (more spill at 64 registers)
 #pragma unroll
     for (int g = 0; g < R; g += G) {
         uint32_t old[G];
