@@ -610,6 +610,7 @@ __global__ void __launch_bounds__(BK_T, 2) bucket_hist_kernel(const T *__restric
     __shared__ typename CT::C spl[BK_MAXB + 1];
     __shared__ uint32_t rng[BK_SLOTS];
     const BkMap m = *map;
+    if (!ADP && m.ad) return;  // (int32: the adaptive map's instance counts this sort, first_level)
     __shared__ uint32_t hist[BK_MAXB];
     load_splitters<T>(spl_g, BP, spl);
     for (int b = threadIdx.x; b < B; b += BK_T) hist[b] = 0;

@@ -2138,26 +2138,28 @@ static int first_level(dsort_ctx *ctx, const T *d_in, uint64_t n, uint64_t ioff,
     hipLaunchKernelGGL(bucket_slotmap_kernel<T>, dim3(1), dim3(BK_MAXB), 0, s, L.spl, B, n, L.map);
     ctx->bk_hot = &L.map->hot;
     // int32: which map did the splitters choose -- the fixed one (packed lookup) or the adaptive
-    // one (many small keys)?  Its kernels are separate instances, so the host waits for the choice
-    // (a few us of idle GPU; launching both instances and letting the other return at once costs a
-    // grid of empty workgroups each, about 40 us for the scatter's)
+    // one (many small keys)?  Its kernels are separate instances, so the host reads the choice back
+    // (launching both scatter instances and letting the other return at once would cost a grid of
+    // empty workgroups, about 40 us)
     bool ad = false;
     BkMap *hm = reinterpret_cast<BkMap *>(reinterpret_cast<char *>(hb) + (size_t)(BK_MAXB + 1) * 8 + (size_t)BK_MAXB * 16);
     if constexpr (!Comp<T>::ADAPT) {
         DSORT_HIP(ctx, hipMemcpyAsync(hm, L.map, sizeof(BkMap), hipMemcpyDeviceToHost, s));
         DSORT_HIP(ctx, hipEventRecord(ctx->bucket_ev, s));
-        if (int rc_ = sync_event(ctx, ctx->bucket_ev, "slot map")) return rc_;
-        ad = hm->ad != 0;
     }
     if ((rc = stage_event(ctx, s, timed, 9))) return rc;
+    // (int32: the fixed map's histogram goes first -- it returns at once when the map is adaptive
+    // -- so the GPU is busy while the host reads the map's choice; only the adaptive case launches
+    // a second instance behind it)
+    hipLaunchKernelGGL((bucket_hist_kernel<T, false>), dim3((unsigned)L.G), dim3(BK_T), 0, s, d_in, n, L.spl, L.map, B,
+                       BP, L.subs, L.cnt, ioff, L.ids);
     if constexpr (!Comp<T>::ADAPT) {
+        if (int rc_ = sync_event(ctx, ctx->bucket_ev, "slot map")) return rc_;
+        ad = hm->ad != 0;
         if (ad)
             hipLaunchKernelGGL((bucket_hist_kernel<T, true>), dim3((unsigned)L.G), dim3(BK_T), 0, s, d_in, n, L.spl,
                                L.map, B, BP, L.subs, L.cnt, ioff, L.ids);
     }
-    if (!ad)
-        hipLaunchKernelGGL((bucket_hist_kernel<T, false>), dim3((unsigned)L.G), dim3(BK_T), 0, s, d_in, n, L.spl, L.map,
-                           B, BP, L.subs, L.cnt, ioff, L.ids);
     if ((rc = stage_event(ctx, s, timed, 10))) return rc;
     hipLaunchKernelGGL(bucket_colsum_kernel, dim3((unsigned)L.nchunk), dim3(BK_MAXB), 0, s, L.cnt, (uint32_t)L.G, B,
                        L.part);
