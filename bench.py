@@ -505,13 +505,18 @@ def run_single(args):
         raise SystemExit("bench: sorted output failed verification")
     torch.cuda.synchronize()
     # the timed steps run back to back (a sort returns while its last kernels run; nothing is read
-    # back in between), then as many steps again, each followed by a read of its HIP events, give
-    # the per-stage device times of the roofline (outside the timed region)
+    # back in between) with no stage events (DSORT_OPT_STAGE_TIMING = 0: each event costs the GPU a
+    # few us between two kernels), then as many steps again, each with its HIP events and followed
+    # by a read of them, give the per-stage device times of the roofline (outside the timed region)
+    ctx.set_option("stage_timing", 0)
+    ctx.sort_dev(t_in, out)  # (untimed: the first sort of this mode)
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         ctx.sort_dev(t_in, out)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
+    ctx.set_option("stage_timing", 1)
     acc = {k: 0.0 for k in ("merge_kernel_ms", "block_sort_ms", "total_ms", "tile_sort_kernel_ms", "partition_ms",
                             "bucket_hist_ms", "bucket_scatter_ms", "sub_partition_ms")}
     npass, tkeys = 0, 0
@@ -593,6 +598,7 @@ def run_multi(args, rank, world):
     dist.all_gather(allinfo, info)
     fps = [None] * world
     dist.all_gather_object(fps, (in_fp[0], in_fp[1], fs.value, fx.value))
+    ctx.set_option("stage_timing", 0)  # (no stage events in the timed steps, as at N = 1)
     torch.cuda.synchronize()
     dist.barrier()
     t0 = time.perf_counter()
@@ -601,6 +607,7 @@ def run_multi(args, rank, world):
     torch.cuda.synchronize()
     dist.barrier()
     t1 = time.perf_counter()
+    ctx.set_option("stage_timing", 1)
     el = torch.tensor([t1 - t0], dtype=torch.float64)
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
     # per-stage device times from as many instrumented steps again (outside the timed region)

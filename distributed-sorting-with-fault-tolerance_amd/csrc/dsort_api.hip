@@ -996,6 +996,7 @@ int dsort_init(dsort_ctx **out, int device) {
         if (hipEventCreate(&e) != hipSuccess) ctx->ev_ok = false;
     for (auto &e : ctx->kev)
         if (hipEventCreate(&e) != hipSuccess) ctx->ev_ok = false;
+    ctx->ev_created = ctx->ev_ok;
     *out = ctx;
     return DSORT_OK;
 }
@@ -1095,6 +1096,11 @@ int dsort_set_option(dsort_ctx *ctx, int option, int64_t v) {
             if (v < -1) return set_err(ctx, DSORT_EINVAL, "DSORT_OPT_TEST_FAIL_EXCHANGE: -1 or a collective index");
             o.test_fail_exchange = v;
             return DSORT_OK;
+        case DSORT_OPT_STAGE_TIMING:
+            if (v != 0 && v != 1) return set_err(ctx, DSORT_EINVAL, "DSORT_OPT_STAGE_TIMING: 0 or 1");
+            o.stage_timing = v;
+            ctx->ev_ok = ctx->ev_created && v != 0;
+            return DSORT_OK;
         default:
             return set_err(ctx, DSORT_EINVAL, "unknown option " + std::to_string(option));
     }
@@ -1113,6 +1119,7 @@ int dsort_get_option(const dsort_ctx *ctx, int option, int64_t *v) {
         case DSORT_OPT_COMM_TIMEOUT_MS: *v = o.comm_timeout_ms; return DSORT_OK;
         case DSORT_OPT_TEST_HOLD_EXCHANGE: *v = o.test_hold_exchange; return DSORT_OK;
         case DSORT_OPT_TEST_FAIL_EXCHANGE: *v = o.test_fail_exchange; return DSORT_OK;
+        case DSORT_OPT_STAGE_TIMING: *v = o.stage_timing; return DSORT_OK;
         case DSORT_OPT_SUB_KEYS: *v = o.sub_keys; return DSORT_OK;
         case DSORT_OPT_SUB_OVERSAMPLE: *v = o.sub_os; return DSORT_OK;
         case DSORT_OPT_SUB_GATHER: *v = o.sub_gather; return DSORT_OK;

@@ -60,6 +60,7 @@ struct dsort_opts {
     int64_t bucket_os = DSORT_BUCKET_OS_DEFAULT;  // DSORT_OPT_BUCKET_OVERSAMPLE
     int64_t max_logf = -1;          // DSORT_OPT_MAX_FANIN_LOG2: -1 = per key type default
     int64_t kill_after_pass = -1;   // DSORT_OPT_KILL_AFTER_STAGE
+    int64_t stage_timing = 1;       // DSORT_OPT_STAGE_TIMING
     int64_t kill_in_exchange = -1;  // DSORT_OPT_KILL_IN_EXCHANGE
     int64_t comm_timeout_ms = 0;    // DSORT_OPT_COMM_TIMEOUT_MS
     int64_t test_hold_exchange = 0; // DSORT_OPT_TEST_HOLD_EXCHANGE
@@ -176,7 +177,8 @@ struct dsort_ctx {
     static constexpr int kMaxKev = 128;  // per-launch events of the merge kernel (2 per pass)
     hipEvent_t kev[kMaxKev] = {};
     int kev_used = 0;
-    bool ev_ok = false;
+    bool ev_ok = false;       // stage events recorded: created, and DSORT_OPT_STAGE_TIMING on
+    bool ev_created = false;
     dsort_stats stats = {};
 };
 

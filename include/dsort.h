@@ -149,6 +149,10 @@ int dsort_synchronize(dsort_ctx *ctx);
                                          sample sort (0 = the key-count all-gather); its peers must
                                          leave at the next status gate with DSORT_ECOMM instead of
                                          blocking.  -1 = off (default)                               */
+#define DSORT_OPT_STAGE_TIMING 14      /* ABI 5: 1 = every sort records its per-stage HIP events for
+                                         dsort_get_stats (default); 0 = none (the *_ms statistics read
+                                         0).  Each event sits between two kernels of the sort: about
+                                         6 us of idle GPU apiece, ~1 % of a 2^30-key sort */
 int dsort_set_option(dsort_ctx *ctx, int option, int64_t value);
 int dsort_get_option(const dsort_ctx *ctx, int option, int64_t *value);
 

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Phase timeline of the bin sort (bin_sort_kernel<int, true>) from a DSORT_STAMPS build
+"""Phase timeline of the bin sort (bin_sort_kernel<T, true>) from a DSORT_STAMPS build
 (DSORT_LIB=build_variants/stamps/libdsort.so): per tile, s_memtime deltas between the phase stamps
 of wave 0 and wave 15 (median / p90).  Stamp slots: 0 start, 1 gathered, 2 range, 3 counted,
 4 starts, 5 placed, 6 window pass 1, 7 pass 2 (+3 if any), 8 before out, 9 done."""
@@ -16,8 +16,12 @@ import dsort  # noqa: E402
 
 n = 1 << 30
 ctx = dsort.Context(0)
-t = torch.empty(n, dtype=torch.int32, device="cuda")
-ctx.gen_uniform(t, 0x5EED2026)
+if len(sys.argv) > 1 and sys.argv[1] == "i64z":  # (binstamps.py i64z: 2^30 Zipf int64, config C4)
+    t = torch.empty(n, dtype=torch.int64, device="cuda")
+    ctx.gen_zipf_i64(t, 0x5EED2026)
+else:
+    t = torch.empty(n, dtype=torch.int32, device="cuda")
+    ctx.gen_uniform(t, 0x5EED2026)
 o = torch.empty_like(t)
 ctx.sort_dev(t, o)
 ctx.sort_dev(t, o)

@@ -293,6 +293,31 @@ def test_back_to_back_sorts_on_two_streams(gpu_ctx):
     assert torch.equal(ob, torch.sort(b)[0])
 
 
+def test_stage_timing_off_sorts_the_same_and_records_nothing(gpu_ctx):
+    """DSORT_OPT_STAGE_TIMING = 0 (bench.py's timed steps): the sort records no stage events -- its
+    *_ms statistics read 0 -- and its output is the same as with them; switched back on, the next
+    sort's statistics are measured again."""
+    import torch
+    n = (1 << 25) + 123
+    a = torch.empty(n, dtype=torch.int32, device="cuda")
+    gpu_ctx.gen_uniform(a, 21)
+    o = torch.empty_like(a)
+    exp = torch.sort(a)[0]
+    with gpu_ctx.options(stage_timing=0):
+        assert gpu_ctx.get_option("stage_timing") == 0
+        gpu_ctx.sort_dev(a, o)
+        torch.cuda.synchronize()
+        st = gpu_ctx.stats()
+    assert torch.equal(o, exp)
+    assert st["total_ms"] == 0 and st["tile_sort_kernel_ms"] == 0 and st["bucket_scatter_ms"] == 0, st
+    o.zero_()
+    gpu_ctx.sort_dev(a, o)
+    torch.cuda.synchronize()
+    st = gpu_ctx.stats()
+    assert torch.equal(o, exp)
+    assert st["total_ms"] > 0 and st["tile_sort_kernel_ms"] > 0 and st["bucket_scatter_ms"] > 0, st
+
+
 def test_c3_receive_merge_8_runs_bit_exact(gpu_ctx):
     """Config C3's per-rank receive merge (dsort_api.hip sample_sort step 8: the gather + merge of
     server.c:414-415 / 500-515): 8 sorted runs of 2^26 int32 keys inside one rank's key range
