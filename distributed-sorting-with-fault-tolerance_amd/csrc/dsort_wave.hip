@@ -1172,6 +1172,19 @@ __global__ void __launch_bounds__(64 * W, WG<T>::OCC) bin_sort_kernel(const T *i
         if (known) {
             klo = gt.j0 > 0 ? sp[gt.j0 - 1].k : bk::Comp<T>::key_of(bs[gt.b - 1]);
             khi = gt.j1 < gt.nsub ? sp[gt.j1 - 1].k : bk::Comp<T>::key_of(bs[gt.b]);
+#ifndef DSORT_ONEKEY_TILES
+#define DSORT_ONEKEY_TILES 1
+#endif
+            if (DSORT_ONEKEY_TILES && sizeof(T) == 8 && klo == khi) {
+                // Bounds of one key: every key of the tile is that key (the sub-buckets of a heavy
+                // duplicate, int64 Zipf's keys with thousands of copies) -- the tile is written as
+                // its key, without reading it.  (The first level does the same for pure buckets.)
+                // C4 tile sort 2.94 -> 1.79 ms.  int64 only: the branch makes the gather wait for the
+                // bounds' loads, +0.04 ms on the 2^30 int32 tile sort, where such tiles are rare.)
+                T *o = out + base;
+                for (int i = (int)threadIdx.x; i < valid; i += (int)blockDim.x) o[i] = klo;
+                return;
+            }
         }
         // a duplicate run inside a gathered tile shows as two equal neighbouring splitters
         const int jl = gt.j0 > 0 ? (int)gt.j0 - 1 : 0, jh = (int)gt.j1 - 1;  // splitters around the tile
