@@ -882,6 +882,21 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
         gb = o - ph;
         hist[tb] = 0;
     }
+    // Pure buckets (one key) with out2: their keys are dropped here -- not ranked, placed or written
+    // -- and the host fills their output ranges with their key (bucket_sort: fill_segments_kernel),
+    // write-only.  (Through the line streams they cost the scatter as much LDS work as any key: C4
+    // has 47 % of its keys in pure buckets.)  pmask: bit b = bucket b is pure, one ballot per wave.
+#ifndef DSORT_DROP_PURE
+#define DSORT_DROP_PURE 1
+#endif
+    __shared__ uint32_t pmask[BK_MAXB / 32];
+    {
+        const uint64_t pb = __ballot(DSORT_DROP_PURE && pure != 0);
+        if (lane == 0 && 2 * w + 1 < BK_MAXB / 32) {
+            pmask[2 * w] = (uint32_t)pb;
+            pmask[2 * w + 1] = (uint32_t)(pb >> 32);
+        }
+    }
     const BkMap m = *map;
 #ifndef DSORT_IDS_ONLY
     if (BkIds<T>::ON && (m.ids != 0) != IDS) return;  // (workgroup-uniform: the other variant's sort)
@@ -892,6 +907,10 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
         build_slots<T, true, BK_SLOTB, ADP>(spl, BP, m, rng);
     }
     __syncthreads();
+    bool anyp = false;  // (workgroup-uniform)
+#pragma unroll
+    for (int i = 0; i < BK_MAXB / 32; ++i) anyp = anyp || pmask[i] != 0u;
+    const auto dropped = [&](int b) { return anyp && ((pmask[b >> 5] >> (b & 31)) & 1u) != 0u; };
     const uint64_t g0 = (uint64_t)g * subs * SUB;
 #ifdef DSORT_STAMPS
     uint64_t bk_acc[8] = {}, bk_t0 = __builtin_amdgcn_s_memtime();
@@ -939,8 +958,9 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
                 const uint64_t i = s0 + tb + (uint64_t)k * BK_T;
                 const bool act = i < n;
                 const int b = IDS ? (int)sl[k] : bucket_fast<T, true, true, ADP>(spl_look, rng, sl[k], key[k], CT::make(key[k], i + ioff));
-                const uint32_t r = bucket_bump<true>(hist, b, act);
-                pk[k] = act ? r | (uint32_t)b << 16 : ~0u;
+                const bool a = act && !dropped(b);
+                const uint32_t r = bucket_bump<true>(hist, b, a);
+                pk[k] = a ? r | (uint32_t)b << 16 : ~0u;
             }
         } else {
           bool batched = false;
@@ -973,8 +993,14 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
                             b[g] = packed_slow(reinterpret_cast<const int64_t *>(spl_look), r[g], (int32_t)key[k0 + g],
                                                (int64_t)CT::make(key[k0 + g], s0 + tb + (uint64_t)(k0 + g) * BK_T + ioff));
                 }
+                if (anyp) {
 #pragma unroll
-                for (int g = 0; g < CB; ++g) pk[k0 + g] = atomicAdd(&hist[b[g]], 1u) | (uint32_t)b[g] << 16;
+                    for (int g = 0; g < CB; ++g)
+                        pk[k0 + g] = dropped(b[g]) ? ~0u : atomicAdd(&hist[b[g]], 1u) | (uint32_t)b[g] << 16;
+                } else {
+#pragma unroll
+                    for (int g = 0; g < CB; ++g) pk[k0 + g] = atomicAdd(&hist[b[g]], 1u) | (uint32_t)b[g] << 16;
+                }
             }
            }
           }
@@ -985,7 +1011,7 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
                 pk[k] = ~0u;
                 if (i < n) {
                     const int b = IDS ? (int)sl[k] : bucket_fast<T, true, true, ADP>(spl_look, rng, sl[k], key[k], CT::make(key[k], i + ioff));
-                    pk[k] = atomicAdd(&hist[b], 1u) | (uint32_t)b << 16;
+                    if (!dropped(b)) pk[k] = atomicAdd(&hist[b], 1u) | (uint32_t)b << 16;
                 }
             }
           }

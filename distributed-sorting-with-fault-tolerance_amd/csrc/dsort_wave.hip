@@ -1731,17 +1731,37 @@ struct FillSeg {
     uint64_t dst, len;
     T key;
 };
+// 16-byte stores from the segment's first 16-byte boundary (the keys before it and the ones after
+// the last whole vector by the first threads of block 0), FILL_U stores in flight per thread.  (One
+// key per lane and store: 4 GB of C4's pure buckets at 3 TB/s.)
+constexpr int FILL_U = 8;
 template <typename T>
 __global__ void __launch_bounds__(256) fill_segments_kernel(T *out, const FillSeg<T> *segs) {
+    using V = typename std::conditional<sizeof(T) == 4, int4, longlong2>::type;
+    constexpr int N = 16 / (int)sizeof(T);
     const FillSeg<T> f = segs[blockIdx.y];
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < f.len; i += (uint64_t)gridDim.x * 256)
-        out[f.dst + i] = f.key;
+    T *p = out + f.dst;
+    const uint64_t h = ((16 - ((uintptr_t)p & 15)) & 15) / sizeof(T);
+    const uint64_t head = h < f.len ? h : f.len;
+    const uint64_t nv = (f.len - head) / N, t0 = head + nv * N;
+    if (blockIdx.x == 0 && threadIdx.x < head) p[threadIdx.x] = f.key;
+    if (blockIdx.x == 0 && threadIdx.x < f.len - t0) p[t0 + threadIdx.x] = f.key;
+    V v;
+    T *vk = reinterpret_cast<T *>(&v);
+#pragma unroll
+    for (int j = 0; j < N; ++j) vk[j] = f.key;
+    V *q = reinterpret_cast<V *>(p + head);
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 * FILL_U + threadIdx.x; i < nv; i += (uint64_t)gridDim.x * 256 * FILL_U) {
+#pragma unroll
+        for (int u = 0; u < FILL_U; ++u)
+            if (i + (uint64_t)u * 256 < nv) q[i + (uint64_t)u * 256] = v;
+    }
 }
 
 template <typename T>
 static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_t *hb, int B, uint64_t m_in,
                     hipStream_t s, bool timed, bool local, const uint8_t *pure, bool pure_done, const void *bspl,
-                    bool retry = false, const PieceMap<T> *pm = nullptr) {
+                    bool retry = false, const PieceMap<T> *pm = nullptr, const T *fill_keys = nullptr) {
     using namespace sb;
     // The tile: int32 buckets above 2M keys take 16384-key tiles -- their sub-buckets (at most
     // SB_MAXS per bucket) would average above a quarter of an 8192-key tile, and sampled 8 per
@@ -1827,7 +1847,8 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
                  o_cnt = take(nch * (SS + 1) * 4), o_offs = take(local ? 0 : nch * SS * 4),
                  o_tt = take(tmax * sizeof(GTile)),
                  o_ovf = take(nsubs * sizeof(Ovf)), o_num = take(8), o_stl = take(B * sizeof(bk::TileRef) + 16),
-                 o_pcs = take(local ? tcap * PS * sizeof(uint2) : 0), o_fill = take(pm ? B * sizeof(FillSeg<T>) : 0);
+                 o_pcs = take(local ? tcap * PS * sizeof(uint2) : 0),
+                 o_fill = take(pm || fill_keys ? B * sizeof(FillSeg<T>) : 0);
     int rc = ensure(ctx, &ctx->sub, &ctx->sub_bytes, off, "sub-bucket partition");
     if (rc) return rc;
     char *a = static_cast<char *>(ctx->sub);
@@ -1848,7 +1869,7 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
     const size_t h_ch = (B * sizeof(BInfo) + 15) & ~(size_t)15, h_stl = h_ch + nch * sizeof(Chunk);
     const size_t h_num = h_stl + B * sizeof(bk::TileRef) + 16;
     const size_t h_fill = h_num + 16;
-    const size_t hbytes = h_fill + (pm ? B * sizeof(FillSeg<T>) : 0);
+    const size_t hbytes = h_fill + (pm || fill_keys ? B * sizeof(FillSeg<T>) : 0);
     if (!ctx->sub_ev && hipEventCreateWithFlags(&ctx->sub_ev, hipEventDisableTiming) != hipSuccess)
         return set_err(ctx, DSORT_EHIP, "hipEventCreate");
     if (int rc_ = sync_event(ctx, ctx->sub_ev, "tile count")) return rc_;  // the previous call's read-back is done with the staging
@@ -1878,13 +1899,14 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
             boff -= ceil_div(pc.len, CH) * CH - pc.len;  // (the last chunk of a piece may be short)
         }
     }
-    // pure buckets of a piece map: their one key written over their output range
+    // pure buckets of a piece map, or whose keys the first-level scatter dropped (fill_keys): their
+    // one key written over their output range
     FillSeg<T> *hf = reinterpret_cast<FillSeg<T> *>(h + h_fill);
     uint32_t nfill = 0;
     uint64_t maxfill = 0;
-    for (int b = 0; pm && b < B; ++b)
+    for (int b = 0; (pm || fill_keys) && b < B; ++b)
         if (pure[b] && hb[b + 1] > hb[b]) {
-            hf[nfill++] = FillSeg<T>{hb[b], hb[b + 1] - hb[b], pm->pure_key[b]};
+            hf[nfill++] = FillSeg<T>{hb[b], hb[b + 1] - hb[b], pm ? pm->pure_key[b] : fill_keys[b]};
             maxfill = std::max(maxfill, hb[b + 1] - hb[b]);
         }
     bk::TileRef *hst = reinterpret_cast<bk::TileRef *>(h + h_stl);
@@ -1912,7 +1934,7 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
     // pure buckets (one key) to the output as they lie, runs of them in one copy (unless the
     // scatter wrote them there); a piece map's pure buckets are filled with their key
     if (nfill) {
-        const unsigned gx = (unsigned)std::min<uint64_t>(ceil_div(maxfill, 256 * 16), 1024);
+        const unsigned gx = (unsigned)std::min<uint64_t>(ceil_div(maxfill, 256 * FILL_U * (16 / sizeof(T))), 1024);
         hipLaunchKernelGGL(fill_segments_kernel<T>, dim3(gx, nfill), dim3(256), 0, s, d_keys,
                            reinterpret_cast<const FillSeg<T> *>(a + o_fill));
         DSORT_HIP(ctx, hipGetLastError());
@@ -2298,8 +2320,16 @@ static int bucket_sort(dsort_ctx *ctx, const T *d_in, T *d_keys, size_t n, hipSt
         // it and copies it to the output.
         std::vector<uint8_t> pure((size_t)B, 0);
         for (int b = 1; b + 1 < B; ++b) pure[b] = Comp<T>::key_of(hspl[b - 1]) == Comp<T>::key_of(hspl[b]);
+        // (the scatter dropped the pure buckets' keys when it had `direct`: the second level fills
+        // their output ranges with their key, dsort_bucket.h)
+        std::vector<T> fk;
+        if (direct && DSORT_DROP_PURE) {
+            fk.assign((size_t)B, T(0));
+            for (int b = 1; b + 1 < B; ++b)
+                if (pure[b]) fk[b] = Comp<T>::key_of(hspl[b]);
+        }
         return sub_sort<T>(ctx, part_out, d_keys, n, hb, B, m, s, timed, ctx->opt.sub_gather != 0, pure.data(),
-                           direct != nullptr, spl);
+                           direct != nullptr, spl, false, nullptr, fk.empty() ? nullptr : fk.data());
     }
     // pass plan: the runs of every bucket; the largest bucket's run count R sets the merge
     // levels L = ceil(log2 R), split into the fewest passes of <= max_logf levels (larger passes
