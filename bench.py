@@ -663,9 +663,12 @@ def result_header(args, world):
             "data": f"synthetic {args.dist} keys, splitmix64(seed={SEED:#x} + global index)"}
 
 
-def stage_roofline(k, w, n, dist="uniform"):
+def stage_roofline(k, w, n, dist="uniform", drop_pure=False):
     """Per-stage HIP-event times of the sort's kernels (the average launch of each over the timed
-    steps) against their algorithmic bytes, and the slowest of them."""
+    steps) against their algorithmic bytes, and the slowest of them.  drop_pure: the one-GPU
+    out-of-place sort, whose first-level scatter writes only the keys outside single-key buckets
+    (round 5: the second level fills those with their key) -- it reads n keys and writes
+    tile_sort_keys; the bucket exchange's scatter writes all n."""
     stages = []
     for kernel, field, per_key, keys_field in STAGE_KERNELS[w]:
         # (int64: the scatter variant that reads the histogram's bucket ids runs on skewed keys --
@@ -675,6 +678,8 @@ def stage_roofline(k, w, n, dist="uniform"):
         if ms <= 0:
             continue
         nb = per_key * w * k[keys_field]
+        if drop_pure and field == "bucket_scatter_ms":
+            nb = w * (k[keys_field] + k["tile_sort_keys"])
         ach = nb / (ms * 1e-3) / 1e9
         stages.append({"kernel": kernel, "avg_launch_ms": round(ms, 4), "algorithmic_bytes_per_launch": nb,
                        "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
@@ -692,7 +697,7 @@ def report_single(args, elapsed, k):
                                     f"(BASELINE metric size); tile {k['tile']} keys, {k['passes']} merge passes",
                         "keys": n, "parallelism": "1 GPU"}
     w = k["w"]
-    stages = stage_roofline(k, w, n, args.dist)
+    stages = stage_roofline(k, w, n, args.dist, drop_pure=True)
     if stages:  # the bucketed path: the dominant kernel is the slowest stage
         dom = max(stages, key=lambda r: r["avg_launch_ms"])
     else:  # below 2^25 keys: tile sort + merge passes

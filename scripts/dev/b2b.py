@@ -15,13 +15,17 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--keys", type=lambda s: int(eval(s, {}, {})), default=1 << 30)
 ap.add_argument("--steps", type=int, default=6)
 ap.add_argument("--dtype", choices=["i32", "i64"], default="i32")
+ap.add_argument("--dist", choices=["uniform", "zipf"], default="uniform")
 ap.add_argument("--timing", type=int, default=1, help="DSORT_OPT_STAGE_TIMING (0: no stage events)")
 a = ap.parse_args()
 ctx = dsort.Context(0)
 if a.timing != 1:
     ctx.set_option("stage_timing", a.timing)
 t = torch.empty(a.keys, dtype=torch.int32 if a.dtype == "i32" else torch.int64, device="cuda")
-ctx.gen_uniform(t, 0x5EED2026)
+if a.dist == "zipf":
+    ctx.gen_zipf_i64(t, 0x5EED2026)
+else:
+    ctx.gen_uniform(t, 0x5EED2026)
 o = torch.empty_like(t)
 ctx.sort_dev(t, o)
 torch.cuda.synchronize()
