@@ -2176,9 +2176,15 @@ static int first_level(dsort_ctx *ctx, const T *d_in, uint64_t n, uint64_t ioff,
     // one (many small keys)?  Its kernels are separate instances, so the host reads the choice back
     // (launching both scatter instances and letting the other return at once would cost a grid of
     // empty workgroups, about 40 us)
-    bool ad = false;
+    // int64 (round 5): likewise which scatter variant -- with or without the histogram's bucket ids
+    // (launching both and letting the other return cost its grid of ~11 K workgroups, 48 us at C4)
+#ifndef DSORT_IDS_READBACK
+#define DSORT_IDS_READBACK 1
+#endif
+    constexpr bool RB = !Comp<T>::ADAPT || (BkIds<T>::ON && DSORT_IDS_READBACK);
+    bool ad = false, ids = false;
     BkMap *hm = reinterpret_cast<BkMap *>(reinterpret_cast<char *>(hb) + (size_t)(BK_MAXB + 1) * 8 + (size_t)BK_MAXB * 16);
-    if constexpr (!Comp<T>::ADAPT) {
+    if constexpr (RB) {
         DSORT_HIP(ctx, hipMemcpyAsync(hm, L.map, sizeof(BkMap), hipMemcpyDeviceToHost, s));
         DSORT_HIP(ctx, hipEventRecord(ctx->bucket_ev, s));
     }
@@ -2188,9 +2194,12 @@ static int first_level(dsort_ctx *ctx, const T *d_in, uint64_t n, uint64_t ioff,
     // a second instance behind it)
     hipLaunchKernelGGL((bucket_hist_kernel<T, false>), dim3((unsigned)L.G), dim3(BK_T), 0, s, d_in, n, L.spl, L.map, B,
                        BP, L.subs, L.cnt, ioff, L.ids);
-    if constexpr (!Comp<T>::ADAPT) {
+    if constexpr (RB) {
         if (int rc_ = sync_event(ctx, ctx->bucket_ev, "slot map")) return rc_;
-        ad = hm->ad != 0;
+        ad = !Comp<T>::ADAPT && hm->ad != 0;
+        ids = BkIds<T>::ON && hm->ids != 0;
+    }
+    if constexpr (!Comp<T>::ADAPT) {
         if (ad)
             hipLaunchKernelGGL((bucket_hist_kernel<T, true>), dim3((unsigned)L.G), dim3(BK_T), 0, s, d_in, n, L.spl,
                                L.map, B, BP, L.subs, L.cnt, ioff, L.ids);
@@ -2211,7 +2220,7 @@ static int first_level(dsort_ctx *ctx, const T *d_in, uint64_t n, uint64_t ioff,
     DSORT_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->ready_ev, 0));
     DSORT_HIP(ctx, hipMemcpyAsync(hb, L.bst, (size_t)(B + 1) * 8, hipMemcpyDeviceToHost, ctx->side));
     if (B > 1) DSORT_HIP(ctx, hipMemcpyAsync(hspl, L.spl, (size_t)(B - 1) * sizeof(C), hipMemcpyDeviceToHost, ctx->side));
-    if constexpr (Comp<T>::ADAPT)  // (int64: the map only for the statistics)
+    if constexpr (!RB)  // (int64: the map only for the statistics)
         DSORT_HIP(ctx, hipMemcpyAsync(hm, L.map, sizeof(BkMap), hipMemcpyDeviceToHost, ctx->side));
     DSORT_HIP(ctx, hipEventRecord(ctx->bucket_ev, ctx->side));
     if ((rc = stage_event(ctx, s, timed, 11))) return rc;
@@ -2224,13 +2233,14 @@ static int first_level(dsort_ctx *ctx, const T *d_in, uint64_t n, uint64_t ioff,
                 hipLaunchKernelGGL((bucket_scatter_lines_kernel<T, false, true>), dim3((unsigned)L.G), dim3(BK_T), 0, s,
                                    d_in, n, L.spl, L.map, B, BP, L.subs, L.offs, part_out, direct, ioff, L.ids);
         }
-        if (!ad)
+        if (!ad && !(RB && ids))
             hipLaunchKernelGGL((bucket_scatter_lines_kernel<T, false, false>), dim3((unsigned)L.G), dim3(BK_T), 0, s, d_in,
                                n, L.spl, L.map, B, BP, L.subs, L.offs, part_out, direct, ioff, L.ids);
     }
-    if constexpr (BkIds<T>::ON)  // (the variant the slot map did not choose returns at once)
-        hipLaunchKernelGGL((bucket_scatter_lines_kernel<T, true>), dim3((unsigned)L.G), dim3(BK_T), 0, s, d_in, n, L.spl,
-                           L.map, B, BP, L.subs, L.offs, part_out, direct, ioff, L.ids);
+    if constexpr (BkIds<T>::ON)  // (without the read-back: the variant the slot map did not choose returns at once)
+        if (!RB || ids)
+            hipLaunchKernelGGL((bucket_scatter_lines_kernel<T, true>), dim3((unsigned)L.G), dim3(BK_T), 0, s, d_in, n,
+                               L.spl, L.map, B, BP, L.subs, L.offs, part_out, direct, ioff, L.ids);
     DSORT_HIP(ctx, hipGetLastError());
     if ((rc = stage_event(ctx, s, timed, 12))) return rc;
     fault_point(ctx, s, 0);  // first-level partition done
