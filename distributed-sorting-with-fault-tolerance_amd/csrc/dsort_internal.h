@@ -55,7 +55,7 @@ struct dsort_opts {
     int64_t buckets = -1;           // DSORT_OPT_BUCKETS: -1 auto, 0 off, B forced
     int64_t bucket_keys = 1 << 20;  // DSORT_OPT_BUCKET_KEYS
 #ifndef DSORT_BUCKET_OS_DEFAULT
-#define DSORT_BUCKET_OS_DEFAULT 256
+#define DSORT_BUCKET_OS_DEFAULT 128
 #endif
     int64_t bucket_os = DSORT_BUCKET_OS_DEFAULT;  // DSORT_OPT_BUCKET_OVERSAMPLE
     int64_t max_logf = -1;          // DSORT_OPT_MAX_FANIN_LOG2: -1 = per key type default

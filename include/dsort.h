@@ -109,7 +109,8 @@ int dsort_synchronize(dsort_ctx *ctx);
 #define DSORT_OPT_BUCKETS 1           /* partition pass: -1 automatic (default), 0 off, B >= 2 forces B
                                          buckets at any size (<= 1024)                               */
 #define DSORT_OPT_BUCKET_KEYS 2       /* nominal keys per bucket (default 2^20)                        */
-#define DSORT_OPT_BUCKET_OVERSAMPLE 3 /* splitter samples per bucket, 1..4096 (default 256)            */
+#define DSORT_OPT_BUCKET_OVERSAMPLE 3 /* splitter samples per bucket, 1..4096 (default 128; 256 before   
+                                         round 5)                                                    */
 /* 4: retired (skewed bucket sizes of the round-1 merge plan); rejected as unknown               */
 #define DSORT_OPT_MAX_FANIN_LOG2 5    /* cap on log2(F) of one merge pass; -1 = per key type default   */
 #define DSORT_OPT_KILL_AFTER_STAGE 6  /* fault injection (config C5): SIGKILL the calling process right

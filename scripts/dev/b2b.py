@@ -17,8 +17,12 @@ ap.add_argument("--steps", type=int, default=6)
 ap.add_argument("--dtype", choices=["i32", "i64"], default="i32")
 ap.add_argument("--dist", choices=["uniform", "zipf"], default="uniform")
 ap.add_argument("--timing", type=int, default=1, help="DSORT_OPT_STAGE_TIMING (0: no stage events)")
+ap.add_argument("--opt", action="append", default=[], help="dsort option name=value (repeatable)")
 a = ap.parse_args()
 ctx = dsort.Context(0)
+for kv in a.opt:
+    k, v = kv.split("=")
+    ctx.set_option(k, int(v))
 if a.timing != 1:
     ctx.set_option("stage_timing", a.timing)
 t = torch.empty(a.keys, dtype=torch.int32 if a.dtype == "i32" else torch.int64, device="cuda")
