@@ -171,9 +171,6 @@ __device__ __forceinline__ int sub_of(const Spl<T> *spl, const uint32_t *rng, T 
     // fewer bank conflicts), then the rare crowded slot
     const uint32_t r = rng[slot_of<T>(key, klo, sh)];
     const int lo = (int)(r & 0x7FFF), hi = (int)(r >> 16);
-#ifdef DSORT_EXP_NOSPL  // (timing experiment only: no splitter reads -- wrong sub-buckets)
-    return lo;
-#endif
     Spl<T> a{}, b{};
     if (lo < hi) a = spl[lo];
     if (lo + 1 < hi) b = spl[lo + 1];
