@@ -65,3 +65,21 @@ def test_report_multi_without_cpu_baseline(capsys):
     bench.report_multi(args, 2, 10 * 4e-3, _per_rank(2, 1 << 30, 4), 4)
     d = json.loads([ln for ln in capsys.readouterr().out.splitlines() if ln.startswith("{")][-1])
     assert "cpu_baseline" not in d and d["n_gpus"] == 2
+
+
+def test_stage_roofline_counts_only_the_scatters_written_keys():
+    """The one-GPU out-of-place sort's first-level scatter writes only the keys outside single-key
+    buckets (round 5: the second level fills those): its algorithmic bytes are n keys read plus
+    tile_sort_keys written; the bucket exchange's scatter (drop_pure False) reads and writes all n."""
+    sys.path.insert(0, REPO)
+    import bench
+
+    n, w, tk = 1 << 30, 8, 507 << 20
+    k = {"bucket_hist_ms": 2.2, "bucket_scatter_ms": 3.9, "sub_partition_ms": 2.4, "tile_sort_kernel_ms": 1.7,
+         "n": n, "tile_sort_keys": tk}
+    one = {s["kernel"].split("<")[0]: s for s in bench.stage_roofline(k, w, n, "zipf", drop_pure=True)}
+    multi = {s["kernel"].split("<")[0]: s for s in bench.stage_roofline(k, w, n, "zipf")}
+    assert one["bucket_scatter_lines_kernel"]["algorithmic_bytes_per_launch"] == w * (n + tk)
+    assert multi["bucket_scatter_lines_kernel"]["algorithmic_bytes_per_launch"] == 2 * w * n
+    assert one["bucket_hist_kernel"]["algorithmic_bytes_per_launch"] == w * n
+    assert one["bin_sort_kernel"]["algorithmic_bytes_per_launch"] == 2 * w * tk
