@@ -723,7 +723,8 @@ __device__ unsigned long long g_sbstamps[(1u << 18) * 8];
 #endif
 // int32: 1024 threads of 15 keys, 8 waves per SIMD at two workgroups per CU: twice the waves of
 // round 2's 512 threads of 31 keys to hide the lookups' LDS round trips (2.33 -> 2.02 ms at 2^30).
-// (int64 at 1024 threads of 6 keys: C4 -0.24 ms, 2^30 uniform int64 +0.4 ms; kept at 512 x 13)
+// (int64 at 1024 threads of 6 keys: round 4 C4 -0.24 ms, 2^30 uniform int64 +0.4 ms; round 5, with the
+// one-key slots, C4 +0.9 ms (profiles/r5_ab_c4_local_1024x6.log): kept at 512 x 13)
 template <typename T> constexpr int SB_LT = sizeof(T) == 4 ? 1024 : 512;
 // keys per thread: the chunk (int32 60 KiB, int64 52 KiB) + tables fit two workgroups per CU
 template <typename T> constexpr int SB_LKPT = sizeof(T) == 4 ? 15 : 13;
