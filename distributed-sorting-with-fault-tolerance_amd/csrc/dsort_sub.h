@@ -36,6 +36,9 @@ constexpr int SB_T = 256;              // threads of the per-chunk kernels
 constexpr int SB_MAXS = 1024;          // sub-buckets per bucket at most
 constexpr int SB_SLOTB = 10;           // slot table: 1024 key slots per bucket
 constexpr int SB_SLOTS = 1 << SB_SLOTB;
+#ifndef DSORT_SUB_TOTALS
+#define DSORT_SUB_TOTALS 1  // local path: sb_local_kernel adds up the sub-bucket totals (global atomics)
+#endif
 constexpr int SB_ST = 4;               // sub-tiles per chunk
 template <typename T> constexpr int SB_KPT = sizeof(T) == 4 ? 16 : 8;  // keys per thread per sub-tile
 template <typename T> constexpr int SB_SUB = SB_T * SB_KPT<T>;   // keys of a sub-tile
@@ -527,21 +530,39 @@ __device__ __forceinline__ uint2 tile_piece(const uint32_t *counts, int SS, uint
     return make_uint2(lo, nch == 1 ? lo + valid : base + pc[j1]);
 }
 
+#ifdef DSORT_STAMPS
+// Diagnostic build only: per-workgroup phase cycles of sb_local_kernel (or, with DSORT_SCAN_STAMPS,
+// of sb_scan_kernel<true> in rows 0..B-1), read back by dsort_debug_sbstamps().
+__device__ unsigned long long g_sbstamps[(1u << 18) * 8];
+#endif
 template <bool LOCAL>
-__global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restrict__ bi, int SS,
+__global__ void __launch_bounds__(SB_MAXS, 8) sb_scan_kernel(const BInfo *__restrict__ bi, int SS,
                                                           const uint32_t *__restrict__ counts,
                                                           uint32_t *__restrict__ offs, int tile, int align,
                                                           uint32_t mis, uint32_t cpad, void *__restrict__ tiles,
                                                           uint32_t *__restrict__ ntiles, Ovf *__restrict__ ovf,
                                                           uint32_t *__restrict__ novf, uint32_t trec,
                                                           const Chunk *__restrict__ ch, uint2 *__restrict__ pieces,
-                                                          uint32_t PS, uint32_t tcap) {
+                                                          uint32_t PS, uint32_t tcap, const uint32_t *__restrict__ stot) {
     __shared__ uint32_t wsum[SB_MAXS / 64];
     __shared__ uint32_t ss[SB_MAXS + 1];   // sub-bucket starts (positions)
     __shared__ uint16_t nxt[SB_MAXS];      // first sub-bucket after the tile starting at i
     __shared__ uint16_t chain[SB_MAXS];    // sub-buckets that start a tile
     __shared__ uint16_t tix[SB_MAXS];      // LOCAL: tile of chain entry i, relative to tbase (0xFFFF: none)
     __shared__ uint32_t nchain, tbase;
+#ifdef DSORT_SCAN_STAMPS
+    uint64_t sc_acc[8] = {}, sc_t0 = __builtin_amdgcn_s_memtime();
+#define SCST(k)                                            \
+    do {                                                   \
+        const uint64_t t1_ = __builtin_amdgcn_s_memtime(); \
+        sc_acc[k] += t1_ - sc_t0;                          \
+        sc_t0 = t1_;                                       \
+    } while (0)
+#else
+#define SCST(k) \
+    do {        \
+    } while (0)
+#endif
     const BInfo b = bi[blockIdx.x];
     const int j = threadIdx.x;
     const int ns = (int)b.nsub;
@@ -557,12 +578,17 @@ __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restric
         }
     };
     uint32_t tot = 0;
-    if constexpr (LOCAL) {
+    if (LOCAL && stot) {  // (the totals sb_local_kernel added up)
+        if (j < ns) tot = stot[(uint64_t)blockIdx.x * SS + j];
+    } else if constexpr (LOCAL) {
         // sub-bucket j's total = A_j - A_{j-1}, A_j = the sum over the chunks of pref[c][j + 1]
         // (pref[c][0] = 0): one load per chunk instead of two
         uint32_t a = 0;
         if (j < ns) {
-#pragma unroll 8  // (independent loads in flight: the loop is latency-bound)
+#ifndef DSORT_SCAN_SUM_U
+#define DSORT_SCAN_SUM_U 16
+#endif
+#pragma unroll DSORT_SCAN_SUM_U  // (independent loads in flight: the loop is latency-bound)
             for (uint32_t c = b.c0; c < b.c1; ++c) a += counts[(uint64_t)c * (SS + 1) + j + 1];
             ss[j + 1] = a;
         }
@@ -574,6 +600,7 @@ __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restric
     }
     uint32_t all;
     const uint32_t ex = scan_excl_1024(tot, wsum, all);
+    SCST(0);
     const uint32_t st = (uint32_t)b.start + ex;
     if (j < ns) {
         if constexpr (!LOCAL) {
@@ -587,6 +614,7 @@ __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restric
     }
     if (j == 0) ss[ns] = (uint32_t)b.start + b.len;
     __syncthreads();
+    SCST(1);
     if (j < ns) {
         const uint32_t p = ss[j];
         const uint32_t room = (uint32_t)tile - ((p + mis) & (uint32_t)(align - 1));
@@ -605,12 +633,44 @@ __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restric
         nxt[j] = (uint16_t)(e > j ? e : j + 1);  // e == j: sub-bucket j alone is too large
     }
     __syncthreads();
-    if (j == 0) {
+    SCST(2);
+#ifndef DSORT_SCAN_CHAIN_WAVE
+#define DSORT_SCAN_CHAIN_WAVE 1
+#endif
+    if (DSORT_SCAN_CHAIN_WAVE && j < 64) {
+        // the chain 0, nxt[0], nxt[nxt[0]], ... walked by wave 0 through a 64-entry window of nxt
+        // held one entry per lane: a step is a lane read (readlane) instead of an LDS round trip
+        // (one thread walking ~130 steps through LDS was a quarter of the kernel).  i, base, k and
+        // the window's member mask m are wave-uniform.
+        const int lane = j;
+        int i = 0, base = 0;
+        uint32_t k = 0;
+        uint32_t v = lane < ns ? nxt[lane] : 0u;
+        uint64_t m = 0;
+        const auto flush = [&]() {
+            if ((m >> lane) & 1ull) chain[k + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)(base + lane);
+            k += (uint32_t)__popcll(m);
+        };
+        while (i < ns) {
+            if (i >= base + 64) {
+                flush();
+                base = i & ~63;
+                v = base + lane < ns ? nxt[base + lane] : 0u;
+                m = 0;
+            }
+            m |= 1ull << (i - base);
+            i = __builtin_amdgcn_readlane((int)v, i - base);
+        }
+        flush();
+        if (lane == 0) nchain = k;
+    }
+    if (!DSORT_SCAN_CHAIN_WAVE && j == 0) {
         int k = 0;
         for (int i = 0; i < ns; i = nxt[i]) chain[k++] = (uint16_t)i;
         nchain = (uint32_t)k;
     }
     __syncthreads();
+    SCST(3);
     const int nc = (int)nchain;
     uint32_t nt = 0, i0 = 0, i1 = 0, room = 0;
     bool over = false;
@@ -630,6 +690,7 @@ __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restric
     const uint32_t tex = scan_excl_1024(nt, wsum, tall);
     if (j == 0) tbase = tall ? atomicAdd(ntiles, tall) : 0;
     __syncthreads();
+    SCST(4);
     if (LOCAL && j < nc) tix[j] = nt && !over ? (uint16_t)tex : (uint16_t)0xFFFF;
     if (j < nc && nt) {
         const uint32_t p = ss[i0], len = ss[i1] - p;
@@ -667,7 +728,54 @@ __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restric
             }
         }
     }
-    if (LOCAL && pieces) {
+#ifndef DSORT_SCAN_PIECES
+#define DSORT_SCAN_PIECES 1
+#endif
+    if (LOCAL && pieces && DSORT_SCAN_PIECES) {
+        // The piece tables: entry (tile t, chunk c) = chunk c's start + pref[c][bnd[t]], + pref[c][bnd[t + 1]]
+        // with bnd = the chain, then ns.  A group of chunks' prefix values at the tile bounds goes to
+        // LDS first: the loads run along a chunk's prefix row and the table stores along a tile's
+        // chunks, both coalesced.  (A wave per tile walking its chunks, or the (tile, chunk) entries
+        // spread over the workgroup, loaded each chunk's row at two words per entry: a 64-byte line
+        // per lane and load, 9100 entries per 2^20-key bucket -- the texture unit's line rate, 36 %
+        // of the kernel, in both forms.)
+        constexpr uint32_t PVW = 8192, PVC = 256, U = 8;
+        __shared__ uint32_t pv[PVW];   // [chunk of the group][bound]
+        __shared__ uint32_t pbs[PVC];  // the group's chunk starts
+        const uint32_t nch = b.c1 - b.c0, nb = (uint32_t)nc + 1;
+        uint32_t cg = PVW / nb;
+        cg = cg < PVC ? cg : PVC;
+        for (uint32_t g0 = 0; g0 < nch; g0 += cg) {
+            const uint32_t gn = nch - g0 < cg ? nch - g0 : cg, items = gn * nb;
+            __syncthreads();  // (tix; the previous group's reads of pv)
+            for (uint32_t i0 = j; i0 < items; i0 += U * SB_MAXS) {
+                uint32_t v[U];
+#pragma unroll
+                for (uint32_t u = 0; u < U; ++u) {
+                    const uint32_t i = i0 + u * SB_MAXS;
+                    v[u] = 0;
+                    if (i < items) {
+                        const uint32_t c = i / nb, q = i - c * nb;
+                        const uint32_t bnd = q < (uint32_t)nc ? (uint32_t)chain[q] : (uint32_t)ns;
+                        v[u] = counts[(uint64_t)(b.c0 + g0 + c) * (SS + 1) + bnd];
+                    }
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < U; ++u)
+                    if (i0 + u * SB_MAXS < items) pv[i0 + u * SB_MAXS] = v[u];
+            }
+            for (uint32_t c = j; c < gn; c += SB_MAXS) pbs[c] = (uint32_t)ch[b.c0 + g0 + c].start;
+            __syncthreads();
+            for (uint32_t i = j; i < (uint32_t)nc * gn; i += SB_MAXS) {
+                const uint32_t t = i / gn, c = i - t * gn;
+                const uint32_t k = tbase + tix[t];
+                if (tix[t] == 0xFFFF || k >= tcap) continue;  // (the host sees ntiles > tcap and fails the sort)
+                const uint32_t bs = pbs[c];
+                pieces[(uint64_t)k * PS + g0 + c] = make_uint2(bs + pv[c * nb + t], bs + pv[c * nb + t + 1]);
+            }
+        }
+    }
+    if (LOCAL && pieces && !DSORT_SCAN_PIECES) {
         __syncthreads();
         // the piece tables: a wave per tile, a lane per chunk (no division per entry)
         const uint32_t nch = b.c1 - b.c0, lane = threadIdx.x & 63;
@@ -683,6 +791,12 @@ __global__ void __launch_bounds__(SB_MAXS) sb_scan_kernel(const BInfo *__restric
             }
         }
     }
+    SCST(6);
+#ifdef DSORT_SCAN_STAMPS
+    if (threadIdx.x == 0 && LOCAL && blockIdx.x < (1u << 18))
+        for (int k = 0; k < 8; ++k) g_sbstamps[blockIdx.x * 8 + k] = sc_acc[k];
+#endif
+#undef SCST
 }
 
 // The piece table of every gathered tile (LOCAL path): a wave per tile, a lane per chunk -- the
@@ -716,11 +830,6 @@ __device__ __forceinline__ uint32_t sb_chunk_order(uint32_t bid, uint32_t G) {
     return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
 }
 
-#ifdef DSORT_STAMPS
-// Diagnostic build only: per-workgroup phase cycles of sb_local_kernel, read back by
-// dsort_debug_sbstamps().
-__device__ unsigned long long g_sbstamps[(1u << 18) * 8];
-#endif
 // int32: 1024 threads of 15 keys, 8 waves per SIMD at two workgroups per CU: twice the waves of
 // round 2's 512 threads of 31 keys to hide the lookups' LDS round trips (2.33 -> 2.02 ms at 2^30).
 // (int64 at 1024 threads of 6 keys: round 4 C4 -0.24 ms, 2^30 uniform int64 +0.4 ms; round 5, with the
@@ -737,7 +846,8 @@ __global__ void __launch_bounds__(SB_LT<T>, SB_LT<T> / 128) sb_local_kernel(T *_
                                                          const Spl<T> *__restrict__ spl_g,
                                                          const uint32_t *__restrict__ rng_g,
                                                          const SlotFn<T> *__restrict__ sfn,
-                                                         uint32_t *__restrict__ pref, const uint32_t *__restrict__ hotp) {
+                                                         uint32_t *__restrict__ pref, const uint32_t *__restrict__ hotp,
+                                                         uint32_t *__restrict__ stot) {
     constexpr int LT = SB_LT<T>, KPT = SB_LKPT<T>, CHL = SB_LCH<T>, PER = SB_MAXS / LT;
     static_assert(SB_MAXS % LT == 0, "sub-buckets per thread");
     __shared__ Spl<T> spl[SB_MAXS + 1];
@@ -770,6 +880,7 @@ __global__ void __launch_bounds__(SB_LT<T>, SB_LT<T> / 128) sb_local_kernel(T *_
         if (tid == 0) {
             pc[0] = 0;
             pc[1] = c.len;
+            if (stot) atomicAdd(&stot[(uint64_t)c.b * SS], c.len);
         }
         return;
     }
@@ -876,6 +987,9 @@ __global__ void __launch_bounds__(SB_LT<T>, SB_LT<T> / 128) sb_local_kernel(T *_
         const int j = PER * tid + q;
         hist[j] = ex;
         if (j < ns) pc[j] = ex;
+        // the bucket's sub-bucket totals for sb_scan_kernel (summing every chunk's prefix row
+        // there read the whole table again: 190 MB at 2^30 int32, 60 % of that kernel)
+        if (stot && j < ns && h[q]) atomicAdd(&stot[(uint64_t)c.b * SS + j], h[q]);
         ex += h[q];
     }
     __syncthreads();

@@ -1836,6 +1836,10 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         SS = (int)ns > SS ? (int)ns : SS;
     }
     SS = (SS + 63) & ~63;
+    // local path, int32: the sub-bucket totals added up by sb_local_kernel's atomics (sb_scan 126 -> 91 us,
+    // sb_local +10 us at 2^30); int64 sums the prefix rows in sb_scan (C4: the atomics cost sb_local
+    // about as much as they saved, profiles/r5_ab_sub_scan.log)
+    constexpr bool SUB_TOTALS = DSORT_SUB_TOTALS && sizeof(T) == 4;
     // tiles, bound (sb_scan_kernel); the local path's split tiles: tcap
     const uint64_t tmax = std::max<uint64_t>(nsubs + ceil_div(n, TILE) + (uint64_t)B, local ? tcap : 0);
     size_t off = 0;
@@ -1848,7 +1852,8 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
                  o_tt = take(tmax * sizeof(GTile)),
                  o_ovf = take(nsubs * sizeof(Ovf)), o_num = take(8), o_stl = take(B * sizeof(bk::TileRef) + 16),
                  o_pcs = take(local ? tcap * PS * sizeof(uint2) : 0),
-                 o_fill = take(pm || fill_keys ? B * sizeof(FillSeg<T>) : 0);
+                 o_fill = take(pm || fill_keys ? B * sizeof(FillSeg<T>) : 0),
+                 o_tot = take(local && SUB_TOTALS ? (size_t)B * SS * 4 : 0);
     int rc = ensure(ctx, &ctx->sub, &ctx->sub_bytes, off, "sub-bucket partition");
     if (rc) return rc;
     char *a = static_cast<char *>(ctx->sub);
@@ -1865,6 +1870,7 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
     uint32_t *num = reinterpret_cast<uint32_t *>(a + o_num);  // tiles, merge records
     bk::TileRef *stl = reinterpret_cast<bk::TileRef *>(a + o_stl);  // sample tiles, then their count
     uint2 *pcs = reinterpret_cast<uint2 *>(a + o_pcs);                // local path: piece tables
+    uint32_t *stot = local && SUB_TOTALS ? reinterpret_cast<uint32_t *>(a + o_tot) : nullptr;  // sub-bucket totals
     // pinned staging: the two tables, the sample tiles + count, then the two counters read back
     const size_t h_ch = (B * sizeof(BInfo) + 15) & ~(size_t)15, h_stl = h_ch + nch * sizeof(Chunk);
     const size_t h_num = h_stl + B * sizeof(bk::TileRef) + 16;
@@ -1924,6 +1930,7 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
     if (nch) DSORT_HIP(ctx, hipMemcpyAsync(dch, h + h_ch, nch * sizeof(Chunk), hipMemcpyHostToDevice, ctx->side));
     DSORT_HIP(ctx, hipMemcpyAsync(stl, hst, B * sizeof(bk::TileRef) + 16, hipMemcpyHostToDevice, ctx->side));
     DSORT_HIP(ctx, hipMemsetAsync(num, 0, 8, ctx->side));
+    if (stot) DSORT_HIP(ctx, hipMemsetAsync(stot, 0, (size_t)B * SS * 4, ctx->side));
     if (nfill)
         DSORT_HIP(ctx, hipMemcpyAsync(a + o_fill, hf, nfill * sizeof(FillSeg<T>), hipMemcpyHostToDevice, ctx->side));
     DSORT_HIP(ctx, hipEventRecord(ctx->side_ev, ctx->side));
@@ -1976,15 +1983,18 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         if (nch) {
             if ((rc = stage_event(ctx, s, timed, 13))) return rc;
             hipLaunchKernelGGL(sb_local_kernel<T>, dim3((unsigned)nch), dim3(SB_LT<T>), 0, s, src, dch, dbi, SS, spl, rng,
-                               sfn, cnt, ctx->bk_hot);
+                               sfn, cnt, ctx->bk_hot, stot);
             DSORT_HIP(ctx, hipGetLastError());
             if ((rc = stage_event(ctx, s, timed, 14))) return rc;
         }
         // (the piece tables inside the scan with many buckets; with few, a kernel of their own)
-        const bool pieces_in_scan = B >= 256;
+#ifndef DSORT_PIECES_SCAN_MINB
+#define DSORT_PIECES_SCAN_MINB 256
+#endif
+        const bool pieces_in_scan = B >= DSORT_PIECES_SCAN_MINB;
         hipLaunchKernelGGL(sb_scan_kernel<true>, dim3((unsigned)B), dim3(SB_MAXS), 0, s, dbi, SS, cnt, nullptr, TILE, 1,
                            0u, (uint32_t)(2 * (ALIGN - 1)), tt, num, ovf, num + 1, (uint32_t)tmax,
-                           static_cast<const Chunk *>(dch), pieces_in_scan ? pcs : nullptr, PS, (uint32_t)tcap);
+                           static_cast<const Chunk *>(dch), pieces_in_scan ? pcs : nullptr, PS, (uint32_t)tcap, stot);
         DSORT_HIP(ctx, hipGetLastError());
         DSORT_HIP(ctx, hipMemcpyAsync(hn, num, 8, hipMemcpyDeviceToHost, s));
         DSORT_HIP(ctx, hipEventRecord(ctx->sub_ev, s));
@@ -2036,7 +2046,7 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         DSORT_HIP(ctx, hipGetLastError());
     }
     hipLaunchKernelGGL(sb_scan_kernel<false>, dim3((unsigned)B), dim3(SB_MAXS), 0, s, dbi, SS, cnt, offs, TILE,
-                       (int)ALIGN, mis, 0u, tt, num, ovf, num + 1, (uint32_t)tmax, nullptr, nullptr, 0u, 0u);
+                       (int)ALIGN, mis, 0u, tt, num, ovf, num + 1, (uint32_t)tmax, nullptr, nullptr, 0u, 0u, nullptr);
     DSORT_HIP(ctx, hipGetLastError());
     DSORT_HIP(ctx, hipMemcpyAsync(hn, num, 8, hipMemcpyDeviceToHost, s));
     DSORT_HIP(ctx, hipEventRecord(ctx->sub_ev, s));
