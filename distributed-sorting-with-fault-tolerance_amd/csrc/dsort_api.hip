@@ -1101,6 +1101,10 @@ int dsort_set_option(dsort_ctx *ctx, int option, int64_t v) {
             o.stage_timing = v;
             ctx->ev_ok = ctx->ev_created && v != 0;
             return DSORT_OK;
+        case DSORT_OPT_TEST_TILE_CAP:
+            if (v < 0) return set_err(ctx, DSORT_EINVAL, "DSORT_OPT_TEST_TILE_CAP: >= 0");
+            o.test_tile_cap = v;
+            return DSORT_OK;
         default:
             return set_err(ctx, DSORT_EINVAL, "unknown option " + std::to_string(option));
     }
@@ -1120,6 +1124,7 @@ int dsort_get_option(const dsort_ctx *ctx, int option, int64_t *v) {
         case DSORT_OPT_TEST_HOLD_EXCHANGE: *v = o.test_hold_exchange; return DSORT_OK;
         case DSORT_OPT_TEST_FAIL_EXCHANGE: *v = o.test_fail_exchange; return DSORT_OK;
         case DSORT_OPT_STAGE_TIMING: *v = o.stage_timing; return DSORT_OK;
+        case DSORT_OPT_TEST_TILE_CAP: *v = o.test_tile_cap; return DSORT_OK;
         case DSORT_OPT_SUB_KEYS: *v = o.sub_keys; return DSORT_OK;
         case DSORT_OPT_SUB_OVERSAMPLE: *v = o.sub_os; return DSORT_OK;
         case DSORT_OPT_SUB_GATHER: *v = o.sub_gather; return DSORT_OK;

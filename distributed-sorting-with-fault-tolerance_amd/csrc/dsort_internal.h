@@ -65,6 +65,7 @@ struct dsort_opts {
     int64_t comm_timeout_ms = 0;    // DSORT_OPT_COMM_TIMEOUT_MS
     int64_t test_hold_exchange = 0; // DSORT_OPT_TEST_HOLD_EXCHANGE
     int64_t test_fail_exchange = -1; // DSORT_OPT_TEST_FAIL_EXCHANGE
+    int64_t test_tile_cap = 0;      // DSORT_OPT_TEST_TILE_CAP
     int64_t sub_keys = -1;          // DSORT_OPT_SUB_KEYS: -1 = 3/16 of a tile, 0 = no second level
     int64_t sub_os = -1;            // DSORT_OPT_SUB_OVERSAMPLE: -1 = 8 (4 at sub-buckets <= TILE/8)
     int64_t sub_gather = 1;         // DSORT_OPT_SUB_GATHER

@@ -306,12 +306,14 @@ __global__ void __launch_bounds__(SB_MAXS) sb_splitter_kernel(const int64_t *__r
                                                               const BInfo *__restrict__ bi, const Chunk *__restrict__ ch,
                                                               int os, int SS,
                                                               Spl<T> *__restrict__ spl, uint32_t *__restrict__ rng,
-                                                              SlotFn<T> *__restrict__ sfn) {
+                                                              SlotFn<T> *__restrict__ sfn, uint32_t *__restrict__ stot) {
     using U = typename KeyU<T>::U;
     __shared__ uint32_t sslot[SB_MAXS];
     __shared__ T skey[SB_MAXS];
     const BInfo b = bi[blockIdx.x];
     const int tid = threadIdx.x;
+    if (stot)  // (the bucket's sub-bucket totals, which sb_local_kernel adds up)
+        for (int j = tid; j < SS; j += SB_MAXS) stot[(uint64_t)blockIdx.x * SS + j] = 0;
     const int nspl = (int)b.nsub - 1;
     T klo = 0;
     uint32_t sh = 0;

@@ -1130,7 +1130,8 @@ __device__ __forceinline__ bool load_tile(const T *in, uint64_t n, const uint4 *
 template <typename T, bool GATHER, int W>
 __global__ void __launch_bounds__(64 * W, WG<T>::OCC) bin_sort_kernel(const T *in, T *out, uint64_t n,
                                                                      const uint4 *tiles, const uint32_t *ntiles,
-                                                                     sb::Gather ga, uint32_t *fb, uint32_t *nfb) {
+                                                                     sb::Gather ga, uint32_t *fb, uint32_t *nfb,
+                                                                     uint32_t toff) {
     constexpr int TILE = TILE_W<W>;
     static_assert(128 + 3 * kMaxPieces<T> + 1 <= TILE * (int)sizeof(T) / 4, "the piece table fits in the tile");
     __shared__ __attribute__((aligned(16))) T s[TILE];
@@ -1151,7 +1152,7 @@ __global__ void __launch_bounds__(64 * W, WG<T>::OCC) bin_sort_kernel(const T *i
         // round-robin over the 8 XCDs).  Consecutive tiles of a bucket end and start inside the
         // same 128-byte lines of every chunk: run on one XCD at about the same time, such a line
         // comes from HBM once and from that XCD's L2 the second time.
-        j = xcd_block(blockIdx.x, gridDim.x);
+        j = toff + xcd_block(blockIdx.x, gridDim.x);  // (toff: tiles [toff, toff + grid) of a split launch)
         if (j >= *ntiles) return;
         uint2 pe[2];
         gather_pieces(ga, j, pe);
@@ -1194,7 +1195,7 @@ __global__ void __launch_bounds__(64 * W, WG<T>::OCC) bin_sort_kernel(const T *i
         hint = __ballot(hint) != 0;
         gather_tile<T, W>(ga, pe, gt, in, s32 + 128, s32 + 96, x, threadIdx.x);
     } else {
-        j = blockIdx.x;
+        j = toff + blockIdx.x;
         if (!load_tile<T, false, W>(in, n, tiles, ntiles, ga, j, nullptr, nullptr, x, base, valid)) return;
         if (valid == 0) return;
     }
@@ -1512,24 +1513,61 @@ static int tile_sort_event(dsort_ctx *ctx, hipStream_t s, bool timed, int which)
 // The tile sort of `grid` tiles (an upper bound when the count lives on the device): the bin
 // sort first, then the bitonic sort of the tiles it declined.  Events 7 / 8 around both.
 constexpr uint32_t kFallbackWgs = 512;  // two workgroups per CU
+// In parts: tile_sort_begin (the fallback list for up to `cap` tiles, the bin sort of tiles
+// [0, grid)), tile_sort_more (tiles [toff, toff + grid)), tile_sort_end (the bitonic kernel over the
+// declined tiles of `tiles_total`).  The local path launches the first part before the host knows
+// the tile count (tile_sort_early).
 template <typename T, bool GATHER, int W>
-static int tile_sort_w(dsort_ctx *ctx, const T *in, T *out, uint64_t n, const uint4 *tiles, const uint32_t *ntiles,
-                       const sb::Gather &ga, uint32_t grid, hipStream_t s) {
-    const dim3 blk(64 * W);
-    int rc = ensure(ctx, &ctx->tfb, &ctx->tfb_bytes, ((size_t)grid + 1) * 4, "tile fallback list");
+static int tile_sort_begin(dsort_ctx *ctx, const T *in, T *out, uint64_t n, const uint4 *tiles, const uint32_t *ntiles,
+                           const sb::Gather &ga, uint32_t grid, uint32_t cap, hipStream_t s) {
+    int rc = ensure(ctx, &ctx->tfb, &ctx->tfb_bytes, ((size_t)cap + 1) * 4, "tile fallback list");
     if (rc) return rc;
-    uint32_t *fb = static_cast<uint32_t *>(ctx->tfb), *nfb = fb + grid;
+    uint32_t *fb = static_cast<uint32_t *>(ctx->tfb), *nfb = fb + cap;
     DSORT_HIP(ctx, hipMemsetAsync(nfb, 0, 4, s));
-    hipLaunchKernelGGL((bin_sort_kernel<T, GATHER, W>), dim3(grid), blk, 0, s, in, out, n, tiles, ntiles, ga, fb, nfb);
+    if (grid)
+        hipLaunchKernelGGL((bin_sort_kernel<T, GATHER, W>), dim3(grid), dim3(64 * W), 0, s, in, out, n, tiles, ntiles, ga, fb,
+                           nfb, 0u);
     DSORT_HIP(ctx, hipGetLastError());
+    return DSORT_OK;
+}
+template <typename T, bool GATHER, int W>
+static int tile_sort_more(dsort_ctx *ctx, const T *in, T *out, uint64_t n, const uint4 *tiles, const uint32_t *ntiles,
+                          const sb::Gather &ga, uint32_t toff, uint32_t grid, uint32_t cap, hipStream_t s) {
+    uint32_t *fb = static_cast<uint32_t *>(ctx->tfb), *nfb = fb + cap;
+    if (grid)
+        hipLaunchKernelGGL((bin_sort_kernel<T, GATHER, W>), dim3(grid), dim3(64 * W), 0, s, in, out, n, tiles, ntiles, ga, fb,
+                           nfb, toff);
+    DSORT_HIP(ctx, hipGetLastError());
+    return DSORT_OK;
+}
+template <typename T, bool GATHER, int W>
+static int tile_sort_end(dsort_ctx *ctx, const T *in, T *out, uint64_t n, const uint4 *tiles, const uint32_t *ntiles,
+                         const sb::Gather &ga, uint32_t tiles_total, uint32_t cap, hipStream_t s) {
+    const uint32_t *fb = static_cast<const uint32_t *>(ctx->tfb), *nfb = fb + cap;
     // the declined tiles: a grid of at most one round of workgroups over the chip walks the
     // list, whose length stays on the device (round 2 read it back: the host waited for the
     // bin sort, and the GPU idled about 70 us per sort until the next work arrived)
-    const uint32_t fgrid = grid < kFallbackWgs ? grid : kFallbackWgs;
-    hipLaunchKernelGGL((block_sort_w_kernel<T, GATHER, W>), dim3(fgrid), blk, 0, s, in, out, n, tiles, ntiles, ga,
-                       static_cast<const uint32_t *>(fb), static_cast<const uint32_t *>(nfb));
+    const uint32_t fgrid = tiles_total < kFallbackWgs ? tiles_total : kFallbackWgs;
+    if (fgrid)
+        hipLaunchKernelGGL((block_sort_w_kernel<T, GATHER, W>), dim3(fgrid), dim3(64 * W), 0, s, in, out, n, tiles, ntiles,
+                           ga, fb, nfb);
     DSORT_HIP(ctx, hipGetLastError());
     return DSORT_OK;
+}
+template <typename T, bool GATHER, int W>
+static int tile_sort_w(dsort_ctx *ctx, const T *in, T *out, uint64_t n, const uint4 *tiles, const uint32_t *ntiles,
+                       const sb::Gather &ga, uint32_t grid, hipStream_t s) {
+    int rc = tile_sort_begin<T, GATHER, W>(ctx, in, out, n, tiles, ntiles, ga, grid, grid, s);
+    if (rc) return rc;
+    return tile_sort_end<T, GATHER, W>(ctx, in, out, n, tiles, ntiles, ga, grid, grid, s);
+}
+// f(std::integral_constant<int, W>) with the wave count W of a tile size (TILE_OF<T>, or int32's 16384)
+template <typename T, typename F>
+static int with_tile_waves(dsort_ctx *ctx, int tile, F &&f) {
+    if (tile == TILE_OF<T>) return f(std::integral_constant<int, WG<T>::WAVES>{});
+    if constexpr (sizeof(T) == 4)
+        if (tile == TILE_W<16>) return f(std::integral_constant<int, 16>{});
+    return set_err(ctx, DSORT_EINVAL, "tile sort: no kernel for this tile size");
 }
 // tile: the tile size in keys (TILE_OF<T>, or 16384 for int32's large buckets: sub_sort)
 template <typename T, bool GATHER>
@@ -1541,13 +1579,9 @@ static int tile_sort(dsort_ctx *ctx, const T *in, T *out, uint64_t n, const uint
     // back, and a tile of a bucket's 2048 samples costs the bin sort a quarter of what the bitonic
     // sort spends on the whole padded tile.)
     if (grid) {
-        rc = DSORT_EINVAL;
-        if (tile == TILE_OF<T>) {
-            rc = tile_sort_w<T, GATHER, WG<T>::WAVES>(ctx, in, out, n, tiles, ntiles, ga, grid, s);
-        } else if constexpr (sizeof(T) == 4) {
-            if (tile == TILE_W<16>) rc = tile_sort_w<T, GATHER, 16>(ctx, in, out, n, tiles, ntiles, ga, grid, s);
-        }
-        if (rc == DSORT_EINVAL) return set_err(ctx, DSORT_EINVAL, "tile sort: no kernel for this tile size");
+        rc = with_tile_waves<T>(ctx, tile, [&](auto w) {
+            return tile_sort_w<T, GATHER, decltype(w)::value>(ctx, in, out, n, tiles, ntiles, ga, grid, s);
+        });
         if (rc) return rc;
     }
     return tile_sort_event(ctx, s, timed, 1);
@@ -1836,6 +1870,7 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         SS = (int)ns > SS ? (int)ns : SS;
     }
     SS = (SS + 63) & ~63;
+    if (ctx->opt.test_tile_cap > 0) tcap = std::min<uint64_t>(tcap, (uint64_t)ctx->opt.test_tile_cap);
     // local path, int32: the sub-bucket totals added up by sb_local_kernel's atomics (sb_scan 126 -> 91 us,
     // sb_local +10 us at 2^30); int64 sums the prefix rows in sb_scan (C4: the atomics cost sb_local
     // about as much as they saved, profiles/r5_ab_sub_scan.log)
@@ -1930,7 +1965,6 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
     if (nch) DSORT_HIP(ctx, hipMemcpyAsync(dch, h + h_ch, nch * sizeof(Chunk), hipMemcpyHostToDevice, ctx->side));
     DSORT_HIP(ctx, hipMemcpyAsync(stl, hst, B * sizeof(bk::TileRef) + 16, hipMemcpyHostToDevice, ctx->side));
     DSORT_HIP(ctx, hipMemsetAsync(num, 0, 8, ctx->side));
-    if (stot) DSORT_HIP(ctx, hipMemsetAsync(stot, 0, (size_t)B * SS * 4, ctx->side));
     if (nfill)
         DSORT_HIP(ctx, hipMemcpyAsync(a + o_fill, hf, nfill * sizeof(FillSeg<T>), hipMemcpyHostToDevice, ctx->side));
     DSORT_HIP(ctx, hipEventRecord(ctx->side_ev, ctx->side));
@@ -1973,8 +2007,10 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         rc = tile_sort<int64_t, false>(ctx, cmp, cmp, nsmp, stl4, pnst, sb::Gather{}, nst, s, false);
         if (rc) return rc;
         hipLaunchKernelGGL(sb_splitter_kernel<T>, dim3((unsigned)B), dim3(SB_MAXS), 0, s, cmp, smp, dbi, dch, os, SS, spl,
-                           rng, sfn);
+                           rng, sfn, stot);
         DSORT_HIP(ctx, hipGetLastError());
+    } else if (stot) {
+        DSORT_HIP(ctx, hipMemsetAsync(stot, 0, (size_t)B * SS * 4, s));
     }
     const uint32_t mis = (uint32_t)((reinterpret_cast<uintptr_t>(d_keys) / sizeof(T)) & (ALIGN - 1));
     uint32_t *hn = reinterpret_cast<uint32_t *>(h + h_num);
@@ -1996,8 +2032,31 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
                            0u, (uint32_t)(2 * (ALIGN - 1)), tt, num, ovf, num + 1, (uint32_t)tmax,
                            static_cast<const Chunk *>(dch), pieces_in_scan ? pcs : nullptr, PS, (uint32_t)tcap, stot);
         DSORT_HIP(ctx, hipGetLastError());
+        const Gather ga{static_cast<const GTile *>(tt), dch, dbi, cnt, pcs, PS, SS, spl, bspl, B};
         DSORT_HIP(ctx, hipMemcpyAsync(hn, num, 8, hipMemcpyDeviceToHost, s));
         DSORT_HIP(ctx, hipEventRecord(ctx->sub_ev, s));
+        // The tile sort of the first `early` tiles goes out behind the count's read-back, before the
+        // host waits for it: every tile holds at most TILE keys, so there are at least (keys in
+        // tiles) / TILE of them.  The rest follow the count (at 2^30 int32 ~15 % of the tiles), and
+        // the wait -- the read-back, then the launch -- runs under the first part instead of idling
+        // the GPU (about 35 us per sort).  (With the piece tables made by the scan only: a kernel of
+        // their own needs the count for its grid.  Not under a stage-1 kill point, which must see
+        // the second level finished and nothing after it.)
+#ifndef DSORT_TILE_EARLY
+#define DSORT_TILE_EARLY 1
+#endif
+        const uint64_t ebound = (n - npure) / (uint64_t)TILE;
+        const uint32_t early = DSORT_TILE_EARLY && pieces_in_scan && ctx->opt.kill_after_pass != 1
+                                   ? (uint32_t)std::min<uint64_t>(ebound, tcap)
+                                   : 0u;
+        if (early) {
+            if ((rc = tile_sort_event(ctx, s, timed, 0))) return rc;
+            rc = with_tile_waves<T>(ctx, TILE, [&](auto w) {
+                return tile_sort_begin<T, true, decltype(w)::value>(ctx, src, d_keys, n, nullptr, num, ga, early,
+                                                                    (uint32_t)tcap, s);
+            });
+            if (rc) return rc;
+        }
         // (the tile count sizes the grid: a grid at its bound, 9x the tiles at 2^30 int32, cost
         // more in empty workgroups than this wait -- measured 10.6 vs 10.1 ms)
         if (int rc_ = sync_event(ctx, ctx->sub_ev, "tile count")) return rc_;
@@ -2006,6 +2065,10 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         // partitioned chunks -- its sample takes single keys, since a run of adjacent keys now lies
         // in one sub-bucket of this attempt.
         if (ntiles > tmax || ntiles > tcap) {
+            // (the early tile sort still reads the tables the scatter path's side-stream uploads
+            // overwrite: it finishes first -- its output is rewritten by that path)
+            if (early)
+                if (int rc_ = sync_stream(ctx, s, "early tile sort")) return rc_;
             ctx->stats.sub_scatter_fallback = 1;
             return sub_sort<T>(ctx, src, d_keys, n, hb, B, m, s, timed, false, pure, pure_done, bspl, true, pm);
         }
@@ -2019,8 +2082,16 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         fault_point(ctx, s, 1);  // second-level partition done
         ctx->stats.merge_passes = 0;
         // 3. tile sort: gathered from the chunks into d_keys
-        if (ntiles) {
-            const Gather ga{static_cast<const GTile *>(tt), dch, dbi, cnt, pcs, PS, SS, spl, bspl, B};
+        if (early) {  // (ntiles >= early)
+            rc = with_tile_waves<T>(ctx, TILE, [&](auto w) {
+                constexpr int W = decltype(w)::value;
+                int r = tile_sort_more<T, true, W>(ctx, src, d_keys, n, nullptr, num, ga, early,
+                                                   ntiles > early ? ntiles - early : 0u, (uint32_t)tcap, s);
+                return r ? r : tile_sort_end<T, true, W>(ctx, src, d_keys, n, nullptr, num, ga, ntiles, (uint32_t)tcap, s);
+            });
+            if (rc) return rc;
+            if ((rc = tile_sort_event(ctx, s, timed, 1))) return rc;
+        } else if (ntiles) {
             rc = tile_sort<T, true>(ctx, src, d_keys, n, nullptr, num, ga, ntiles, s, timed, TILE);
             if (rc) return rc;
         }

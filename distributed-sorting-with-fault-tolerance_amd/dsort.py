@@ -50,7 +50,7 @@ OPTIONS = {"buckets": 1, "bucket_keys": 2, "bucket_oversample": 3,
            "max_fanin_log2": 5, "kill_after_stage": 6, "kill_in_exchange": 7,
            "comm_timeout_ms": 8,
            "sub_keys": 9, "sub_oversample": 10, "sub_gather": 11, "test_hold_exchange": 12,
-           "test_fail_exchange": 13, "stage_timing": 14}
+           "test_fail_exchange": 13, "stage_timing": 14, "test_tile_cap": 15}
 # ABI 2's option name, a deprecated alias of "kill_after_stage" until ABI 6 (dsort.h)
 DEPRECATED_OPTIONS = {"kill_after_pass": "kill_after_stage"}
 

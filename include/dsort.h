@@ -154,6 +154,10 @@ int dsort_synchronize(dsort_ctx *ctx);
                                          dsort_get_stats (default); 0 = none (the *_ms statistics read
                                          0).  Each event sits between two kernels of the sort: about
                                          6 us of idle GPU apiece, ~1 % of a 2^30-key sort */
+#define DSORT_OPT_TEST_TILE_CAP 15     /* test only (ABI 5): t > 0 = the local second level's tile
+                                         tables hold at most t tiles, so a sort needing more takes
+                                         the scatter path (stats.sub_scatter_fallback), as a
+                                         pathological sampling would.  0 = off (default)            */
 int dsort_set_option(dsort_ctx *ctx, int option, int64_t value);
 int dsort_get_option(const dsort_ctx *ctx, int option, int64_t *value);
 

@@ -399,3 +399,36 @@ def test_int32_one_key_slots(gpu_ctx, order, mode, B):
     opts = {"local": dict(), "scatter": dict(sub_gather=0)}[mode]
     with gpu_ctx.options(buckets=B, **opts):
         assert np.array_equal(_sort(gpu_ctx, a, False), np.sort(a))
+
+
+@pytest.mark.parametrize("dtype", ["i32", "i64"])
+@pytest.mark.parametrize("kind", ["uniform", "sorted"])
+def test_tile_table_overflow_after_early_tile_sort(gpu_ctx, dtype, kind):
+    """The local path launches the tile sort of its first (keys / TILE) tiles before the host reads
+    the tile count back (sub_sort, tile_sort_early).  DSORT_OPT_TEST_TILE_CAP shrinks the tile
+    tables below the tiles the packing makes but above that early part, so the sort finds the
+    overflow with the early tile sort in flight and takes the scatter path over the same arena:
+    the output is still exact, and the fallback is reported."""
+    import torch
+    B = 256  # (the piece tables inside the scan, the early launch's condition)
+    tile = TILE  # (8192 keys for both widths)
+    n = B * 5 * tile + 333
+    rng = np.random.default_rng(91 + len(kind))
+    a = _keys(rng, kind, n) if dtype == "i32" else _keys64(rng, "uniform", n)
+    if dtype == "i64" and kind == "sorted":
+        a = np.sort(a)
+    t = torch.from_numpy(a).cuda()
+    out = torch.empty_like(t)
+    early = n // tile
+    with gpu_ctx.options(buckets=B, test_tile_cap=early + 8):
+        gpu_ctx.sort_dev(t, out)
+        torch.cuda.synchronize()
+        st = gpu_ctx.stats()
+    assert np.array_equal(out.cpu().numpy(), np.sort(a))
+    assert st["sub_scatter_fallback"] == 1
+    with gpu_ctx.options(buckets=B):
+        gpu_ctx.sort_dev(t, out)
+        torch.cuda.synchronize()
+        st = gpu_ctx.stats()
+    assert np.array_equal(out.cpu().numpy(), np.sort(a))
+    assert st["sub_scatter_fallback"] == 0
