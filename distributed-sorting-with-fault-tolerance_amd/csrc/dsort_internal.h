@@ -123,7 +123,7 @@ struct dsort_ctx {
     bool done_pending = false;
     void *tfb = nullptr;          // tiles the bin sort declined (+ their count, on the device)
     size_t tfb_bytes = 0;
-    void *text_status = nullptr;  // per-tile look-back status words of the text codec
+    void *text_status = nullptr;  // per-tile counts and their prefixes of the text codec
     size_t text_status_bytes = 0;
     void *red = nullptr;       // 64 B of reduction accumulators
     uint64_t *red_host = nullptr;  // pinned mirror
