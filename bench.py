@@ -448,13 +448,14 @@ def _pmc_doc(w, dist="uniform"):
 
 
 def pmc_traffic(kernel, n, w, dist="uniform"):
-    """HBM bytes per launch of `kernel` from the newest PMC table, scaled to this run's key count;
+    """HBM bytes per sort of `kernel` (all its launches) from the newest PMC table, scaled to this run's key count;
     None when absent, measured on another key width, or on another build / distribution."""
     doc = _pmc_doc(w, dist)
     if not doc or not doc["match"] or kernel not in doc["kernels"]:
         return None
     rec = doc["kernels"][kernel]
-    return round(rec["traffic_bytes_per_launch"] * n / doc.get("keys", 1 << 30))
+    # (per sort when the table has it: the stage times span all of a kernel's launches in a sort)
+    return round(rec.get("traffic_bytes_per_sort", rec["traffic_bytes_per_launch"]) * n / doc.get("keys", 1 << 30))
 
 
 def pmc_sort_bytes(n, w, dist="uniform"):
@@ -463,7 +464,8 @@ def pmc_sort_bytes(n, w, dist="uniform"):
     doc = _pmc_doc(w, dist)
     if not doc:
         return None, None, False
-    tot = sum(r["traffic_bytes_per_launch"] for k, r in doc["kernels"].items() if not k.startswith(NOT_SORT))
+    tot = sum(r.get("traffic_bytes_per_sort", r["traffic_bytes_per_launch"]) for k, r in doc["kernels"].items()
+              if not k.startswith(NOT_SORT))
     return round(tot * n / doc.get("keys", 1 << 30)), doc["file"], doc["match"]
 
 

@@ -83,3 +83,18 @@ def test_stage_roofline_counts_only_the_scatters_written_keys():
     assert multi["bucket_scatter_lines_kernel"]["algorithmic_bytes_per_launch"] == 2 * w * n
     assert one["bucket_hist_kernel"]["algorithmic_bytes_per_launch"] == w * n
     assert one["bin_sort_kernel"]["algorithmic_bytes_per_launch"] == 2 * w * tk
+
+
+def test_pmc_sort_bytes_count_every_launch_of_a_kernel():
+    """The PMC table's per-sort traffic counts every launch of a kernel in one sort (round 5: the
+    tile sort runs in two launches, the first before the host reads the tile count), and the bench
+    line's whole-sort bytes and per-stage traffic use it."""
+    import bench
+    doc = bench._pmc_doc(4, "uniform")
+    assert doc is not None
+    bs = doc["kernels"]["bin_sort_kernel<int, true, 8>"]
+    assert bs["launches_per_sort"] == 2
+    assert bs["traffic_bytes_per_sort"] == int(bs["traffic_bytes_per_launch"] * 2)
+    pb, _, _ = bench.pmc_sort_bytes(1 << 30, 4, "uniform")
+    exp = sum(r["traffic_bytes_per_sort"] for k, r in doc["kernels"].items() if not k.startswith(bench.NOT_SORT))
+    assert pb == exp and pb > 3 * 2 * 4 * (1 << 30)  # about 3.7x one read + one write of the keys
