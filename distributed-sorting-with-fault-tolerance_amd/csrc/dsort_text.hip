@@ -90,15 +90,20 @@ __device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t *wsum) {
     return agg;
 }
 
-// Per-tile totals -> exclusive prefixes (one workgroup of 1024 threads, 16 tiles per thread and
-// round, loaded as four 16-byte vectors); *total = their sum.
-constexpr int SCAN_T = 1024, SCAN_Q = 16;
+// Per-tile totals -> exclusive prefixes (one workgroup of 1024 threads); *total = their sum.  A round
+// takes SCAN_Q consecutive tiles per thread (16-byte loads), scans the thread sums, and stages the
+// tiles' offsets from the round's start in LDS, so that the 8-byte prefixes go out coalesced.
+// (Written straight from each thread's registers, every store instruction touched 64 lines: 105 us
+// for the 180 000 tiles of 2^28 keys' text.)
+constexpr int SCAN_T = 1024, SCAN_Q = 32, SCAN_ROUND = SCAN_T * SCAN_Q;
 __global__ void __launch_bounds__(SCAN_T) tile_scan_kernel(const uint32_t *__restrict__ cnt, uint64_t *__restrict__ pref,
                                                            uint32_t ntiles, uint64_t *__restrict__ total) {
     __shared__ uint64_t wsum[SCAN_T / 64];
+    __shared__ uint32_t rel[SCAN_ROUND + SCAN_ROUND / SCAN_Q];  // (one pad word per thread's run)
     const int lane = lane_id(), w = threadIdx.x >> 6;
+    const auto slot = [](uint32_t j) { return j + j / SCAN_Q; };
     uint64_t carry = 0;
-    for (uint32_t b0 = 0; b0 < ntiles; b0 += SCAN_T * SCAN_Q) {
+    for (uint32_t b0 = 0; b0 < ntiles; b0 += SCAN_ROUND) {
         const uint32_t i0 = b0 + SCAN_Q * threadIdx.x;
         uint32_t v[SCAN_Q];
         if (i0 + SCAN_Q <= ntiles) {
@@ -111,29 +116,28 @@ __global__ void __launch_bounds__(SCAN_T) tile_scan_kernel(const uint32_t *__res
 #pragma unroll
             for (int q = 0; q < SCAN_Q; ++q) v[q] = i0 + q < ntiles ? cnt[i0 + q] : 0u;
         }
-        uint64_t sum = 0;
+        uint32_t sum = 0;  // (a round's tiles hold < 2^32 bytes or tokens: 32768 tiles of <= 24 KiB)
 #pragma unroll
         for (int q = 0; q < SCAN_Q; ++q) sum += v[q];
-        uint64_t incl = sum;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint64_t y = __shfl_up(incl, o);
-            if (lane >= o) incl += y;
-        }
+        uint32_t incl = wave_incl_sum(sum);
         if (lane == 63) wsum[w] = incl;
         __syncthreads();
-        uint64_t ex = carry + incl - sum, all = 0;
+        uint32_t ex = incl - sum, all = 0;
 #pragma unroll
         for (int i = 0; i < SCAN_T / 64; ++i) {
-            ex += i < w ? wsum[i] : 0;
-            all += wsum[i];
+            ex += i < w ? (uint32_t)wsum[i] : 0u;
+            all += (uint32_t)wsum[i];
         }
 #pragma unroll
         for (int q = 0; q < SCAN_Q; ++q) {
-            if (i0 + q < ntiles) pref[i0 + q] = ex;
+            rel[slot(SCAN_Q * threadIdx.x + q)] = ex;
             ex += v[q];
         }
+        __syncthreads();
+        const uint32_t nr = ntiles - b0 < (uint32_t)SCAN_ROUND ? ntiles - b0 : (uint32_t)SCAN_ROUND;
+        for (uint32_t j = threadIdx.x; j < nr; j += SCAN_T) pref[b0 + j] = carry + rel[slot(j)];
         carry += all;
-        __syncthreads();  // (wsum is rewritten by the next round)
+        __syncthreads();  // (wsum and rel are rewritten by the next round)
     }
     if (threadIdx.x == 0) *total = carry;
 }
@@ -307,6 +311,43 @@ __global__ void __launch_bounds__(NT) parse_count_kernel(const char *__restrict_
     if (threadIdx.x == 0) cnt[blockIdx.x] = agg;
 }
 
+// The key of the token starting at LDS byte pos.  Fast path: the 16 staged bytes from the token's
+// dword (pos + 15 < PLDS for every start of the tile); a sign, then L < 12 digits and a whitespace
+// byte.  (Round 1 read every digit from LDS in a dependent chain of byte loads: 2.86 ms at 2^28
+// keys, 0.18 of HBM.)  Longer tokens (leading zeros) and malformed ones take the byte loop.
+__device__ __forceinline__ uint32_t parse_token(const uint32_t *lw, const unsigned char *lb, int pos, const char *ga,
+                                                const char *text, uint64_t len, uint64_t tb,
+                                                unsigned long long *err_pos) {
+    const int a = pos >> 2;
+    const uint64_t lo64 = (uint64_t)lw[a + 1] << 32 | lw[a], hi64 = (uint64_t)lw[a + 3] << 32 | lw[a + 2];
+    const uint32_t c0 = (uint32_t)(lo64 >> (8 * (pos & 3))) & 255u;
+    const bool neg = c0 == '-', sg = neg || c0 == '+';
+    const uint32_t s8 = 8u * (uint32_t)((pos & 3) + (sg ? 1 : 0));  // 0..32
+    const uint64_t r0 = s8 ? (lo64 >> s8) | (hi64 << (64u - s8)) : lo64, r1 = hi64 >> s8;
+    const uint32_t e[3] = {(uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)r1};  // bytes after the sign
+    const uint32_t m12 = pack4(dig_bits4(e[0])) | pack4(dig_bits4(e[1])) << 4 | pack4(dig_bits4(e[2])) << 8;
+    const int L = __ffs(~m12) - 1;  // leading digits, 0..12
+    const uint32_t tw = L < 4 ? e[0] : (L < 8 ? e[1] : e[2]);
+    const uint32_t term = (tw >> (8 * (L & 3))) & 255u;
+    if (L > 0 && L < 12 && is_ws(term)) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            const uint32_t d = ((e[k >> 2] >> (8 * (k & 3))) & 255u) - '0';
+            v = k < L ? v * 10u + d : v;
+        }
+        uint64_t V = v;
+#pragma unroll
+        for (int k = 9; k < 11; ++k) {
+            const uint32_t d = ((e[k >> 2] >> (8 * (k & 3))) & 255u) - '0';
+            V = k < L ? V * 10u + d : V;
+        }
+        // the oracle's saturation at 2^32 (then the int32 wrap): a value >= 2^32 is key 0
+        return V >= (1ull << 32) ? 0u : (neg ? 0u - (uint32_t)V : (uint32_t)V);
+    }
+    return parse_slow(lb, pos, ga, text, len, tb + pos - 16, err_pos);
+}
+
 __global__ void __launch_bounds__(NT) parse_kernel(const char *__restrict__ text, uint64_t len,
                                                    int32_t *__restrict__ keys, uint64_t cap,
                                                    const uint64_t *__restrict__ pref, unsigned long long *err_pos) {
@@ -356,44 +397,12 @@ __global__ void __launch_bounds__(NT) parse_kernel(const char *__restrict__ text
     while (starts) {
         const int i = __ffsll((long long)starts) - 1;
         starts &= starts - 1;
-        const int pos = my0 + i;
-        // Fast path: the 16 staged bytes from the token's dword (pos + 15 < PLDS for every start
-        // of the tile); a sign, then L < 12 digits and a whitespace byte.  (Round 1 read every
-        // digit from LDS in a dependent chain of byte loads: 2.86 ms at 2^28 keys, 0.18 of HBM.)
-        const int a = pos >> 2;
-        const uint64_t lo64 = (uint64_t)lw[a + 1] << 32 | lw[a], hi64 = (uint64_t)lw[a + 3] << 32 | lw[a + 2];
-        const uint32_t c0 = (uint32_t)(lo64 >> (8 * (pos & 3))) & 255u;
-        const bool neg = c0 == '-', sg = neg || c0 == '+';
-        const uint32_t s8 = 8u * (uint32_t)((pos & 3) + (sg ? 1 : 0));  // 0..32
-        const uint64_t r0 = s8 ? (lo64 >> s8) | (hi64 << (64u - s8)) : lo64, r1 = hi64 >> s8;
-        const uint32_t e[3] = {(uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)r1};  // bytes after the sign
-        const uint32_t m12 = pack4(dig_bits4(e[0])) | pack4(dig_bits4(e[1])) << 4 | pack4(dig_bits4(e[2])) << 8;
-        const int L = __ffs(~m12) - 1;  // leading digits, 0..12
-        const uint32_t tw = L < 4 ? e[0] : (L < 8 ? e[1] : e[2]);
-        const uint32_t term = (tw >> (8 * (L & 3))) & 255u;
-        uint32_t key;
-        if (L > 0 && L < 12 && is_ws(term)) {
-            uint32_t v = 0;
-#pragma unroll
-            for (int k = 0; k < 9; ++k) {
-                const uint32_t d = ((e[k >> 2] >> (8 * (k & 3))) & 255u) - '0';
-                v = k < L ? v * 10u + d : v;
-            }
-            uint64_t V = v;
-#pragma unroll
-            for (int k = 9; k < 11; ++k) {
-                const uint32_t d = ((e[k >> 2] >> (8 * (k & 3))) & 255u) - '0';
-                V = k < L ? V * 10u + d : V;
-            }
-            // the oracle's saturation at 2^32 (then the int32 wrap): a value >= 2^32 is key 0
-            key = V >= (1ull << 32) ? 0u : (neg ? 0u - (uint32_t)V : (uint32_t)V);
-        } else {
-            // long tokens (12 or more digits: leading zeros), and the error cases
-            key = parse_slow(lb, pos, ga, text, len, tb + pos - 16, err_pos);
-        }
+        const uint32_t key = parse_token(lw, lb, my0 + i, ga, text, len, tb, err_pos);
         if (idx < cap) keys[idx] = (int32_t)key;
         ++idx;
     }
+    // (Measured and not kept: the tile's token starts listed in LDS and taken round-robin by the
+    // threads -- balanced lanes, coalesced key stores -- 1.77-1.84 against 1.77 ms.)
 #ifdef DSORT_STAMPS
     TXST(3);
     if (threadIdx.x == 0 && tile < (1u << 18))
