@@ -397,13 +397,14 @@ def cpu_baseline(sample_keys, target_keys):
 # (the second level and the tile sort only the keys outside single-key buckets).
 STAGE_KERNELS = {
     # (round 5: the first level's kernels carry the adaptive-map flag; uniform int32 keys take the
-    # fixed map, int64 has one map kind)
+    # fixed map, int64 has one map kind; the scatter's last flag is the sorted-runs instance, which
+    # uniform and Zipf keys do not take)
     4: [("bucket_hist_kernel<int, false>", "bucket_hist_ms", 1, "n"),
-        ("bucket_scatter_lines_kernel<int, false, false>", "bucket_scatter_ms", 2, "n"),
+        ("bucket_scatter_lines_kernel<int, false, false, false>", "bucket_scatter_ms", 2, "n"),
         ("sb_local_kernel<int>", "sub_partition_ms", 2, "tile_sort_keys"),
         ("bin_sort_kernel<int, true, 8>", "tile_sort_kernel_ms", 2, "tile_sort_keys")],
     8: [("bucket_hist_kernel<long, false>", "bucket_hist_ms", 1, "n"),
-        ("bucket_scatter_lines_kernel<long, {ids}, false>", "bucket_scatter_ms", 2, "n"),
+        ("bucket_scatter_lines_kernel<long, {ids}, false, false>", "bucket_scatter_ms", 2, "n"),
         ("sb_local_kernel<long>", "sub_partition_ms", 2, "tile_sort_keys"),
         ("bin_sort_kernel<long, true, 8>", "tile_sort_kernel_ms", 2, "tile_sort_keys")],
 }

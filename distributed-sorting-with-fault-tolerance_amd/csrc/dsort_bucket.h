@@ -834,7 +834,9 @@ __device__ unsigned long long g_bkstamps[8192 * 16];
 // IDS: the variant that reads the histogram's buckets (BkIds).  The host launches both variants for
 // int64 (it does not know the map's choice); the one that does not match m.ids returns at once
 // (one kernel with a run-time branch: uniform int64 scatter 5.29 -> 5.84 ms).
-template <typename T, bool IDS, bool AD = false>
+// HT: the instance for input with runs of one bucket (BkMap.hot: sorted, reversed), which enters a
+// long line stream in the line map with the owner's whole wave.
+template <typename T, bool IDS, bool AD = false, bool HT = false>
 __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__restrict__ in, uint64_t n,
                                                                     const typename Comp<T>::C *__restrict__ spl_g,
                                                                     const BkMap *__restrict__ map, int B, int BP, int subs,
@@ -1040,7 +1042,21 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
             st[tb] = make_uint2(lks | p0 << 16, vc | ph << 5 | pure << 10 | L << 11);
             sgb[tb] = gb;
             hist[tb] = lks;  // the placement's LDS starts (a dense array: fewer bank conflicts)
-            for (uint32_t i = 0; i < nl; ++i) lmap[p0 + i] = (uint16_t)tb;
+            if (!HT || nl <= 8)
+                for (uint32_t i = 0; i < nl; ++i) lmap[p0 + i] = (uint16_t)tb;
+        }
+        if constexpr (HT) {
+            // sorted or reversed input puts a sub-tile's keys in one or two buckets, up to SUB / LK
+            // lines of one stream: its owner's whole wave enters them in the line map (the owner
+            // thread alone: 2^30 sorted int32 scatter 3.3 ms; in every instance, the code cost the
+            // uniform scatter 0.22 ms -- profiles/r5_ab_lmap_wave.log)
+            uint64_t big = __ballot(nl > 8);
+            while (big) {
+                const int l = __ffsll((long long)big) - 1;
+                big &= big - 1;
+                const uint32_t bp0 = __shfl(p0, l), bnl = __shfl(nl, l);
+                for (uint32_t i = (uint32_t)lane; i < bnl; i += 64) lmap[bp0 + i] = (uint16_t)(64 * w + l);
+            }
         }
         __syncthreads();  // C
         BKST(2);

@@ -2314,9 +2314,14 @@ static int first_level(dsort_ctx *ctx, const T *d_in, uint64_t n, uint64_t ioff,
                 hipLaunchKernelGGL((bucket_scatter_lines_kernel<T, false, true>), dim3((unsigned)L.G), dim3(BK_T), 0, s,
                                    d_in, n, L.spl, L.map, B, BP, L.subs, L.offs, part_out, direct, ioff, L.ids);
         }
-        if (!ad && !(RB && ids))
-            hipLaunchKernelGGL((bucket_scatter_lines_kernel<T, false, false>), dim3((unsigned)L.G), dim3(BK_T), 0, s, d_in,
-                               n, L.spl, L.map, B, BP, L.subs, L.offs, part_out, direct, ioff, L.ids);
+        if (!ad && !(RB && ids)) {
+            if (!Comp<T>::ADAPT && RB && hm->hot)  // (int32 read the map back: runs of one bucket)
+                hipLaunchKernelGGL((bucket_scatter_lines_kernel<T, false, false, true>), dim3((unsigned)L.G), dim3(BK_T), 0,
+                                   s, d_in, n, L.spl, L.map, B, BP, L.subs, L.offs, part_out, direct, ioff, L.ids);
+            else
+                hipLaunchKernelGGL((bucket_scatter_lines_kernel<T, false, false>), dim3((unsigned)L.G), dim3(BK_T), 0, s,
+                                   d_in, n, L.spl, L.map, B, BP, L.subs, L.offs, part_out, direct, ioff, L.ids);
+        }
     }
     if constexpr (BkIds<T>::ON)  // (without the read-back: the variant the slot map did not choose returns at once)
         if (!RB || ids)
