@@ -77,6 +77,12 @@ def parse(argv=None):
     ap.add_argument("--reassign", choices=["first-live", "next-live"], default="first-live")
     ap.add_argument("--codec", action="store_true",
                     help="time the GPU text codec (output.txt format + %%d parse) on --keys sorted keys")
+    ap.add_argument("--legs", default="all",
+                    help="sample-sort runs only (N > 1, or --path samplesort): extra legs after the metric's "
+                         "timed region, comma-separated from c3,c4,c5 ('all', default; 'none' to skip)")
+    ap.add_argument("--no-legs", dest="legs", action="store_const", const="none")
+    ap.add_argument("--leg-timeout", type=float, default=180.0,
+                    help="exchange deadline of a sort leg in seconds (the C5 leg gets 4x)")
     ap.add_argument("--launcher-selftest", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
@@ -557,40 +563,63 @@ def run_single(args):
     return t1 - t0, k
 
 
-def run_multi(args, rank, world):
-    """One rank per GPU: gloo for control, RCCL (inside libdsort) for the key exchange.  Strong
-    scaling: the --keys total is split into equal contiguous chunks (server.c:185-216)."""
+def _sync_ok(dist, flag):
+    """Every rank's status after a phase of a measurement: the minimum over ranks (gloo), so every
+    rank leaves a failed phase together instead of pairing different collectives."""
     import torch
-    import torch.distributed as dist
+
+    t = torch.tensor([1 if flag else 0], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
+def measure_samplesort(ctx, dist, rank, world, n, dtype, distname, steps, warmup, strict=True):
+    """One sample-sort workload on the ranks' communicator: n keys in all, split into equal
+    contiguous chunks (server.c:185-216), `warmup` untimed sorts, verification (local order, global
+    multiset fingerprint, rank boundaries), `steps` timed sorts back to back between two barriers
+    (no stage events), then `steps` instrumented sorts for the per-stage device times.  Returns
+    (elapsed_max_over_ranks, verified, per_rank table (PR_* columns), key bytes, error).  strict:
+    a library error raises (the metric line); else every rank returns it (an extra leg)."""
+    import torch
 
     import dsort
 
-    local = int(os.environ.get("LOCAL_RANK", rank))
-    torch.cuda.set_device(local)
-    if world == 1 and "MASTER_PORT" not in os.environ:  # --path samplesort, one GPU, no launcher
-        os.environ.setdefault("DSORT_BENCH_STORE", os.path.join(tempfile.mkdtemp(prefix="dsort_bench_"), "store"))
-    init_group(dist, rank, world)
-    ctx = dsort.Context(local)
-    uid = [dsort.Context.unique_id() if rank == 0 else None]
-    dist.broadcast_object_list(uid, src=0)
-    ctx.comm_init(world, rank, uid[0])
-    n = args.keys
     sz = n // world + (1 if rank < n % world else 0)          # server.c:185-216 partition rule
     first = rank * (n // world) + min(rank, n % world)
-    t_in = make_input(ctx, sz, first, args.dtype, args.dist)
-    w = 4 if args.dtype == "i32" else 8
-    in_fp = ctx.fingerprint(t_in)
-    for _ in range(max(args.warmup, 1)):
-        ptr, nout = ctx.sample_sort_dev(t_in)
-    ctx.synchronize()
+    w = 4 if dtype == "i32" else 8
+    err = None
+
+    def guarded(fn):
+        nonlocal err
+        try:
+            fn()
+            return True
+        except dsort.DsortError as e:
+            if strict:
+                raise
+            err = f"rank {rank}: {e}"
+            return False
+
+    st_in = {}
+
+    def prepare():
+        st_in["t"] = make_input(ctx, sz, first, dtype, distname)
+        st_in["fp"] = ctx.fingerprint(st_in["t"])
+        for _ in range(max(warmup, 1)):
+            st_in["res"] = ctx.sample_sort_dev(st_in["t"])
+        ctx.synchronize()
+
+    if not _sync_ok(dist, guarded(prepare)):
+        return None, False, None, w, err or "a peer failed"
+    t_in, in_fp = st_in["t"], st_in["fp"]
+    ptr, nout = st_in["res"]
     # verification outside the timed region: local order, global multiset, rank boundaries
-    sfx = args.dtype
     c, fs, fx = dsort.U64(), dsort.U64(), dsort.U64()
-    ctx.check(getattr(ctx.lib, f"dsort_count_descents_{sfx}")(ctx.h, ptr, nout, ctypes.byref(c)))
-    ctx.check(getattr(ctx.lib, f"dsort_fingerprint_{sfx}")(ctx.h, ptr, nout, ctypes.byref(fs), ctypes.byref(fx)))
+    ctx.check(getattr(ctx.lib, f"dsort_count_descents_{dtype}")(ctx.h, ptr, nout, ctypes.byref(c)))
+    ctx.check(getattr(ctx.lib, f"dsort_fingerprint_{dtype}")(ctx.h, ptr, nout, ctypes.byref(fs), ctypes.byref(fx)))
     ends = np.zeros(2, np.int64)
     if nout:
-        hb = np.zeros(1, np.int64 if sfx == "i64" else np.int32)
+        hb = np.zeros(1, np.int64 if dtype == "i64" else np.int32)
         ctx.copy_d2h(hb, ptr, hb.itemsize)
         ends[0] = hb[0]
         ctx.copy_d2h(hb, ptr + (nout - 1) * hb.itemsize, hb.itemsize)
@@ -605,12 +634,18 @@ def run_multi(args, rank, world):
     torch.cuda.synchronize()
     dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        ptr, nout = ctx.sample_sort_dev(t_in)
-    torch.cuda.synchronize()
+
+    def timed_steps():
+        for _ in range(steps):
+            ctx.sample_sort_dev(t_in)
+        torch.cuda.synchronize()
+
+    ok_t = guarded(timed_steps)
     dist.barrier()
     t1 = time.perf_counter()
     ctx.set_option("stage_timing", 1)
+    if not _sync_ok(dist, ok_t):
+        return None, False, None, w, err or "a peer failed"
     el = torch.tensor([t1 - t0], dtype=torch.float64)
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
     # per-stage device times from as many instrumented steps again (outside the timed region)
@@ -618,25 +653,29 @@ def run_multi(args, rank, world):
              "bucket_hist_ms", "bucket_scatter_ms", "sub_partition_ms", "total_ms")
     acc = {k: 0.0 for k in timed}
     acc.update({"merge_kernel_launches": 0, "merge_passes": 0, "sent": 0, "tile_sort_keys": 0, "exchange_path": 0})
-    for _ in range(args.steps):
-        ptr, nout = ctx.sample_sort_dev(t_in)
-        st = ctx.stats()  # synchronizes this rank's stream
-        for k in timed:
-            acc[k] += st[k]
-        acc["tile_sort_keys"] += st["tile_sort_keys"]
-        acc["merge_kernel_launches"] += st["merge_kernel_launches"]
-        acc["merge_passes"] += st["merge_passes"]
-        acc["sent"] += st["keys_sent"]
-        acc["exchange_path"] = st["exchange_path"]
-    torch.cuda.synchronize()
-    dist.barrier()
+
+    def instrumented():
+        for _ in range(steps):
+            ctx.sample_sort_dev(t_in)
+            st = ctx.stats()  # synchronizes this rank's stream
+            for k in timed:
+                acc[k] += st[k]
+            acc["tile_sort_keys"] += st["tile_sort_keys"]
+            acc["merge_kernel_launches"] += st["merge_kernel_launches"]
+            acc["merge_passes"] += st["merge_passes"]
+            acc["sent"] += st["keys_sent"]
+            acc["exchange_path"] = st["exchange_path"]
+        torch.cuda.synchronize()
+
+    if not _sync_ok(dist, guarded(instrumented)):
+        return None, False, None, w, err or "a peer failed"
     # per-rank figures of the roofline, gathered (rank 0 reports the slowest rank)
-    steps = max(args.steps, 1)
-    mine = torch.tensor([acc["tile_sort_kernel_ms"] / steps, acc["alltoall_ms"] / steps, acc["exchange_ms"] / steps,
-                         acc["final_merge_ms"] / steps, acc["sent"] / steps, sz,
-                         acc["bucket_hist_ms"] / steps, acc["bucket_scatter_ms"] / steps,
-                         acc["sub_partition_ms"] / steps, acc["tile_sort_keys"] / steps, acc["exchange_path"],
-                         acc["total_ms"] / steps],
+    st_n = max(steps, 1)
+    mine = torch.tensor([acc["tile_sort_kernel_ms"] / st_n, acc["alltoall_ms"] / st_n, acc["exchange_ms"] / st_n,
+                         acc["final_merge_ms"] / st_n, acc["sent"] / st_n, sz,
+                         acc["bucket_hist_ms"] / st_n, acc["bucket_scatter_ms"] / st_n,
+                         acc["sub_partition_ms"] / st_n, acc["tile_sort_keys"] / st_n, acc["exchange_path"],
+                         acc["total_ms"] / st_n],
                         dtype=torch.float64)
     everyone = [torch.zeros_like(mine) for _ in range(world)]
     dist.all_gather(everyone, mine)
@@ -651,11 +690,119 @@ def run_multi(args, rank, world):
     for r in range(world - 1):
         if A[r, 1] > 0 and A[r + 1, 1] > 0:
             ok &= bool(A[r, 3] <= A[r + 1, 2])
-    ctx.comm_destroy()
+    del t_in, st_in
+    torch.cuda.empty_cache()
+    return float(el.item()), ok, torch.stack(everyone).numpy(), w, None
+
+
+# The extra legs of a multi-GPU run (the driver issues one `bench.py --gpus N` per N,
+# so the other multi-GPU configs ride on it, after the metric's timed region): BASELINE configs
+# C3 (2^32 int32 over 8 GPUs; at N < 8 the same 2^29 keys per GPU), C4 (2^30 Zipf int64 over N)
+# and C5 (the C3 size with worker min(3, N-1) killed after its first partition level; through the
+# C master, in a child process).  Each leg: 3 timed steps after 1 warmup, an exchange deadline.
+LEG_NAMES = ("c3", "c4", "c5")
+
+
+def leg_plan(world):
+    c3_keys = 1 << 32 if world == 8 else (1 << 29) * world
+    return {"c3": {"keys": c3_keys, "dtype": "i32", "dist": "uniform"},
+            "c4": {"keys": 1 << 30, "dtype": "i64", "dist": "zipf"},
+            # (one GPU: two workers sharing it over the master's relay, a plumbing check at 2^26 keys)
+            "c5": ({"keys": c3_keys, "workers": world, "kill_rank": min(3, world - 1), "transport": "rccl"}
+                   if world > 1 else {"keys": 1 << 26, "workers": 2, "kill_rank": 1, "transport": "relay"})}
+
+
+def legs_wanted(args):
+    if args.legs in ("", "none"):
+        return []
+    want = LEG_NAMES if args.legs == "all" else tuple(x for x in args.legs.split(",") if x)
+    bad = [x for x in want if x not in LEG_NAMES]
+    if bad:
+        raise SystemExit(f"bench: unknown --legs {bad} (choose from {LEG_NAMES})")
+    return list(want)
+
+
+def leg_summary(name, spec, world, steps, res):
+    """The report of one sort leg (C3 / C4) from measure_samplesort's result, or its error."""
+    elapsed, ok, per_rank, w, err = res
+    out = {"config": {"c3": "C3", "c4": "C4"}[name], "keys": spec["keys"], "dtype": "int32" if w == 4 else "int64",
+           "dist": spec["dist"], "n_gpus": world, "steps": steps}
+    if err or elapsed is None:
+        out.update({"verified": False, "error": err or "failed"})
+        return out
+    ns = argparse.Namespace(keys=spec["keys"], steps=steps, warmup=1, dtype=spec["dtype"], dist=spec["dist"],
+                            no_cpu_baseline=True)
+    full = summarize_multi(ns, world, elapsed, per_rank, w)
+    out.update({"verified": bool(ok), "value": full["value"], "unit": "keys/s", "ms_per_step": full["ms_per_step"],
+                "workload": full["config"]["workload"], "roofline": full["roofline"]})
+    return out
+
+
+def run_c5_leg(spec, dtype="i32", timeout_s=900):
+    """C5 in a child process (bench.py --kill-rank, which runs the C master and its workers): this
+    process may have touched the GPU, so the master is started as a child, never exec'd."""
+    cmd = [sys.executable, "-u", os.path.abspath(__file__), "--kill-rank", str(spec["kill_rank"]),
+           "--gpus", str(spec["workers"]), "--keys", str(spec["keys"]), "--dtype", dtype, "--kill-after-stage", "0"]
+    t0 = time.perf_counter()
+    try:
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        return {"config": "C5", "verified": False, "error": f"timed out after {timeout_s} s"}
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    if p.returncode != 0 or not lines:
+        return {"config": "C5", "verified": False, "error": f"rc {p.returncode}: {(p.stderr or p.stdout)[-600:]}"}
+    r = json.loads(lines[-1])
+    r.update({"config": "C5", "wall_s": round(time.perf_counter() - t0, 1), "transport": spec["transport"]})
+    return r
+
+
+def run_multi(args, rank, world):
+    """One rank per GPU: gloo for control, RCCL (inside libdsort) for the key exchange.  Strong
+    scaling: the --keys total is split into equal contiguous chunks (server.c:185-216).  Then the
+    extra legs (--legs), which do not touch the metric's numbers."""
+    import torch
+    import torch.distributed as dist
+
+    import dsort
+
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    torch.cuda.set_device(local)
+    if world == 1 and "MASTER_PORT" not in os.environ:  # --path samplesort, one GPU, no launcher
+        os.environ.setdefault("DSORT_BENCH_STORE", os.path.join(tempfile.mkdtemp(prefix="dsort_bench_"), "store"))
+    init_group(dist, rank, world)
+    ctx = dsort.Context(local)
+    uid = [dsort.Context.unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(uid, src=0)
+    ctx.comm_init(world, rank, uid[0])
+    elapsed, ok, per_rank, w, _ = measure_samplesort(ctx, dist, rank, world, args.keys, args.dtype, args.dist,
+                                                     args.steps, args.warmup)
+    legs = {}
+    plan = leg_plan(world)
+    for name in legs_wanted(args):
+        if name == "c5":
+            continue
+        spec = plan[name]
+        ctx.set_option("comm_timeout_ms", int(args.leg_timeout * 1000))  # (a stuck exchange ends the leg)
+        t0 = time.perf_counter()
+        res = measure_samplesort(ctx, dist, rank, world, spec["keys"], spec["dtype"], spec["dist"], 3, 1, strict=False)
+        legs[name] = leg_summary(name, spec, world, 3, res)
+        legs[name]["wall_s"] = round(time.perf_counter() - t0, 1)
+        if res[4]:  # (the communicator may be gone: no further sort leg)
+            break
+    ctx.set_option("comm_timeout_ms", 0)
+    try:
+        ctx.comm_destroy()
+    except dsort.DsortError:
+        pass
     ctx.close()
+    torch.cuda.empty_cache()
+    dist.barrier()
+    if "c5" in legs_wanted(args) and rank == 0:
+        # (the other ranks hold no sort memory now and wait at the barrier below)
+        legs["c5"] = run_c5_leg(plan["c5"], timeout_s=int(args.leg_timeout * 4))
     dist.barrier()
     dist.destroy_process_group()
-    return float(el.item()), ok, torch.stack(everyone).numpy(), w
+    return elapsed, ok, per_rank, w, legs
 
 
 def result_header(args, world):
@@ -731,8 +878,10 @@ def report_single(args, elapsed, k):
     result["roofline"] = roof
     if k.get("torch_sort_ms"):
         result["gpu_library_reference"] = {
-            "what": "torch.sort of the same resident keys on the same GPU (rocPRIM radix sort), values only; "
-                    "for context, outside the timed region",
+            "what": "torch.sort of the same resident keys on the same GPU (rocPRIM radix sort of (key, int64 "
+                    "index) pairs -- torch.sort always returns the indices too, so it moves 3x (int32) / 2x "
+                    "(int64) the bytes of a keys-only sort: not like for like); for context, outside the "
+                    "timed region",
             "ms": round(k["torch_sort_ms"], 3), "keys_per_s": n / (k["torch_sort_ms"] * 1e-3),
             "speedup_of_value": round(k["torch_sort_ms"] / step_ms, 3)}
     if not args.no_cpu_baseline and args.dtype == "i32":
@@ -749,12 +898,17 @@ def multi_all_kernels(per_rank, w, world, dist):
     of the one-GPU sort, bytes per key scaled to the rank's keys: a rank runs the same kernels on its
     chunk and on the keys it receives) plus the exchange's own HBM traffic (the bytes a rank ships
     are read once and written once at the receiver), over the slowest rank's device time, against
-    the aggregate HBM peak (N x 8 TB/s).  None when there is no PMC table of this key width."""
-    tot, src, match = 0, None, False
+    the aggregate HBM peak (N x 8 TB/s).  None when there is no PMC table of this key width, or for
+    skewed keys: the one-GPU out-of-place sort drops the keys of single-key buckets in
+    its scatter, the bucket exchange writes every key, so the one-GPU table would misstate them."""
+    if dist != "uniform":
+        return None
+    tot, src, match = 0, None, True
     for r in range(world):
-        pb, src, match = pmc_sort_bytes(int(per_rank[r, PR_KEYS]), w, dist)
+        pb, src, m = pmc_sort_bytes(int(per_rank[r, PR_KEYS]), w, dist)
         if pb is None:
             return None
+        match &= bool(m)  # (measured only when every rank's figure is)
         tot += pb + 2 * w * int(per_rank[r, PR_SENT])
     dev = float(per_rank[:, PR_TOTAL].max())
     if dev <= 0:
@@ -767,7 +921,18 @@ def multi_all_kernels(per_rank, w, world, dist):
                                "+ 2 x key bytes shipped) / slowest rank's device time / (N x 8 TB/s)"}}
 
 
-def report_multi(args, world, elapsed, per_rank, w):
+def report_multi(args, world, elapsed, per_rank, w, legs=None):
+    result = summarize_multi(args, world, elapsed, per_rank, w)
+    if legs:
+        result["legs"] = legs
+    if not args.no_cpu_baseline and args.dtype == "i32":
+        # the reference's CPU path beside the N-GPU number (rank 0, after the timed region and the
+        # other ranks' exit): the same leg as N = 1
+        result["cpu_baseline"] = cpu_baseline(args.cpu_sample_keys, args.keys)
+    print(json.dumps(result), flush=True)
+
+
+def summarize_multi(args, world, elapsed, per_rank, w):
     result = result_header(args, world)
     n = args.keys
     step_ms = 1000.0 * elapsed / args.steps
@@ -828,11 +993,7 @@ def report_multi(args, world, elapsed, per_rank, w):
         roof["all_kernels"] = ak["detail"]
     roof["device_ms_per_rank"] = [round(float(x), 3) for x in per_rank[:, PR_TOTAL]]
     result["roofline"] = roof
-    if not args.no_cpu_baseline and args.dtype == "i32":
-        # the reference's CPU path beside the N-GPU number (rank 0, after the timed region and the
-        # other ranks' exit): the same leg as N = 1
-        result["cpu_baseline"] = cpu_baseline(args.cpu_sample_keys, n)
-    print(json.dumps(result), flush=True)
+    return result
 
 
 def run_fault(args):
@@ -975,11 +1136,11 @@ def main(argv=None):
         elapsed, k = run_single(args)
         report_single(args, elapsed, k)
         return 0
-    elapsed, ok, per_rank, w = run_multi(args, rank, world)
+    elapsed, ok, per_rank, w, legs = run_multi(args, rank, world)
     if rank == 0:
         if not ok:
             raise SystemExit("bench: distributed output failed verification")
-        report_multi(args, world, elapsed, per_rank, w)
+        report_multi(args, world, elapsed, per_rank, w, legs)
     return 0
 
 

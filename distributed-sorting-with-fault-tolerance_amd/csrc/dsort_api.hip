@@ -495,6 +495,66 @@ static int comm_stream(dsort_ctx *ctx) {
     return DSORT_OK;
 }
 
+// DSORT_OPT_TEST_WAVE_FENCE (test only): fingerprints (fingerprint_kernel: sum and xor of
+// splitmix64, order independent) of device ranges taken on the sort stream before and after a step
+// of the exchange; any range that changed fails the sort with DSORT_EHIP naming it.  Value 2 tests
+// the fence itself: one key of the first range is flipped between the two prints.
+template <typename T>
+__global__ void fence_poke_kernel(T *p) {
+    p[0] ^= (T)1;
+}
+
+template <typename T>
+struct WaveFence {
+    struct R {
+        const T *p;
+        uint64_t n;
+        std::string what;
+    };
+    std::vector<R> r;
+    bool on() const { return !r.empty(); }
+    void add(const T *p, uint64_t n, std::string what) {
+        if (n) r.push_back(R{p, n, std::move(what)});
+    }
+    int prepare(dsort_ctx *ctx) {
+        if (r.empty()) return DSORT_OK;
+        const size_t bytes = r.size() * 4 * sizeof(unsigned long long);
+        int rc = ensure(ctx, &ctx->fence, &ctx->fence_bytes, bytes, "wave fence");
+        return rc ? rc : ensure_host(ctx, &ctx->fence_host, &ctx->fence_host_bytes, bytes);
+    }
+    // which = 0: before, 1: after
+    int print(dsort_ctx *ctx, hipStream_t s, int which) {
+        auto *acc = static_cast<unsigned long long *>(ctx->fence) + (size_t)which * 2 * r.size();
+        DSORT_HIP(ctx, hipMemsetAsync(acc, 0, r.size() * 2 * sizeof(unsigned long long), s));
+        for (size_t i = 0; i < r.size(); ++i) {
+            hipLaunchKernelGGL((fingerprint_kernel<T>), dim3(grid_for(r[i].n, 256 * 8)), dim3(256), 0, s, r[i].p,
+                               r[i].n, acc + 2 * i);
+            DSORT_HIP(ctx, hipGetLastError());
+        }
+        return DSORT_OK;
+    }
+    int check(dsort_ctx *ctx, hipStream_t s, double deadline) {
+        if (ctx->opt.test_wave_fence == 2) {
+            hipLaunchKernelGGL((fence_poke_kernel<T>), dim3(1), dim3(1), 0, s, const_cast<T *>(r[0].p));
+            DSORT_HIP(ctx, hipGetLastError());
+        }
+        int rc = print(ctx, s, 1);
+        if (rc) return rc;
+        const size_t m = r.size() * 4;
+        DSORT_HIP(ctx, hipMemcpyAsync(ctx->fence_host, ctx->fence, m * sizeof(unsigned long long),
+                                      hipMemcpyDeviceToHost, s));
+        if ((rc = exch_wait(ctx, s, true, deadline, "wave fence"))) return rc;
+        const auto *h = static_cast<const unsigned long long *>(ctx->fence_host);
+        const size_t R2 = 2 * r.size();
+        for (size_t i = 0; i < r.size(); ++i)
+            if (h[2 * i] != h[R2 + 2 * i] || h[2 * i + 1] != h[R2 + 2 * i + 1])
+                return set_err(ctx, DSORT_EHIP, "DSORT_OPT_TEST_WAVE_FENCE: wave 0's second level / tile sort changed " +
+                                                    r[i].what + " (" + std::to_string(r[i].n) + " keys)");
+        ctx->stats.fence_ranges += (int)r.size();
+        return DSORT_OK;
+    }
+};
+
 // The bucket exchange (dsort_internal.h): samples of the unsorted keys from every
 // rank -> the same Btot global splitters everywhere -> this rank's keys partitioned into the Btot
 // buckets (the first level of the one-GPU sort) -> buckets [q Bl, (q+1) Bl) to rank q (RCCL
@@ -593,6 +653,24 @@ static int sample_sort_bx(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, T **d
     if (rc) return rc;
     T *rb = behind ? part : static_cast<T *>(ctx->recv);  // (the second level's source)
     exchange_fault_point(ctx, 2);
+    // DSORT_OPT_TEST_WAVE_FENCE: what wave 1 still needs while wave 0's second level and tile sort
+    // run -- its sends (part, every q != me), this rank's own wave-1 buckets (read in place when
+    // `behind`) and its landing zone -- fingerprinted before and after wave 0 (dsort.h).  Set up before anything is
+    // enqueued on the comm stream (the arena may grow)
+    WaveFence<T> fence;
+    if (ctx->opt.test_wave_fence && W == 2) {
+        const int w = 1;
+        for (int q = 0; q < P; ++q) {
+            const uint64_t so = hme[(size_t)q * Bl + jb[w]], sn = hme[(size_t)q * Bl + jb[w + 1]] - so;
+            fence.add(part + so, sn, q != me ? "wave-1 send range of part to rank " + std::to_string(q)
+                                             : std::string("this rank's own wave-1 buckets in part"));
+            const size_t k = (size_t)w * P + q;
+            // (over RCCL with peers the landing zone fills while wave 0 runs: not fenced there)
+            if (!(behind && q == me) && (host_tx || P == 1))
+                fence.add(rb + rpos[k], rcnt[k], "wave-1 landing zone of the keys from rank " + std::to_string(q));
+        }
+        if ((rc = fence.prepare(ctx))) return rc;
+    }
     // 4. the buckets to their ranks: per wave one send and one receive per peer (all-to-all-v over
     //    xGMI), on the comm stream after the partition
     if (ctx->ev_ok) {
@@ -624,18 +702,22 @@ static int sample_sort_bx(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, T **d
                                               hipMemcpyDeviceToDevice, cs));
             DSORT_HIP(ctx, hipEventRecord(ctx->xev[w], cs));
         }
-    } else {
+    }
+    if (host_tx) {
+        // The same order as RCCL's: wave w's send ranges are staged from `part` right
+        // before its all-to-all, and wave w's second level and tile sort are queued before wave
+        // w+1 is staged -- so wave 1's sends are read from `part` after wave 0's kernels ran on it,
+        // as the 8-GPU run reads them while those kernels run.  The host buffer mirrors `part`
+        // (send displacements = positions in part); the receive layout is the device one minus
+        // the partition (behind: the other sources from n_local on, this rank's own buckets not
+        // shipped).
         rc = ensure_host(ctx, &ctx->xfer, &ctx->xfer_bytes, (pl.n_local ? pl.n_local : 1) * sizeof(T));
         if (rc) return rc;
         rc = ensure_host(ctx, &ctx->xfer2, &ctx->xfer2_bytes, (nrecv ? nrecv : 1) * sizeof(T));
         if (rc) return rc;
-        if (pl.n_local)
-            DSORT_HIP(ctx, hipMemcpyAsync(ctx->xfer, part, pl.n_local * sizeof(T), hipMemcpyDeviceToHost, s));
-        rc = exch_wait(ctx, s, true, deadline, "key staging");
-        if (rc) return rc;
-        // wave by wave; the receive layout of the host buffer is the device one minus the partition
-        // (behind: the other sources from n_local on, this rank's own buckets not shipped)
         const uint64_t shift = behind ? pl.n_local : 0;
+        T *outp = static_cast<T *>(ctx->recv2);
+        uint64_t out_off = 0;
         for (int w = 0; w < W; ++w) {
             std::vector<size_t> sc(P), sd(P), rcn(P), rd(P);
             uint64_t lo = ~0ull, hi = 0;
@@ -647,11 +729,16 @@ static int sample_sort_bx(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, T **d
                 sc[q] = self ? 0 : (hme[(size_t)q * Bl + jb[w + 1]] - so) * sizeof(T);
                 rcn[q] = self ? 0 : rcnt[k] * sizeof(T);
                 rd[q] = self ? 0 : (rpos[k] - shift) * sizeof(T);
+                if (sc[q])  // (stage this wave's range for q, and nothing else)
+                    DSORT_HIP(ctx, hipMemcpyAsync(static_cast<char *>(ctx->xfer) + sd[q], part + so, sc[q],
+                                                  hipMemcpyDeviceToHost, s));
                 if (!self && rcnt[k]) {
                     lo = std::min<uint64_t>(lo, rpos[k]);
                     hi = std::max<uint64_t>(hi, rpos[k] + rcnt[k]);
                 }
             }
+            rc = exch_wait(ctx, s, true, deadline, w ? "key staging (wave 1)" : "key staging (wave 0)");
+            if (rc) return rc;
             if ((rc = tx_fault_point(ctx))) return rc;
             if ((rc = ctx->tx->alltoallv(ctx->xfer, sc.data(), sd.data(), ctx->xfer2, rcn.data(), rd.data(),
                                          w ? "key all-to-all (wave 1)" : "key all-to-all (wave 0)")))
@@ -659,38 +746,71 @@ static int sample_sort_bx(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, T **d
             if (hi > lo)
                 DSORT_HIP(ctx, hipMemcpyAsync(rb + lo, static_cast<char *>(ctx->xfer2) + (lo - shift) * sizeof(T),
                                               (hi - lo) * sizeof(T), hipMemcpyHostToDevice, s));
+            if (w == 0 && ctx->ev_ok) {
+                DSORT_HIP(ctx, hipEventRecord(ctx->ev[6], s));  // (the first wave's keys in)
+                DSORT_HIP(ctx, hipEventRecord(ctx->ev[3], s));
+                ctx->ev_mask |= 64u | 8u;
+            }
+            if (w == 0 && fence.on() && (rc = fence.print(ctx, s, 0))) return rc;
+            uint64_t nw = 0;
+            rc = bx_local_sort<T>(ctx, rb, outp, pl, hb_all.data(), base.data() + (size_t)w * P, jb[w], jb[w + 1],
+                                  out_off, w, W, s, true, &nw);
+            if (rc) return rc;
+            out_off += nw;
+            if (w == 0 && fence.on() && (rc = fence.check(ctx, s, deadline))) return rc;
         }
+        flush_later(ctx);
+        ctx->last_stream = s;
+        ctx->stats.keys_in = pl.n_local;
+        ctx->stats.keys_out = nrecv;
+        ctx->stats.keys_sent = sent;
+        ctx->stats.exchange_path = 1;
+        *d_out = outp;
+        *n_out = nrecv;
+        return DSORT_OK;
     }
     // 5. the second level and the tile sort of this rank's buckets, wave by wave, each queued behind
     //    its receives while later waves are in flight (the host builds and uploads a wave's tables
     //    meanwhile); the host waits inside poll the abort flag and the deadline, as a dead peer never
     //    completes the stream.  Kill stages 1 and 2 (after the first wave's).
     T *outp = static_cast<T *>(ctx->recv2);
-    ctx->poll_waits = !host_tx;
+    ctx->poll_waits = true;
     ctx->poll_deadline = deadline;
     ctx->poll_stream = s;
     uint64_t out_off = 0;
     for (int w = 0; w < W && !rc; ++w) {
-        if (!host_tx) {
-            DSORT_HIP(ctx, hipStreamWaitEvent(s, ctx->xev[w], 0));
-            if (w == 0 && ctx->ev_ok) {
-                DSORT_HIP(ctx, hipEventRecord(ctx->ev[6], s));  // (the first wave's keys in)
-                DSORT_HIP(ctx, hipEventRecord(ctx->ev[3], s));
-                ctx->ev_mask |= 64u | 8u;
-            }
+        DSORT_HIP(ctx, hipStreamWaitEvent(s, ctx->xev[w], 0));
+        if (w == 0 && ctx->ev_ok) {
+            DSORT_HIP(ctx, hipEventRecord(ctx->ev[6], s));  // (the first wave's keys in)
+            DSORT_HIP(ctx, hipEventRecord(ctx->ev[3], s));
+            ctx->ev_mask |= 64u | 8u;
         }
+        if (w == 0 && fence.on()) rc = fence.print(ctx, s, 0);
         uint64_t nw = 0;
-        rc = bx_local_sort<T>(ctx, rb, outp, pl, hb_all.data(), base.data() + (size_t)w * P, jb[w], jb[w + 1], out_off,
-                              w, W, s, true, &nw);
+        if (!rc)
+            rc = bx_local_sort<T>(ctx, rb, outp, pl, hb_all.data(), base.data() + (size_t)w * P, jb[w], jb[w + 1],
+                                  out_off, w, W, s, true, &nw);
         out_off += nw;
-    }
-    if (host_tx && ctx->ev_ok && !rc) {
-        DSORT_HIP(ctx, hipEventRecord(ctx->ev[6], s));
-        ctx->ev_mask |= 64u;
+        if (!rc && w == 0 && fence.on()) rc = fence.check(ctx, s, deadline);
     }
     ctx->poll_waits = false;
-    if (rc == DSORT_ECOMM || rc == DSORT_ETIMEOUT) abort_comm_locked(ctx);
-    if (rc) return rc;
+    if (rc) {
+        // The arenas the second level replaced while the keys were in flight (release_dev) are
+        // freed once no kernel can touch them (a faulted sort kept its multi-GB scratch
+        // until the next good exchange, so the recovery ran at twice the footprint).  After a
+        // communicator failure the abort ends the comm stream's kernels; after a local failure
+        // every send and receive was enqueued and still completes: wait for it, bounded by the
+        // deadline and the abort flag (a failing wait aborts the communicator).
+        if (rc == DSORT_ECOMM || rc == DSORT_ETIMEOUT) {
+            abort_comm_locked(ctx);
+        } else {
+            const std::string err = ctx->err;
+            (void)exch_wait(ctx, cs, true, deadline, "key all-to-all (after a local failure)");
+            ctx->err = err;
+        }
+        if (hipStreamSynchronize(s) == hipSuccess) flush_later(ctx);
+        return rc;
+    }
     // the receives have landed (and the test hold, DSORT_OPT_TEST_HOLD_EXCHANGE, is released)
     rc = exch_wait(ctx, cs, true, deadline, "key all-to-all", ctx->opt.test_hold_exchange != 0);
     if (rc) return rc;
@@ -1013,13 +1133,14 @@ int dsort_finalize(dsort_ctx *ctx) {
     flush_later(ctx);
     void *bufs[] = {ctx->scratch, ctx->scratch2, ctx->splits, ctx->groups, ctx->io, ctx->io2, ctx->red,
                     ctx->local, ctx->recv, ctx->recv2, ctx->small, ctx->text_status,
-                    ctx->bucket, ctx->sub, ctx->sub_alt, ctx->stmp, ctx->bxs, ctx->tfb};
+                    ctx->bucket, ctx->sub, ctx->sub_alt, ctx->stmp, ctx->bxs, ctx->tfb, ctx->fence};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (ctx->red_host) (void)hipHostFree(ctx->red_host);
     if (ctx->small_host) (void)hipHostFree(ctx->small_host);
     if (ctx->xfer) (void)hipHostFree(ctx->xfer);
     if (ctx->xfer2) (void)hipHostFree(ctx->xfer2);
+    if (ctx->fence_host) (void)hipHostFree(ctx->fence_host);
     if (ctx->groups_host) (void)hipHostFree(ctx->groups_host);
     if (ctx->groups_ev) (void)hipEventDestroy(ctx->groups_ev);
     if (ctx->bucket_host) (void)hipHostFree(ctx->bucket_host);
@@ -1105,6 +1226,10 @@ int dsort_set_option(dsort_ctx *ctx, int option, int64_t v) {
             if (v < 0) return set_err(ctx, DSORT_EINVAL, "DSORT_OPT_TEST_TILE_CAP: >= 0");
             o.test_tile_cap = v;
             return DSORT_OK;
+        case DSORT_OPT_TEST_WAVE_FENCE:
+            if (v < 0 || v > 2) return set_err(ctx, DSORT_EINVAL, "DSORT_OPT_TEST_WAVE_FENCE: 0, 1 or 2");
+            o.test_wave_fence = v;
+            return DSORT_OK;
         default:
             return set_err(ctx, DSORT_EINVAL, "unknown option " + std::to_string(option));
     }
@@ -1125,6 +1250,7 @@ int dsort_get_option(const dsort_ctx *ctx, int option, int64_t *v) {
         case DSORT_OPT_TEST_FAIL_EXCHANGE: *v = o.test_fail_exchange; return DSORT_OK;
         case DSORT_OPT_STAGE_TIMING: *v = o.stage_timing; return DSORT_OK;
         case DSORT_OPT_TEST_TILE_CAP: *v = o.test_tile_cap; return DSORT_OK;
+        case DSORT_OPT_TEST_WAVE_FENCE: *v = o.test_wave_fence; return DSORT_OK;
         case DSORT_OPT_SUB_KEYS: *v = o.sub_keys; return DSORT_OK;
         case DSORT_OPT_SUB_OVERSAMPLE: *v = o.sub_os; return DSORT_OK;
         case DSORT_OPT_SUB_GATHER: *v = o.sub_gather; return DSORT_OK;

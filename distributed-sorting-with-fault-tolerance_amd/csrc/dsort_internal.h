@@ -66,6 +66,7 @@ struct dsort_opts {
     int64_t test_hold_exchange = 0; // DSORT_OPT_TEST_HOLD_EXCHANGE
     int64_t test_fail_exchange = -1; // DSORT_OPT_TEST_FAIL_EXCHANGE
     int64_t test_tile_cap = 0;      // DSORT_OPT_TEST_TILE_CAP
+    int64_t test_wave_fence = 0;    // DSORT_OPT_TEST_WAVE_FENCE
     int64_t sub_keys = -1;          // DSORT_OPT_SUB_KEYS: -1 = 3/16 of a tile, 0 = no second level
     int64_t sub_os = -1;            // DSORT_OPT_SUB_OVERSAMPLE: -1 = 8 (4 at sub-buckets <= TILE/8)
     int64_t sub_gather = 1;         // DSORT_OPT_SUB_GATHER
@@ -136,6 +137,10 @@ struct dsort_ctx {
     size_t xfer_bytes = 0;
     void *xfer2 = nullptr;
     size_t xfer2_bytes = 0;
+    void *fence = nullptr;        // DSORT_OPT_TEST_WAVE_FENCE: fingerprints (device, pinned mirror)
+    size_t fence_bytes = 0;
+    void *fence_host = nullptr;
+    size_t fence_host_bytes = 0;
     int nranks = 1;
     int rank = 0;
     void *local = nullptr;  // locally sorted chunk

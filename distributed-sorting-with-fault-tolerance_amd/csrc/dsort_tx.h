@@ -7,9 +7,11 @@
 // peers: every rank runs the same fixed sequence of collectives (key counts, samples, bucket
 // starts, the key waves), and a rank that fails locally between two of them (an allocation, a HIP
 // error, a stage the sort refuses) must not leave its peers blocked in a collective it never joins.
-// So every collective after the first is preceded by a GATE: an 8-byte all-gather of every rank's
-// status.  A rank that failed reports its failure at the next gate and returns; every peer meets
-// it there and returns DSORT_ECOMM naming that rank.  A callback that fails or gives up (the
+// So every collective, the first one included, is preceded by a GATE: an 8-byte all-gather of
+// every rank's status.  A rank that failed reports its failure at the next gate and returns; every
+// peer meets it there and returns DSORT_ECOMM naming that rank.  (ABI 5 gated the 2nd..last only,
+// so a rank failing before its first collective -- the presorted entry's local staging, or a
+// failure injected at collective 0 -- left its peers blocked in that collective: ADVICE r5.)  A callback that fails or gives up (the
 // transport itself broke, or the exchange deadline passed) ends the sequence on that rank: no
 // further collective runs on a broken transport.  The callbacks bound their own waits by
 // dsort_comm_deadline_ms (the remainder of DSORT_OPT_COMM_TIMEOUT_MS), so a peer that hangs
@@ -36,7 +38,7 @@ inline double tx_now_ms() {
 class TxSeq {
   public:
     // t: the caller's transport over P ranks; deadline on the tx_now_ms() scale (0 = none); ncoll:
-    // the collectives this sort will run (the gates sit in front of the 2nd..last).
+    // the collectives this sort will run (a gate sits in front of each).
     TxSeq(const dsort_transport &t, int P, double deadline, int ncoll)
         : t_(t), P_(P), deadline_(deadline), left_(ncoll) {}
 
@@ -56,7 +58,7 @@ class TxSeq {
     // This rank failed locally: tell the peers at the next gate (when a collective is still ahead
     // and the transport works), so that they leave the sequence there too.
     void report_failure(int code) {
-        if (broken_ || left_ <= 0 || started_ == 0) return;
+        if (broken_ || left_ <= 0) return;
         int64_t st = code ? code : DSORT_ECOMM;
         std::vector<int64_t> all((size_t)P_);
         left_ = 0;  // (whatever the gate says: this rank runs no further collective)
@@ -81,7 +83,7 @@ class TxSeq {
             broken_ = true;
             return set(DSORT_ETIMEOUT, std::string(what) + ": the exchange deadline (DSORT_OPT_COMM_TIMEOUT_MS) passed");
         }
-        if (started_ > 0) {  // the gate in front of every collective but the first
+        {  // the gate in front of every collective
             std::vector<int64_t> all((size_t)P_);
             int rc = call_gate(0, all.data(), what);
             if (rc) return rc;

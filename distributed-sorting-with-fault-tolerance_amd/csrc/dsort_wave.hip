@@ -2070,7 +2070,10 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
             if (early)
                 if (int rc_ = sync_stream(ctx, s, "early tile sort")) return rc_;
             ctx->stats.sub_scatter_fallback = 1;
-            return sub_sort<T>(ctx, src, d_keys, n, hb, B, m, s, timed, false, pure, pure_done, bspl, true, pm);
+            // (fill_keys passed on: the retry fills the dropped pure buckets itself instead of relying
+            // on this attempt's queued fill -- ADVICE r5)
+            return sub_sort<T>(ctx, src, d_keys, n, hb, B, m, s, timed, false, pure, pure_done, bspl, true, pm,
+                               fill_keys);
         }
         // every tile's piece table
         if (ntiles && !pieces_in_scan) {

@@ -22,6 +22,7 @@ except Exception:  # pragma: no cover
     torch = None
 
 DSORT_OK = 0
+DSORT_ECOMM = -4
 DSORT_ETIMEOUT = -6
 ERRORS = {-1: "EINVAL", -2: "ENOMEM", -3: "EHIP", -4: "ECOMM", -5: "ENODEV", -6: "ETIMEOUT", -7: "ESTAGE"}
 
@@ -50,9 +51,8 @@ OPTIONS = {"buckets": 1, "bucket_keys": 2, "bucket_oversample": 3,
            "max_fanin_log2": 5, "kill_after_stage": 6, "kill_in_exchange": 7,
            "comm_timeout_ms": 8,
            "sub_keys": 9, "sub_oversample": 10, "sub_gather": 11, "test_hold_exchange": 12,
-           "test_fail_exchange": 13, "stage_timing": 14, "test_tile_cap": 15}
-# ABI 2's option name, a deprecated alias of "kill_after_stage" until ABI 6 (dsort.h)
-DEPRECATED_OPTIONS = {"kill_after_pass": "kill_after_stage"}
+           "test_fail_exchange": 13, "stage_timing": 14, "test_tile_cap": 15,
+           "test_wave_fence": 16}
 
 
 class DsortError(RuntimeError):
@@ -71,7 +71,8 @@ class Stats(ctypes.Structure):
                 ("bucket_hist_ms", ctypes.c_double), ("bucket_scatter_ms", ctypes.c_double),
                 ("sub_partition_ms", ctypes.c_double), ("sub_split_subbuckets", ctypes.c_int),
                 ("sub_scatter_fallback", ctypes.c_int), ("exchange_path", ctypes.c_int),
-                ("first_level_map", ctypes.c_int)]
+                ("first_level_map", ctypes.c_int),
+                ("fence_ranges", ctypes.c_int)]  # ABI 6
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -98,7 +99,12 @@ def torch_dist_transport(world, pg=None, deadline_fn=None):
     Every wait is bounded by the exchange deadline: `deadline_fn()` gives the milliseconds left
     (-1 = none).  Context.comm_init_transport sets it to dsort_comm_deadline_ms, so a collective
     whose peer never arrives returns DSORT_ETIMEOUT (-6) at the sort's DSORT_OPT_COMM_TIMEOUT_MS
-    instead of blocking until gloo's own timeout (dsort.h, ABI 5)."""
+    instead of blocking until gloo's own timeout (dsort.h, ABI 5).
+
+    A timed-out gloo operation stays queued on the group, so a later collective on it could pair
+    with a slow peer's stale one (a status gate and a key count are both 8 bytes).  After the first
+    timeout the transport is therefore POISONED: every later callback fails at once (the sort
+    returns DSORT_ECOMM) and the group must be rebuilt, as ftsort.py does for its survivors."""
     import datetime
 
     import torch.distributed as dist
@@ -114,11 +120,14 @@ def torch_dist_transport(world, pg=None, deadline_fn=None):
         except RuntimeError as e:
             if "timed out" in str(e).lower():
                 print("dsort host transport: no answer before the exchange deadline", flush=True)
+                t.poisoned = "a collective timed out at the exchange deadline"
                 return DSORT_ETIMEOUT
             raise
         return 0
 
     def _allgather(user, send, recv, nbytes):
+        if t.poisoned:
+            return DSORT_ECOMM
         try:
             mine = torch.frombuffer(bytearray(ctypes.string_at(send, nbytes)), dtype=torch.uint8) \
                 if nbytes else torch.empty(0, dtype=torch.uint8)
@@ -139,6 +148,8 @@ def torch_dist_transport(world, pg=None, deadline_fn=None):
             return 1
 
     def _alltoallv(user, send, sc, sd, recv, rc, rd):
+        if t.poisoned:
+            return DSORT_ECOMM
         try:
             scounts = [int(sc[i]) for i in range(world)]
             rcounts = [int(rc[i]) for i in range(world)]
@@ -168,6 +179,7 @@ def torch_dist_transport(world, pg=None, deadline_fn=None):
     t = Transport(None, ALLGATHER_FN(_allgather), ALLTOALLV_FN(_alltoallv))
     t._keep = (_allgather, _alltoallv)  # the C side holds raw function pointers
     t.deadline_fn = deadline_fn
+    t.poisoned = None  # (set by the first timeout: the group must be rebuilt)
     return t
 
 
@@ -350,13 +362,7 @@ class Context:
     # ---------------- options (dsort_set_option) -----------------------------------------
     @staticmethod
     def _opt(name):
-        if name in DEPRECATED_OPTIONS:
-            import warnings
-
-            warnings.warn(f"dsort option {name!r} is deprecated (removed with ABI 6): use "
-                          f"{DEPRECATED_OPTIONS[name]!r}", DeprecationWarning, stacklevel=3)
-            name = DEPRECATED_OPTIONS[name]
-        return OPTIONS[name]
+        return OPTIONS[name]  # (ABI 6 dropped ABI 2's "kill_after_pass" alias)
 
     def set_option(self, name, value):
         self.check(self.lib.dsort_set_option(self.h, self._opt(name), int(value)))

@@ -175,11 +175,6 @@ int samplesort_master(int argc, char **argv, const char *argv0) {
         else if (!strcmp(a, "--kill-rank")) o.kill_rank = atoi(NEXT());
         else if (!strcmp(a, "--kill-stage")) kill_stage_exchange = !strcmp(NEXT(), "exchange");
         else if (!strcmp(a, "--kill-after-stage")) o.kill_after_pass = atoi(NEXT());
-        else if (!strcmp(a, "--kill-after-pass")) { /* ABI 2 name, kept for one more ABI version */
-            fprintf(stderr, "master: --kill-after-pass is deprecated (removed with ABI 6): it now means "
-                            "--kill-after-stage (stage numbers: dsort.h DSORT_OPT_KILL_AFTER_STAGE)\n");
-            o.kill_after_pass = atoi(NEXT());
-        }
         else if (!strcmp(a, "--kill-in-recovery")) o.kill_in_recovery = atoi(NEXT());
         else if (!strcmp(a, "--hang-rank")) o.hang_rank = atoi(NEXT());
         else if (!strcmp(a, "--kill-exchange-stage")) o.kill_exchange_stage = atoi(NEXT());

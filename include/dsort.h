@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define DSORT_ABI_VERSION 5
+#define DSORT_ABI_VERSION 6
 
 #define DSORT_OK 0
 #define DSORT_EINVAL (-1)   /* bad argument */
@@ -91,6 +91,9 @@ typedef struct dsort_stats {
                                  top-11-bit map (int32 only), 1 linear over the splitters' key range, 2
                                  logarithmic (bucket_slotmap_kernel; int32 leaves the fixed map when it
                                  crowds the splitters of several keys into one slot); -1 none */
+    /* ABI 6 */
+    int fence_ranges;         /* DSORT_OPT_TEST_WAVE_FENCE: device ranges the last sample sort's wave
+                                 fence found unchanged across its first wave (0: no fence ran) */
 } dsort_stats;
 
 /* ---------------------------------------------------------------- lifecycle ---------- */
@@ -120,13 +123,8 @@ int dsort_synchronize(dsort_ctx *ctx);
                                          2^25 keys 0 tile sort, 1 + p merge pass p (dsort_sort_stages).
                                          A stage the sort never reaches makes it return DSORT_ESTAGE
                                          (ABI 3: DSORT_EINVAL) */
-/* ABI 2's DSORT_OPT_KILL_AFTER_PASS (option 6) counted merge passes; ABI 3 renumbered option 6 as
- * stages (merge path: ABI 2's pass p is stage 1 + p; the bucketed path's stages did not exist).
- * The old name stays for one more ABI version as a deprecated alias of option 6 (with the stage
- * meaning); it goes away in ABI 6.  Define DSORT_NO_DEPRECATED to drop it now. */
-#ifndef DSORT_NO_DEPRECATED
-#define DSORT_OPT_KILL_AFTER_PASS DSORT_OPT_KILL_AFTER_STAGE /* deprecated (ABI 5): use ..._STAGE */
-#endif
+/* ABI 2's DSORT_OPT_KILL_AFTER_PASS (option 6, merge passes) was kept as a deprecated alias of
+ * DSORT_OPT_KILL_AFTER_STAGE through ABI 5 and is gone from ABI 6. */
 #define DSORT_OPT_KILL_IN_EXCHANGE 7  /* fault injection: SIGKILL inside the sample-sort exchange, at
                                          stage 1 (samples all-gathered) or 2 (counts exchanged, keys
                                          about to move); -1 = off (default)                            */
@@ -158,6 +156,16 @@ int dsort_synchronize(dsort_ctx *ctx);
                                          tables hold at most t tiles, so a sort needing more takes
                                          the scatter path (stats.sub_scatter_fallback), as a
                                          pathological sampling would.  0 = off (default)            */
+#define DSORT_OPT_TEST_WAVE_FENCE 16   /* test only (ABI 6): 1 = the bucket exchange fingerprints what
+                                         its second wave still needs -- every wave-1 send range of the
+                                         partition buffer, this rank's own wave-1 buckets and (host
+                                         transport, or one rank) the wave-1 landing zone -- before and
+                                         after the first wave's second level and tile sort, and fails
+                                         with DSORT_EHIP naming a range that changed (over RCCL those
+                                         kernels run while wave 1 is on the links).  stats.fence_ranges
+                                         counts the ranges checked.  2 = the same, with one key of the
+                                         first range flipped in between (the fence's own test: the
+                                         sort must fail).  0 = off (default)                         */
 int dsort_set_option(dsort_ctx *ctx, int option, int64_t value);
 int dsort_get_option(const dsort_ctx *ctx, int option, int64_t *value);
 
@@ -227,10 +235,12 @@ int dsort_comm_init(dsort_ctx *ctx, int nranks, int rank, const char id[DSORT_UN
  *   allgather: rank r's `bytes` from `send` land at recv + r*bytes on every rank.
  *   alltoallv: send[sdispls[d] .. +scounts[d]) goes to rank d, which receives it at
  *              recv[rdispls[s] .. +rcounts[s]) for source s.
- * ABI 5: every collective of a sample sort after its first is preceded by an 8-byte all-gather of
- * every rank's status (a gate): a rank that fails locally between two collectives reports it at the
- * next gate, and every rank then returns (the failing one its own error, the others DSORT_ECOMM)
- * instead of blocking in a collective the failed rank never joins. */
+ * ABI 6: every collective of a sample sort, its first included (ABI 5: the 2nd..last), is preceded
+ * by an 8-byte all-gather of every rank's status (a gate): a rank that fails locally before or
+ * between collectives reports it at the next gate, and every rank then returns (the failing one its
+ * own error, the others DSORT_ECOMM) instead of blocking in a collective the failed rank never joins.
+ * The bucket exchange's key waves run in the order of the RCCL path: wave w's send ranges are read
+ * from the partition buffer after the second level and tile sort of wave w-1 were queued. */
 typedef struct dsort_transport {
     void *user;
     int (*allgather)(void *user, const void *send, void *recv, size_t bytes);

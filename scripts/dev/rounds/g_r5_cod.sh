@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 5: GPU text codec tests, then bench.py --codec (2^28 keys) for the default build and each of
-# build_variants/$VARS, interleaved twice.    VARS="v1 v2" TAG=x scripts/g_r5_cod.sh
+# build_variants/$VARS, interleaved twice.    VARS="v1 v2" TAG=x scripts/dev/rounds/g_r5_cod.sh
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$PWD; mkdir -p gpurun_out
 timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_text.py > gpurun_out/${TAG}_tests.log 2>&1 || exit $?

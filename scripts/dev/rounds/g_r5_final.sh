@@ -4,7 +4,7 @@
 # rank, then the bench lines (int32 with the CPU baseline; C4; the text codec with its kernel trace).  Stops at the first failure.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$PWD; mkdir -p gpurun_out
-bash scripts/g_r5_full.sh || exit $?
+bash scripts/dev/rounds/g_r5_full.sh || exit $?
 bash scripts/gpu_profile_r5.sh pmc trace c3 > gpurun_out/r5_profile.log 2>&1 || exit $?
 TAG=r5c3_ SCRIPT=scripts/c3_rank.py ARGS="--steps 1 --warmup 1 --no-check --only-bx" bash scripts/dev/pmc_sub.sh >> gpurun_out/r5_profile.log 2>&1 || exit $?
 # the PMC table of this build, made on the box so the bench lines below find it matched

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 5: A/B of compile-time variants (scripts/dev/ab_multi.sh) and kernel traces of back-to-back
 # sorts for the default build and one variant (one step's timeline: scripts/dev/timeline.py).
-#   VARS="v1 v2" TRACEVAR=v1 TAG=x scripts/g_r5_g.sh
+#   VARS="v1 v2" TRACEVAR=v1 TAG=x scripts/dev/rounds/g_r5_g.sh
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$PWD; mkdir -p gpurun_out
 bash scripts/dev/ab_multi.sh > gpurun_out/${TAG}_ab.log 2>&1 || exit $?

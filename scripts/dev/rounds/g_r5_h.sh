@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 5: GPU sort/bucket tests on the current build, then back-to-back bench-style steps
 # (scripts/dev/b2b.py: host gaps included) and device stage times of the default build against
-# build_variants/$VARS, interleaved.    VARS="v1 v2" TAG=x [B2B="--timing 0"] [NOTEST=1] scripts/g_r5_h.sh
+# build_variants/$VARS, interleaved.    VARS="v1 v2" TAG=x [B2B="--timing 0"] [NOTEST=1] scripts/dev/rounds/g_r5_h.sh
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$PWD; mkdir -p gpurun_out
 if [ -z "$NOTEST" ]; then

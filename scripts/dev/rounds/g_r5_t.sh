@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 5: second-level scan variants.  GPU sort/bucket tests on the current build, then kernel-trace
 # summaries of ktime.py (2^30 int32 and C4) and of the C3 rank for the default build and each of
-# build_variants/$VARS (TAG names the outputs).      VARS="v1 v2" TAG=x scripts/g_r5_t.sh
+# build_variants/$VARS (TAG names the outputs).      VARS="v1 v2" TAG=x scripts/dev/rounds/g_r5_t.sh
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$PWD; mkdir -p gpurun_out
 if [ -z "$NOTEST" ]; then

@@ -2,7 +2,7 @@
 # Round-4 measurement set: PMC passes (separate runs, scripts/dev/pmc_sub.sh) of the 2^30 int32 and
 # int64-Zipf sorts, the rocprofv3 kernel-trace summaries of the bench command, and the C3 rank
 # (scripts/c3_rank.py) trace.  Every GPU step has its own time limit; the script stops at the first
-# failure.   scripts/gpu_profile_r4.sh [pmc] [trace] [c3]     (default: all)
+# failure.   scripts/dev/rounds/gpu_profile_r4.sh [pmc] [trace] [c3]     (default: all)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$PWD; mkdir -p gpurun_out
 WHAT=${*:-pmc trace c3}

@@ -98,3 +98,40 @@ def test_pmc_sort_bytes_count_every_launch_of_a_kernel():
     pb, _, _ = bench.pmc_sort_bytes(1 << 30, 4, "uniform")
     exp = sum(r["traffic_bytes_per_sort"] for k, r in doc["kernels"].items() if not k.startswith(bench.NOT_SORT))
     assert pb == exp and pb > 3 * 2 * 4 * (1 << 30)  # about 3.7x one read + one write of the keys
+
+
+def test_multi_line_carries_c3_c4_c5_legs(capsys):
+    """the driver's one `bench.py --gpus N` run also measures configs C3, C4 and C5
+    after the metric's timed region.  Synthetic per-leg results through leg_summary and a C5 child
+    line: the keys are present, verified, and the metric's own value is unchanged by them."""
+    sys.path.insert(0, REPO)
+    import bench
+
+    world = 8
+    plan = bench.leg_plan(world)
+    assert plan["c3"]["keys"] == 1 << 32 and plan["c4"] == {"keys": 1 << 30, "dtype": "i64", "dist": "zipf"}
+    assert plan["c5"]["kill_rank"] == 3 and plan["c5"]["workers"] == 8 and plan["c5"]["transport"] == "rccl"
+    assert bench.leg_plan(2)["c3"]["keys"] == 1 << 30 and bench.leg_plan(2)["c5"]["kill_rank"] == 1
+    assert bench.leg_plan(1)["c5"]["transport"] == "relay"  # (one GPU: two workers share it)
+    args = bench.parse(["--gpus", str(world), "--steps", "5", "--no-cpu-baseline"])
+    assert bench.legs_wanted(args) == ["c3", "c4", "c5"]
+    assert bench.legs_wanted(bench.parse(["--no-legs"])) == []
+    assert bench.legs_wanted(bench.parse(["--legs", "c4"])) == ["c4"]
+    c3 = bench.leg_summary("c3", plan["c3"], world, 3, (3 * 6.0e-3, True, _per_rank(world, 1 << 32, 4), 4, None))
+    c4 = bench.leg_summary("c4", plan["c4"], world, 3, (3 * 2.0e-3, True, _per_rank(world, 1 << 30, 8), 8, None))
+    bad = bench.leg_summary("c4", plan["c4"], world, 3, (None, False, None, 8, "rank 2: ETIMEOUT"))
+    c5 = {"config": "C5", "value": 812.5, "unit": "ms", "verified": True, "transport": "rccl"}
+    bench.report_multi(args, world, 5 * 2.1e-3, _per_rank(world, 1 << 30, 4), 4, {"c3": c3, "c4": c4, "c5": c5})
+    d = json.loads([ln for ln in capsys.readouterr().out.splitlines() if ln.startswith("{")][-1])
+    assert abs(d["value"] - (1 << 30) / 2.1e-3) < 1e3  # the metric's value is the metric's own
+    legs = d["legs"]
+    assert legs["c3"]["config"] == "C3" and legs["c3"]["verified"] and legs["c3"]["keys"] == 1 << 32
+    assert abs(legs["c3"]["value"] - (1 << 32) / 6.0e-3) < 1e3 and legs["c3"]["dtype"] == "int32"
+    assert "xgmi" in legs["c3"]["roofline"] and legs["c3"]["roofline"]["frac"] > 0  # (synthetic stage times)
+    key = "all_kernels_frac" if "all_kernels_frac" in legs["c3"]["roofline"] else "all_kernels_frac_estimate"
+    assert key in legs["c3"]["roofline"]
+    assert legs["c4"]["dtype"] == "int64" and legs["c4"]["dist"] == "zipf" and legs["c4"]["verified"]
+    # (skewed keys: no all-kernels figure scaled from the one-GPU table, ADVICE r5)
+    assert "all_kernels_frac" not in legs["c4"]["roofline"] and "all_kernels_frac_estimate" not in legs["c4"]["roofline"]
+    assert legs["c5"]["verified"] and legs["c5"]["unit"] == "ms"
+    assert bad["verified"] is False and "ETIMEOUT" in bad["error"]

@@ -432,3 +432,39 @@ def test_tile_table_overflow_after_early_tile_sort(gpu_ctx, dtype, kind):
         st = gpu_ctx.stats()
     assert np.array_equal(out.cpu().numpy(), np.sort(a))
     assert st["sub_scatter_fallback"] == 0
+
+
+@pytest.mark.parametrize("dtype", ["i32", "i64"])
+def test_tile_table_overflow_with_dropped_pure_buckets(gpu_ctx, dtype):
+    """the out-of-place first-level scatter drops the keys of pure buckets (one heavy
+    key) and the second level fills their output ranges.  When the tile tables overflow, the
+    scatter-path retry must fill them itself (it is passed the fill keys) -- half the keys are one
+    heavy key here, so about half the output comes from the fill.  DSORT_OPT_TEST_TILE_CAP is set
+    just above the early tile sort's part, taken from a first run's tile_sort_keys."""
+    import torch
+    B = 256
+    n = B * 5 * TILE + 333
+    rng = np.random.default_rng(4242)
+    if dtype == "i32":
+        a = _keys(rng, "uniform", n)
+        a[rng.random(n) < 0.5] = 123_457
+    else:
+        a = _keys64(rng, "uniform", n)
+        a[rng.random(n) < 0.5] = -(1 << 33) + 5
+    t = torch.from_numpy(a).cuda()
+    out = torch.empty_like(t)
+    with gpu_ctx.options(buckets=B):
+        gpu_ctx.sort_dev(t, out)
+        torch.cuda.synchronize()
+        st = gpu_ctx.stats()
+    want = np.sort(a)
+    assert np.array_equal(out.cpu().numpy(), want)
+    assert st["sub_scatter_fallback"] == 0 and st["tile_sort_keys"] < 0.6 * n, st  # pure buckets skipped
+    early = st["tile_sort_keys"] // TILE
+    out.fill_(0)
+    with gpu_ctx.options(buckets=B, test_tile_cap=early + 8):
+        gpu_ctx.sort_dev(t, out)
+        torch.cuda.synchronize()
+        st = gpu_ctx.stats()
+    assert st["sub_scatter_fallback"] == 1, st
+    assert np.array_equal(out.cpu().numpy(), want)

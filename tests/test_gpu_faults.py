@@ -223,11 +223,14 @@ def test_c3_rank_layout_one_rccl_rank_bit_exact(gpu_ctx):
     ctx.gen_uniform(t, SEED, 3 * n)
     ctx.comm_init(1, 0, dsort.Context.unique_id())
     try:
-        with ctx.options(buckets=128):
+        # (the wave fence: this rank's own wave-1 buckets, read in place from the partition buffer,
+        # are fingerprinted across wave 0's second level and tile sort -- round 6)
+        with ctx.options(buckets=128, test_wave_fence=1):
             ptr, nout = ctx.sample_sort_dev(t)
             ctx.synchronize()
         st = ctx.stats()
         assert nout == n and st["exchange_path"] == 1 and st["tile_keys"] == 16384, st
+        assert st["fence_ranges"] == 1, st
         out = torch.empty_like(t)
         ctx.check(ctx.lib.dsort_copy_d2d(ctx.h, ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ptr), 4 * n))
         torch.cuda.synchronize()

@@ -92,11 +92,19 @@ def test_bucket_exchange_bit_exact(tmp_path, world, dtype, dist):
     second level and the tile sort): ranks sharing the GPU over the host transport, the
     concatenated slices equal numpy's sort of the whole input element for element, for uniform,
     globally sorted / reversed (every rank one key range), few distinct keys (pure buckets filled
-    with their key) and Zipf int64 (heavy keys split across ranks)."""
+    with their key) and Zipf int64 (heavy keys split across ranks).
+
+    The host transport runs the waves in RCCL's order (round 6): wave 1's send ranges are staged
+    from the partition buffer after wave 0's second level and tile sort ran on it.  The wave fence
+    (DSORT_OPT_TEST_WAVE_FENCE) also fingerprints every range wave 1 still needs -- its sends, the
+    rank's own wave-1 buckets, its landing zone -- across wave 0, and would fail the sort naming
+    the range wave 0 wrote into."""
     n = world * (1 << 22) + 12_345
-    ins, outs, meta = run_ranks(tmp_path, world, n, dtype, dist)
+    ins, outs, meta = run_ranks(tmp_path, world, n, dtype, dist, opts={"all": {"test_wave_fence": 1}})
     assert ins.size == n
     assert all(m["stats"]["exchange_path"] == 1 for m in meta), [m["stats"]["exchange_path"] for m in meta]
+    # (every rank fenced its non-empty wave-1 ranges: at least its own buckets)
+    assert all(m["stats"]["fence_ranges"] >= 1 for m in meta), [m["stats"]["fence_ranges"] for m in meta]
     assert np.array_equal(np.concatenate(outs), np.sort(ins))
     if dist in ("uniform", "seq", "rev"):
         sizes = [o.size for o in outs]
@@ -110,15 +118,21 @@ def test_small_sample_sort_takes_the_merge_path(tmp_path):
     assert np.array_equal(np.concatenate(outs), np.sort(ins))
 
 
-@pytest.mark.parametrize("n,fail_at", [(3 * (1 << 22) + 12_345, 3), (3 * (1 << 22) + 12_345, 1),
-                                       (3 * (1 << 22) + 12_345, 4), (1_000_003, 3)])
-def test_local_failure_in_the_exchange_fails_every_rank(tmp_path, n, fail_at):
+@pytest.mark.parametrize("n,fail_at,presorted", [(3 * (1 << 22) + 12_345, 3, False), (3 * (1 << 22) + 12_345, 1, False),
+                                                 (3 * (1 << 22) + 12_345, 4, False), (1_000_003, 3, False),
+                                                 (3 * (1 << 22) + 12_345, 0, False), (1_000_003, 0, True),
+                                                 (1_000_003, 1, True)])
+def test_local_failure_in_the_exchange_fails_every_rank(tmp_path, n, fail_at, presorted):
     """A rank failing locally right before a collective of the host-transport sample sort
     (DSORT_OPT_TEST_FAIL_EXCHANGE; 3 = the key all-to-all of the bucket exchange's first wave, 1 =
     the samples, 4 = the second wave; on the merge path below 2^22 keys per rank, 3 = the keys):
     its peers meet the failure at the next status gate and return DSORT_ECOMM naming it, instead of
-    blocking in a collective it never joins (dsort_tx.h; the survivor side of server.c:421-449)."""
-    res = run_ranks(tmp_path, 3, n, opts={"rank_opts": {"1": {"test_fail_exchange": fail_at}}}, expect_fail=True)
+    blocking in a collective it never joins (dsort_tx.h; the survivor side of server.c:421-449).
+    fail_at 0 (round 6): before the very first collective, which now has a gate too --
+    on the bucket exchange (the key counts) and on the presorted fault-recovery entry
+    (dsort_sample_merge_dev, whose first collective is the samples)."""
+    res = run_ranks(tmp_path, 3, n, opts={"rank_opts": {"1": {"test_fail_exchange": fail_at}}, "presorted": presorted},
+                    expect_fail=True)
     assert res[1]["rc"] == -3 and "DSORT_OPT_TEST_FAIL_EXCHANGE" in res[1]["error"], res[1]
     for r in (0, 2):
         assert res[r]["rc"] == -4 and "rank 1 failed locally" in res[r]["error"], res[r]
@@ -133,7 +147,21 @@ def test_bucket_exchange_oversized_subbuckets(tmp_path, world, gather):
     partition buffer, which still holds this rank's second-wave buckets (and, over RCCL, buckets
     still being sent) -- and the output of the later wave was wrong."""
     n = world * (1 << 22) + 12_345
-    ins, outs, meta = run_ranks(tmp_path, world, n, opts={"all": {"sub_gather": gather, "sub_keys": 20_000}})
+    ins, outs, meta = run_ranks(tmp_path, world, n, opts={"all": {"sub_gather": gather, "sub_keys": 20_000,
+                                                                  "test_wave_fence": 1}})
     assert all(m["stats"]["exchange_path"] == 1 for m in meta)
+    assert all(m["stats"]["fence_ranges"] >= 1 for m in meta), [m["stats"]["fence_ranges"] for m in meta]
     assert any(m["stats"]["sub_split_subbuckets"] > 0 for m in meta), [m["stats"] for m in meta]
     assert np.array_equal(np.concatenate(outs), np.sort(ins))
+
+
+def test_wave_fence_catches_a_write_into_wave_1(tmp_path):
+    """The wave fence is not vacuous: with DSORT_OPT_TEST_WAVE_FENCE = 2 rank 0 flips one key of
+    its first fenced wave-1 range between the two fingerprints (as a stray write of wave 0's second
+    level would); its sort fails with DSORT_EHIP naming the range, and rank 1 leaves at the next
+    status gate with DSORT_ECOMM instead of waiting in the second wave."""
+    n = 2 * (1 << 22) + 12_345
+    res = run_ranks(tmp_path, 2, n, opts={"rank_opts": {"0": {"test_wave_fence": 2}}}, expect_fail=True)
+    assert res[0]["rc"] == -3 and "DSORT_OPT_TEST_WAVE_FENCE" in res[0]["error"], res[0]
+    assert "wave-1" in res[0]["error"] or "own wave-1" in res[0]["error"], res[0]
+    assert res[1]["rc"] == -4 and "rank 0 failed locally" in res[1]["error"], res[1]

@@ -4,7 +4,8 @@ Round 4's multi-rank GPU test hung once.  The library's ho
 sample sort runs a fixed sequence of collectives; every one after the first now has a status gate
 in front of it and every wait is bounded by the exchange deadline (csrc/dsort_tx.h).
 tests/tx/tx_harness.cpp runs that very TxSeq/TxGuard code with the bucket exchange's sequence on
-the CPU through the same Python transport the GPU tests use (dsort.torch_dist_transport), and:
+the CPU through the same Python transport the GPU tests use (dsort.torch_dist_transport), and
+(round 6) the first collective has a gate in front of it too:
   * a rank failing locally right before the key all-to-all (or any other collective) makes every
     rank return at once: the failed one its own error, the peers DSORT_ECOMM naming it -- the
     survivor side of server.c:421-449, where a peer's failure surfaces as an error;
@@ -38,7 +39,7 @@ def build_harness():
     return out
 
 
-def _rank(rank, world, store, so, fail_rank, fail_at, hang_ms, timeout_ms, outdir):
+def _rank(rank, world, store, so, fail_rank, fail_at, hang_ms, timeout_ms, outdir, rerun):
     import datetime
 
     import torch.distributed as dist
@@ -60,15 +61,24 @@ def _rank(rank, world, store, so, fail_rank, fail_at, hang_ms, timeout_ms, outdi
     rc = lib.txh_run(ctypes.byref(t), world, rank, 2, fail_rank, fail_at, hang_ms, timeout_ms, msg, len(msg),
                      ctypes.byref(peer), ctypes.byref(ncoll))
     el = time.monotonic() - t0
+    res = {"rc": rc, "msg": msg.value.decode(), "peer": peer.value, "ncoll": ncoll.value, "s": el,
+           "poisoned": getattr(t, "poisoned", None)}
+    if rerun and rank != fail_rank:
+        # a second sequence on the same transport, no failure injected: after a timeout the
+        # transport is poisoned and must refuse at once (a stale gloo op could pair)
+        t0 = time.monotonic()
+        rc2 = lib.txh_run(ctypes.byref(t), world, rank, 2, -1, -1, 0, 20_000, msg, len(msg),
+                          ctypes.byref(peer), ctypes.byref(ncoll))
+        res.update(rc2=rc2, msg2=msg.value.decode(), s2=time.monotonic() - t0)
     with open(os.path.join(outdir, f"rank{rank}.json"), "w") as f:
-        json.dump({"rc": rc, "msg": msg.value.decode(), "peer": peer.value, "ncoll": ncoll.value, "s": el}, f)
+        json.dump(res, f)
     os._exit(0)  # (a timed-out gloo op may still be pending: leave without waiting for it)
 
 
-def run(tmp_path, fail_rank=-1, fail_at=-1, hang_ms=0, timeout_ms=20_000, world=3):
+def run(tmp_path, fail_rank=-1, fail_at=-1, hang_ms=0, timeout_ms=20_000, world=3, rerun=False):
     so = build_harness()
-    mp.spawn(_rank, args=(world, str(tmp_path / "store"), so, fail_rank, fail_at, hang_ms, timeout_ms, str(tmp_path)),
-             nprocs=world, join=True)
+    mp.spawn(_rank, args=(world, str(tmp_path / "store"), so, fail_rank, fail_at, hang_ms, timeout_ms, str(tmp_path),
+                          rerun), nprocs=world, join=True)
     return [json.load(open(tmp_path / f"rank{r}.json")) for r in range(world)]
 
 
@@ -77,8 +87,9 @@ def test_sequence_runs_clean(tmp_path):
     assert all(r["rc"] == 0 and r["ncoll"] == 5 for r in res), res
 
 
-# collective 3 = the key all-to-all of wave 0 (0 counts, 1 samples, 2 bucket starts, 4 wave 1)
-@pytest.mark.parametrize("fail_at", [3, 1, 4])
+# collective 3 = the key all-to-all of wave 0 (0 counts, 1 samples, 2 bucket starts, 4 wave 1);
+# 0 = before the very first collective (the presorted entry's staging failing)
+@pytest.mark.parametrize("fail_at", [3, 0, 1, 4])
 def test_local_failure_fails_every_rank_at_the_next_gate(tmp_path, fail_at):
     res = run(tmp_path, fail_rank=1, fail_at=fail_at)
     assert res[1]["rc"] == EHIP and "injected" in res[1]["msg"], res[1]
@@ -95,3 +106,12 @@ def test_hung_rank_times_out_its_peers_at_the_deadline(tmp_path):
         assert res[r]["rc"] == ETIMEOUT, res[r]
         assert res[r]["s"] < 5, res[r]  # the 1.5 s deadline, not gloo's 30 s timeout
     assert res[1]["rc"] in (ETIMEOUT, ECOMM), res[1]  # woke up past the deadline
+
+
+def test_transport_is_poisoned_after_a_timeout(tmp_path):
+    res = run(tmp_path, fail_rank=1, fail_at=3, hang_ms=6000, timeout_ms=1500, rerun=True)
+    for r in (0, 2):
+        assert res[r]["rc"] == ETIMEOUT and res[r]["poisoned"], res[r]
+        # the next sort on the same group fails at its first gate, without touching gloo
+        assert res[r]["rc2"] == ECOMM and "callback returned -4" in res[r]["msg2"], res[r]
+        assert res[r]["s2"] < 1.0, res[r]

@@ -4,9 +4,9 @@
 // check over gloo (world size 3, no GPU) that a rank failing locally -- or hanging -- between two
 // collectives makes every rank return within the exchange deadline instead of blocking.
 //
-// The sequence is sample_sort + sample_sort_bx's (dsort_api.hip) on the host transport: key-count
-// all-gather, then [gate] sample all-gather, [gate] bucket-start all-gather, [gate] key all-to-all
-// of wave 0, [gate] wave 1.
+// The sequence is sample_sort + sample_sort_bx's (dsort_api.hip) on the host transport: [gate]
+// key-count all-gather, [gate] sample all-gather, [gate] bucket-start all-gather, [gate] key
+// all-to-all of wave 0, [gate] wave 1.
 #include <stdint.h>
 #include <string.h>
 #include <unistd.h>
