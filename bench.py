@@ -705,7 +705,9 @@ LEG_NAMES = ("c3", "c4", "c5")
 
 def leg_plan(world):
     c3_keys = 1 << 32 if world == 8 else (1 << 29) * world
-    return {"c3": {"keys": c3_keys, "dtype": "i32", "dist": "uniform"},
+    # (C3's bucket geometry at any N: 1024 global buckets over 8 ranks = 128 buckets of 4M keys per
+    # rank; below 8 GPUs the same 128 per rank are forced -- DSORT_OPT_BUCKETS is the global count)
+    return {"c3": {"keys": c3_keys, "dtype": "i32", "dist": "uniform", "buckets": 128 * world},
             "c4": {"keys": 1 << 30, "dtype": "i64", "dist": "zipf"},
             # (one GPU: two workers sharing it over the master's relay, a plumbing check at 2^26 keys)
             "c5": ({"keys": c3_keys, "workers": world, "kill_rank": min(3, world - 1), "transport": "rccl"}
@@ -752,6 +754,7 @@ def run_c5_leg(spec, dtype="i32", timeout_s=900):
     if p.returncode != 0 or not lines:
         return {"config": "C5", "verified": False, "error": f"rc {p.returncode}: {(p.stderr or p.stdout)[-600:]}"}
     r = json.loads(lines[-1])
+    r["workload_config"] = r.pop("config", None)
     r.update({"config": "C5", "wall_s": round(time.perf_counter() - t0, 1), "transport": spec["transport"]})
     return r
 
@@ -783,10 +786,12 @@ def run_multi(args, rank, world):
             continue
         spec = plan[name]
         ctx.set_option("comm_timeout_ms", int(args.leg_timeout * 1000))  # (a stuck exchange ends the leg)
+        ctx.set_option("buckets", spec.get("buckets", -1))
         t0 = time.perf_counter()
         res = measure_samplesort(ctx, dist, rank, world, spec["keys"], spec["dtype"], spec["dist"], 3, 1, strict=False)
+        ctx.set_option("buckets", -1)
         legs[name] = leg_summary(name, spec, world, 3, res)
-        legs[name]["wall_s"] = round(time.perf_counter() - t0, 1)
+        legs[name]["wall_s"] = round(time.perf_counter() - t0, 2)
         if res[4]:  # (the communicator may be gone: no further sort leg)
             break
     ctx.set_option("comm_timeout_ms", 0)

@@ -109,7 +109,8 @@ def test_multi_line_carries_c3_c4_c5_legs(capsys):
 
     world = 8
     plan = bench.leg_plan(world)
-    assert plan["c3"]["keys"] == 1 << 32 and plan["c4"] == {"keys": 1 << 30, "dtype": "i64", "dist": "zipf"}
+    assert plan["c3"]["keys"] == 1 << 32 and plan["c3"]["buckets"] == 1024
+    assert plan["c4"] == {"keys": 1 << 30, "dtype": "i64", "dist": "zipf"}
     assert plan["c5"]["kill_rank"] == 3 and plan["c5"]["workers"] == 8 and plan["c5"]["transport"] == "rccl"
     assert bench.leg_plan(2)["c3"]["keys"] == 1 << 30 and bench.leg_plan(2)["c5"]["kill_rank"] == 1
     assert bench.leg_plan(1)["c5"]["transport"] == "relay"  # (one GPU: two workers share it)
