@@ -2212,7 +2212,7 @@ static int bk_layout(dsort_ctx *ctx, uint64_t n, int B, size_t smp_bytes, BkLayo
     const size_t o_smp = take(smp_bytes), o_spl = take((size_t)L.BP * sizeof(C)), o_cnt = take((size_t)L.G * B * 4),
                  o_part = take((size_t)L.nchunk * B * 8), o_offs = take((size_t)L.G * B * 4),
                  o_bst = take((size_t)(B + 1) * 8), o_tt = take((size_t)L.tmax * sizeof(TileRef)), o_nt = take(4),
-                 o_map = take(BK_MAP_BYTES), o_ids = take(BkIds<T>::ON ? (size_t)L.G * L.subs * BK_T * Geo<T>::KPT * 2 : 0);
+                 o_map = take(sizeof(BkMap)), o_ids = take(BkIds<T>::ON ? (size_t)L.G * L.subs * BK_T * Geo<T>::KPT * 2 : 0);
     int rc = ensure(ctx, &ctx->bucket, &ctx->bucket_bytes, off, "bucket partition");
     if (rc) return rc;
     char *a = static_cast<char *>(ctx->bucket);
@@ -2335,7 +2335,7 @@ static int first_level(dsort_ctx *ctx, const T *d_in, uint64_t n, uint64_t ioff,
     fault_point(ctx, s, 0);  // first-level partition done
     if (int rc_ = sync_event(ctx, ctx->bucket_ev, "bucket starts")) return rc_;
     if (hb[B] != n) return set_err(ctx, DSORT_EHIP, "bucket partition lost keys");
-    ctx->stats.first_level_map = !Comp<T>::ADAPT && !ad ? (RB && hm->r2s ? 3 : 0) : hm->mode == 0 ? 1 : 2;
+    ctx->stats.first_level_map = !Comp<T>::ADAPT && !ad ? 0 : hm->mode == 0 ? 1 : 2;
     return DSORT_OK;
 }
 
