@@ -155,7 +155,33 @@ struct BkMap {
                     // top-11-bit slots, when those crowd many splitters of several keys into one slot
                     // (many small keys: the reference's input.txt holds only 1..100).  The host reads
                     // it back and launches the kernels' adaptive instances (first_level)
+    // int32 on the fixed map (round 6): ONE refined slot -- the most crowded slot of splitters of
+    // several keys, when neither adaptive map thins it (keys of [1, 100] mixed half and half with
+    // uniform ones: every map puts the small keys in one slot) -- gets a second table of BK_R2
+    // sub-slots, linear over its splitters' key range (BkRefine); its keys look their bucket up
+    // there instead of searching the slot's splitters.  r2s = the slot + 1 (0: none).
+    uint32_t r2s;
+    uint32_t r2lo;  // flipped key one below the refined slot's first splitter's (or the slot's start)
+    uint32_t r2sh;  // sub-slot = (flipped key - r2lo) >> r2sh, clamped to [0, BK_R2)
 };
+// The refined slot's table follows the map (bucket_slotmap_kernel writes both): entry i = the
+// splitters below sub-slot i (bits 0-13), "key implied" (bit 14: the sub-slot holds one key value),
+// one-key flag (bit 15: its >= 2 splitters hold one key K), the splitters below sub-slot i + 1 (bits
+// 16-31).  Sub-slot 0 reaches down to the slot's start, the last up to its end.  256 entries: the
+// scatter keeps them in LDS (1 KiB is what its LDS has left) -- from global memory, the classify of a
+// 2^30-key sort of [1, 100] keys mixed with uniform ones waited 20 K cycles per batch of 4 keys.
+constexpr int BK_R2 = 256;
+constexpr int BK_R2_BITS = 8;
+constexpr uint32_t BK_R2_IMPLIED = 0x4000u;
+constexpr size_t BK_MAP_BYTES = 64 + 4 * BK_R2;
+static_assert(sizeof(BkMap) <= 64, "the refined table sits 64 bytes into the map");
+__host__ __device__ __forceinline__ const uint32_t *bk_tab2(const BkMap *m) {
+    return reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(m) + 64);
+}
+// the packed (scatter) entry of the refined slot: two or more splitters, count field all ones
+constexpr uint32_t BK_PACKED_R2 = 0xFFFFFu;
+// the non-packed (histogram) entry's flag of the refined slot
+constexpr uint32_t BK_R2_FLAG = 0x4000u;
 
 // The splitters say whether a wave's consecutive keys will mostly share a bucket: the input is
 // sorted or reversed when the splitters' input indices run (nearly) monotone with their order, and
@@ -279,11 +305,13 @@ __device__ __forceinline__ void build_slots(const typename Comp<T>::C *spl, int 
             const uint32_t in = cnt[1] - cnt[0];
             const uint32_t kb = in == 1 ? ((uint32_t)CT::key_of(spl[cnt[0]]) ^ 0x80000000u) << 11 >> 12 : in;
             const bool one = in >= 2 && CT::key_of(spl[cnt[0]]) == CT::key_of(spl[cnt[1] - 1]);
-            rng[i] = cnt[0] | (one ? 3u : in > 2 ? 2u : in) << 10 | kb << 12;
+            rng[i] = m.r2s == (uint32_t)i + 1 ? cnt[0] | 2u << 10 | BK_PACKED_R2 << 12
+                                              : cnt[0] | (one ? 3u : in > 2 ? 2u : in) << 10 | kb << 12;
         } else {
             // a slot whose (>= 2) splitters all hold one key K: see bucket_fast
             const bool one = cnt[1] >= cnt[0] + 2 && CT::key_of(spl[cnt[0]]) == CT::key_of(spl[cnt[1] - 1]);
-            rng[i] = cnt[0] | (uint32_t)one << 15 | (cnt[1] << 16);
+            const bool r2 = !ADP && m.r2s == (uint32_t)i + 1;
+            rng[i] = cnt[0] | (r2 ? BK_R2_FLAG : (uint32_t)one << 15) | (cnt[1] << 16);
         }
     }
 }
@@ -305,9 +333,8 @@ __device__ __forceinline__ void build_slots(const typename Comp<T>::C *spl, int 
 // them (their number is in the entry).  (Round 2 read the splitter for every key of a slot
 // that had one: half of the keys, a dependent 8-byte LDS read on the way to the rank atomic.)
 template <typename T>
-__device__ __forceinline__ int bucket_onekey(const typename Comp<T>::C *spl, int lo, int hi, T key,
-                                             const typename Comp<T>::C &c) {
-    const typename Comp<T>::C a = spl[lo], z = spl[hi - 1];
+__device__ __forceinline__ int onekey_ab(const typename Comp<T>::C &a, const typename Comp<T>::C &z, int lo, int hi,
+                                         T key, const typename Comp<T>::C &c) {
     const T K = Comp<T>::key_of(a);
     const uint32_t i = Comp<T>::idx_of(c), ia = Comp<T>::idx_of(a), iz = Comp<T>::idx_of(z);
     if (key != K || i <= ia) return key <= K ? lo : hi;
@@ -318,6 +345,56 @@ __device__ __forceinline__ int bucket_onekey(const typename Comp<T>::C *spl, int
     const int j = (int)q;
     return lo + 1 + (j < hi - lo - 2 ? j : hi - lo - 2);
 }
+template <typename T>
+__device__ __forceinline__ int bucket_onekey(const typename Comp<T>::C *spl, int lo, int hi, T key,
+                                             const typename Comp<T>::C &c) {
+    return onekey_ab<T>(spl[lo], spl[hi - 1], lo, hi, key, c);
+}
+// The refined slot (BkMap.r2s, int32 on the fixed map): the key's sub-slot entry, then
+//  - a one-key sub-slot (its splitters all hold K): a key other than K lies below or above all of
+//    them; the copies of K go to the buckets strictly between K's first and last splitter (each
+//    holds only K, so any of them keeps the order), spread by a hash of the index.  (The first
+//    level's one-key slots split K's copies by index range instead, which needs K's first and last
+//    splitter -- two more reads -- and piles a workgroup's copies onto one counter.)  When the
+//    sub-slot is one key value (key implied), no splitter is read at all;
+//  - else a search among the sub-slot's splitters (none to a few)
+// -- instead of a search over the whole slot's (e.g. ~500 splitters of 100 small keys, from global
+// memory in the scatter).  Histogram and scatter pick alike, key for key.
+__device__ __forceinline__ uint32_t refine_sub(uint32_t r2lo, uint32_t r2sh, int32_t key) {
+    const uint32_t u = (uint32_t)key ^ 0x80000000u;
+    const uint32_t d = (u < r2lo ? 0u : u - r2lo) >> r2sh;
+    return d < (uint32_t)BK_R2 ? d : (uint32_t)BK_R2 - 1;
+}
+// the inner bucket of a copy of K at composite index idx (hi - lo >= 2)
+__device__ __forceinline__ int refine_inner(int lo, int hi, uint32_t idx) {
+    return lo + 1 + (int)__umulhi(idx * 2654435761u, (uint32_t)(hi - lo - 1));
+}
+// e: the sub-slot entry; kk: the key of the sub-slot's first splitter when not implied (one-key)
+template <typename T>
+__device__ __forceinline__ int refine_pick(const typename Comp<T>::C *spl, uint32_t e, T key,
+                                           const typename Comp<T>::C &c) {
+    int lo = (int)(e & 0x3FFF), hi = (int)(e >> 16);
+    if (e & 0x8000) {
+        if (!(e & BK_R2_IMPLIED)) {
+            const T K = Comp<T>::key_of(spl[lo]);
+            if (key != K) return key < K ? lo : hi;
+        }
+        return refine_inner(lo, hi, Comp<T>::idx_of(c));
+    }
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (Comp<T>::lt(spl[mid], c)) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+__device__ __forceinline__ bool packed_refined(uint32_t r) { return ((r >> 10) & 3) == 2 && (r >> 12) == BK_PACKED_R2; }
+// A slow key's splitters as a slot entry (lo | one-key << 15 | hi << 16), from its packed entry
+__device__ __forceinline__ uint32_t packed_range(uint32_t r) {
+    const uint32_t lo = r & 1023, in = (r >> 10) & 3, sb = r >> 12;
+    return lo | (in == 3 ? 0x8000u : 0u) | (lo + (in == 1 ? 1u : sb)) << 16;
+}
+
 // The packed int32 entry (bucket_fast's first branch) split in two, for a classify that keeps
 // several keys' table reads in flight: the fast result and whether the key needs the slow path
 // (a slot of two or more splitters, or a key equal to the slot's splitter in bits 31..1).
@@ -330,7 +407,7 @@ __device__ __forceinline__ int packed_fast(uint32_t r, int32_t key, bool &slow) 
 }
 __device__ __forceinline__ int packed_slow(const int64_t *spl, uint32_t r, int32_t key, int64_t c) {
     int lo = (int)(r & 1023);
-    const uint32_t in = (r >> 10) & 3, sb = r >> 12;
+    const uint32_t in = (r >> 10) & 3, sb = r >> 12;  // (the refined slot is the caller's: packed_refined)
     int hi = lo + (in == 1 ? 1 : (int)sb);
     if (in == 3) return bucket_onekey<int32_t>(spl, lo, hi, key, c);
     while (lo < hi) {
@@ -345,9 +422,11 @@ __device__ __forceinline__ int packed_slow(const int64_t *spl, uint32_t r, int32
 // splitters of one key in a slot, and every key searched them (2^30: histogram 4.96 ms, scatter
 // 9.0 ms).  The packed entry marks them with splitter count field 3.
 // ONE = false: the caller knows the table has no one-key slot (BkMap.one).
+// tab2 / m: the refined slot's table and the map (int32 on the fixed map; see BkMap.r2s)
 template <typename T, bool PACK, bool ONE = true, bool ADP = Comp<T>::ADAPT>
 __device__ __forceinline__ int bucket_fast(const typename Comp<T>::C *spl, const uint32_t *rng, uint32_t slot,
-                                           T key, const typename Comp<T>::C &c) {
+                                           T key, const typename Comp<T>::C &c, const uint32_t *tab2 = nullptr,
+                                           const BkMap *m = nullptr) {
     const uint32_t r = rng[slot];
     if constexpr (!ADP && PACK) {
         // branch-free on the usual path; the rare keys that search take one wave-uniform branch
@@ -359,6 +438,8 @@ __device__ __forceinline__ int bucket_fast(const typename Comp<T>::C *spl, const
         const bool slow = in > 1 || (in == 1 && kb == sb);
         if (__builtin_expect(__ballot(slow) == 0, 1)) return j;
         if (!slow) return j;
+        if (tab2 && sb == BK_PACKED_R2 && in == 2)
+            return refine_pick<T>(spl, tab2[refine_sub(m->r2lo, m->r2sh, (int32_t)key)], key, c);
         int hi = lo + (in == 1 ? 1 : (int)sb);  // (the splitters searched: those of the slot)
         if (in == 3) return bucket_onekey<T>(spl, lo, hi, key, c);
         while (lo < hi) {
@@ -368,7 +449,11 @@ __device__ __forceinline__ int bucket_fast(const typename Comp<T>::C *spl, const
         }
         return lo;
     }
-    int lo = (int)(r & 0x7FFF), hi = (int)(r >> 16);
+    if constexpr (!ADP) {
+        if (ONE && tab2 && (r & BK_R2_FLAG))
+            return refine_pick<T>(spl, tab2[refine_sub(m->r2lo, m->r2sh, (int32_t)key)], key, c);
+    }
+    int lo = (int)(r & 0x3FFF), hi = (int)(r >> 16);
     if (ONE && (r & 0x8000)) return bucket_onekey<T>(spl, lo, hi, key, c);
     while (lo < hi) {  // lower bound among the splitters of the slot
         const int mid = (lo + hi) >> 1;
@@ -436,14 +521,103 @@ __global__ void __launch_bounds__(BK_MAXB) bucket_slotmap_kernel(const typename 
         for (int i = j; i < 3 * BK_SLOTS; i += blockDim.x)
             if (dst[i / BK_SLOTS][i % BK_SLOTS] >= 2) atomicMax(&cost[i / BK_SLOTS], tot[i / BK_SLOTS][i % BK_SLOTS]);
         __syncthreads();
+        // the fixed map kept although its most crowded slot of several keys holds more than AD_MIX
+        // splitters: that slot (the lowest of the most crowded) is refined (BkMap.r2s)
+        // -- unless an adaptive map thins every slot to AD_MIX (e.g. all keys in [1, 100]): the choice
+        // is the lower of the adaptive maps' cost and the fixed map's cost without the refined slot
+        __shared__ uint32_t r2slot, cost2;
+        __shared__ BkMap rm;
         if (j == 0) {
-            const int q = cost[0] <= AD_MIX ? 0 : cost[2] < cost[1] ? 2 : 1;
-            BkMap r = q == 0 || cost[q] < cost[0] ? am[q] : am[0];
+            r2slot = ~0u;
+            cost2 = 0;
+        }
+        __syncthreads();
+        const int qa = cost[2] < cost[1] ? 2 : 1;  // the better adaptive map
+        if (cost[0] > AD_MIX && cost[qa] > AD_MIX)
+            for (int i = j; i < BK_SLOTS; i += blockDim.x)
+                if (dst[0][i] >= 2 && tot[0][i] == cost[0]) atomicMin(&r2slot, (uint32_t)i);
+        __syncthreads();
+        if (r2slot != ~0u)
+            for (int i = j; i < BK_SLOTS; i += blockDim.x)
+                if ((uint32_t)i != r2slot && dst[0][i] >= 2) atomicMax(&cost2, tot[0][i]);
+        __syncthreads();
+        const bool refine = r2slot != ~0u && cost2 <= cost[qa];
+        const bool fixed = cost[0] <= AD_MIX || refine;
+        if (j == 0) {
+            if (!refine) r2slot = ~0u;
+            BkMap r = fixed ? am[0] : am[qa];
             r.ad = r.ulo != 0 || r.mode != 0 || r.sh != (uint32_t)(CT::KB - BK_SLOTB) ? 1u : 0u;
             r.ids = BkIds<T>::ON ? 1u : 0u;  // (int32 with DSORT_BK_IDS32: always)
             r.hot = bucket_runs_hint<T>(nasc, ndup, nsp);
             r.one = r.ad ? 1u : (ndup != 0);
+            r.r2s = r.r2lo = r.r2sh = 0;
+            if (r2slot != ~0u) {
+                // the slot's splitters [a, z): sub-slots linear over their key range
+                uint32_t a = 0, z = 0;
+                for (int k = 0; k < nsp; ++k) {
+                    const uint32_t sk = slot_mode<T, BK_SLOTB, 0, false>(am[0], CT::key_of(spl[k]));
+                    a += sk < r2slot;
+                    z += sk <= r2slot;
+                }
+                // (sub-slot 0 below the first splitter's key when the slot starts lower: then sub-slot
+                // 1 is that key, and with r2sh = 0 every inner sub-slot is one key value)
+                uint64_t us0 = 0;
+                (void)slot_first<T, BK_SLOTB>(am[0], r2slot, us0);
+                // (the top 1/32 of the slot's splitters left out of the range: a stray splitter far
+                // above the crowd -- a uniform key in the small keys' slot -- would widen every
+                // sub-slot; keys above the range take the last sub-slot, which searches)
+                const uint32_t k0 = CT::flip(CT::key_of(spl[a])), hi = CT::flip(CT::key_of(spl[z - 1 - (z - a) / 32]));
+                const uint32_t lo = r2slot > 0 && k0 > (uint32_t)us0 ? k0 - 1 : k0;
+                const uint32_t rr = hi - lo;
+                const int bits = rr == 0 ? 0 : 32 - __builtin_clz(rr);
+                r.r2s = r2slot + 1;
+                r.r2lo = lo;
+                r.r2sh = (uint32_t)(bits > BK_R2_BITS ? bits - BK_R2_BITS : 0);
+                r.one = 1;  // (the histogram's loop with the one-key and refined checks)
+                static_assert(BK_R2 == 1 << BK_R2_BITS, "sub-slots");
+            }
+            rm = r;
             *out = r;
+        }
+        __syncthreads();
+        if (rm.r2s) {
+            // sub-slot i: the splitters below its start (sub-slot 0 from the slot's start, a sub-slot
+            // past the slot's end empty at its end), one-key flag as in a slot entry
+            uint32_t *tab = const_cast<uint32_t *>(bk_tab2(out));
+            const uint32_t s2 = rm.r2s - 1;
+            uint64_t us = 0, ue = 0;
+            const bool has_next = s2 + 1 < (uint32_t)BK_SLOTS && slot_first<T, BK_SLOTB>(am[0], s2 + 1, ue);
+            (void)slot_first<T, BK_SLOTB>(am[0], s2, us);  // (the fixed map: slot s2's first flipped key)
+            const int BPl = 1 << (32 - __builtin_clz((uint32_t)(nsp > 0 ? nsp : 1)));  // (a power of two >= nsp)
+            auto below = [&](uint64_t u) -> uint32_t {  // splitters with composite < (flipped key u, index 0)
+                const typename CT::C cc = CT::slot_start(u);
+                uint32_t lo = 0, hi = (uint32_t)nsp;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (CT::lt(spl[mid], cc)) lo = mid + 1;
+                    else hi = mid;
+                }
+                return lo;
+            };
+            (void)BPl;
+            const uint32_t c_lo = s2 == 0 ? 0u : below(us), c_hi = has_next ? below(ue) : (uint32_t)nsp;
+            for (int i = j; i < BK_R2; i += blockDim.x) {
+                uint32_t c0 = c_lo, c1 = c_hi;
+                if (i > 0) {
+                    const uint64_t u = (uint64_t)rm.r2lo + ((uint64_t)i << rm.r2sh);
+                    c0 = has_next && u >= ue ? c_hi : (u > 0xFFFFFFFFull ? c_hi : below(u));
+                }
+                if (i + 1 < BK_R2) {
+                    const uint64_t u = (uint64_t)rm.r2lo + ((uint64_t)(i + 1) << rm.r2sh);
+                    c1 = has_next && u >= ue ? c_hi : (u > 0xFFFFFFFFull ? c_hi : below(u));
+                }
+                c0 = c0 < c_lo ? c_lo : c0;
+                const bool one = c1 >= c0 + 2 && CT::key_of(spl[c0]) == CT::key_of(spl[c1 - 1]);
+                // (one key value: sub-slots 1 .. BK_R2 - 2 of a unit-width table; the outer ones take
+                // every key below / above)
+                const bool implied = rm.r2sh == 0 && i > 0 && i + 1 < BK_R2;
+                tab[i] = c0 | (implied ? BK_R2_IMPLIED : 0u) | (uint32_t)one << 15 | c1 << 16;
+            }
         }
         return;
     }
@@ -612,8 +786,11 @@ __global__ void __launch_bounds__(BK_T, 2) bucket_hist_kernel(const T *__restric
     const BkMap m = *map;
     if (!ADP && m.ad) return;  // (int32: the adaptive map's instance counts this sort, first_level)
     __shared__ uint32_t hist[BK_MAXB];
+    __shared__ uint32_t tab2[ADP ? 1 : BK_R2];  // (the refined slot's table, BkMap.r2s)
     load_splitters<T>(spl_g, BP, spl);
     for (int b = threadIdx.x; b < B; b += BK_T) hist[b] = 0;
+    if (!ADP && m.r2s)
+        for (int i = threadIdx.x; i < BK_R2; i += BK_T) tab2[i] = bk_tab2(map)[i];
     __syncthreads();
     build_slots<T, false, BK_SLOTB, ADP>(spl, BP, m, rng);  // (the packed table measured 0.78 -> 0.93 ms here)
     __syncthreads();
@@ -637,7 +814,7 @@ __global__ void __launch_bounds__(BK_T, 2) bucket_hist_kernel(const T *__restric
             for (int k = 0; k < KPT; ++k) {
                 const uint64_t i = b0 + (uint64_t)k * BK_T;
                 const uint32_t sl = m.mode == 0 ? slot_mode<T, BK_SLOTB, 0, ADP>(m, key[k]) : slot_mode<T, BK_SLOTB, 1, ADP>(m, key[k]);
-                const int b = bucket_fast<T, false, true, ADP>(spl, rng, sl, key[k], CT::make(key[k], i + ioff));
+                const int b = bucket_fast<T, false, true, ADP>(spl, rng, sl, key[k], CT::make(key[k], i + ioff), tab2, &m);
                 bucket_bump<false>(hist, b, i < n);
                 if (i < n) idw[k / 2] |= (uint32_t)b << (16 * (k & 1));
             }
@@ -658,7 +835,7 @@ __global__ void __launch_bounds__(BK_T, 2) bucket_hist_kernel(const T *__restric
                 const uint64_t i = b0 + (uint64_t)k * BK_T;
                 const uint32_t sl = slot_mode<T, BK_SLOTB, 1, ADP>(m, key[k]);
                 if (i < n) {
-                    const int b = bucket_fast<T, false, true, ADP>(spl, rng, sl, key[k], CT::make(key[k], i + ioff));
+                    const int b = bucket_fast<T, false, true, ADP>(spl, rng, sl, key[k], CT::make(key[k], i + ioff), tab2, &m);
                     atomicAdd(&hist[b], 1u);
                     idw[k / 2] |= (uint32_t)b << (16 * (k & 1));
                 }
@@ -900,11 +1077,16 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
         }
     }
     const BkMap m = *map;
+    // (the refined slot's table, BkMap.r2s: in the LDS the scatter has left)
+    __shared__ uint32_t tab2s[ADP || IDS ? 1 : BK_R2];
+    const uint32_t *tab2 = ADP || IDS ? nullptr : tab2s;
 #ifndef DSORT_IDS_ONLY
     if (BkIds<T>::ON && (m.ids != 0) != IDS) return;  // (workgroup-uniform: the other variant's sort)
 #endif
     if (!IDS) {
         load_splitters<T>(spl_g, BP, spl);
+        if (!ADP && m.r2s)
+            for (int i = tb; i < BK_R2; i += BK_T) tab2s[i] = bk_tab2(map)[i];
         __syncthreads();
         build_slots<T, true, BK_SLOTB, ADP>(spl, BP, m, rng);
     }
@@ -947,6 +1129,7 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
                 for (int w = 0; w < KPT / 2; ++w) nid[w] = ids[(s0 + SUB) / 2 + (uint64_t)tb * (KPT / 2) + w];
             }
         }
+        BKST(6);  // (the sub-tile's keys in, their slots)
 #ifndef DSORT_HOT_SCATTER
 #define DSORT_HOT_SCATTER 1
 #endif
@@ -959,7 +1142,7 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
             for (int k = 0; k < KPT; ++k) {
                 const uint64_t i = s0 + tb + (uint64_t)k * BK_T;
                 const bool act = i < n;
-                const int b = IDS ? (int)sl[k] : bucket_fast<T, true, true, ADP>(spl_look, rng, sl[k], key[k], CT::make(key[k], i + ioff));
+                const int b = IDS ? (int)sl[k] : bucket_fast<T, true, true, ADP>(spl_look, rng, sl[k], key[k], CT::make(key[k], i + ioff), tab2, &m);
                 const bool a = act && !dropped(b);
                 const uint32_t r = bucket_bump<true>(hist, b, a);
                 pk[k] = a ? r | (uint32_t)b << 16 : ~0u;
@@ -991,9 +1174,16 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
                 if (__builtin_expect(__ballot(any) != 0, 0)) {
 #pragma unroll
                     for (int g = 0; g < CB; ++g)
-                        if (sw[g])
-                            b[g] = packed_slow(reinterpret_cast<const int64_t *>(spl_look), r[g], (int32_t)key[k0 + g],
-                                               (int64_t)CT::make(key[k0 + g], s0 + tb + (uint64_t)(k0 + g) * BK_T + ioff));
+                        if (sw[g]) {
+                            const int64_t cg = (int64_t)CT::make(key[k0 + g], s0 + tb + (uint64_t)(k0 + g) * BK_T + ioff);
+                            // (the refined slot, BkMap.r2s: its sub-slot entry from LDS -- a one-key sub-slot of
+                            // one key value resolves without a splitter read)
+                            b[g] = m.r2s && packed_refined(r[g])
+                                       ? refine_pick<int32_t>(reinterpret_cast<const int64_t *>(spl_look),
+                                                              tab2[refine_sub(m.r2lo, m.r2sh, (int32_t)key[k0 + g])],
+                                                              (int32_t)key[k0 + g], cg)
+                                       : packed_slow(reinterpret_cast<const int64_t *>(spl_look), r[g], (int32_t)key[k0 + g], cg);
+                        }
                 }
                 if (anyp) {
 #pragma unroll
@@ -1012,12 +1202,13 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
                 const uint64_t i = s0 + tb + (uint64_t)k * BK_T;
                 pk[k] = ~0u;
                 if (i < n) {
-                    const int b = IDS ? (int)sl[k] : bucket_fast<T, true, true, ADP>(spl_look, rng, sl[k], key[k], CT::make(key[k], i + ioff));
+                    const int b = IDS ? (int)sl[k] : bucket_fast<T, true, true, ADP>(spl_look, rng, sl[k], key[k], CT::make(key[k], i + ioff), tab2, &m);
                     if (!dropped(b)) pk[k] = atomicAdd(&hist[b], 1u) | (uint32_t)b << 16;
                 }
             }
           }
         }
+        BKST(7);  // (classify + rank)
         __syncthreads();  // A
         BKST(0);
         // owner: new keys, whole lines to write, entries carried to the next sub-tile

@@ -48,6 +48,8 @@
 
 #include "dsort_bucket.h"
 #include "dsort_internal.h"
+
+#include <rocprofiler-sdk-roctx/roctx.h>
 #include "dsort_part.h"
 #include "dsort_sub.h"
 
@@ -1499,7 +1501,22 @@ static std::vector<int> plan_passes(const dsort_opts &opt, uint64_t runs) {
 // Stage event i of a timed sort (dsort_internal.h: ctx->ev): 7 / 8 around the tile sort kernel
 // (dsort_stats.tile_sort_kernel_ms, partition_ms), 9 / 10 the first-level histogram, 11 / 12 the
 // first-level scatter, 13 / 14 the second-level partition.
+// Every stage boundary of the outermost sort also opens / closes a roctx range on the host thread
+// (rocprofv3 --marker-trace shows when each stage was enqueued; the device times are the events'):
+// dsort:histogram, dsort:scatter, dsort:second-level, dsort:tile-sort.
+static void stage_range(const dsort_ctx *ctx, int i) {
+    if (ctx->nested) return;
+    switch (i) {
+        case 9: roctxRangePushA("dsort:histogram"); break;
+        case 11: roctxRangePushA("dsort:scatter"); break;
+        case 13: roctxRangePushA("dsort:second-level"); break;
+        case 7: roctxRangePushA("dsort:tile-sort"); break;
+        case 10: case 12: case 14: case 8: roctxRangePop(); break;
+        default: break;
+    }
+}
 static int stage_event(dsort_ctx *ctx, hipStream_t s, bool timed, int i) {
+    if (timed) stage_range(ctx, i);
     if (!timed || !ctx->ev_ok) return DSORT_OK;
     if (i == 1 || i == 7 || i == 8 || i == 13 || i == 14) i += ctx->ev_off;
     DSORT_HIP(ctx, hipEventRecord(ctx->ev[i], s));
@@ -2212,7 +2229,7 @@ static int bk_layout(dsort_ctx *ctx, uint64_t n, int B, size_t smp_bytes, BkLayo
     const size_t o_smp = take(smp_bytes), o_spl = take((size_t)L.BP * sizeof(C)), o_cnt = take((size_t)L.G * B * 4),
                  o_part = take((size_t)L.nchunk * B * 8), o_offs = take((size_t)L.G * B * 4),
                  o_bst = take((size_t)(B + 1) * 8), o_tt = take((size_t)L.tmax * sizeof(TileRef)), o_nt = take(4),
-                 o_map = take(sizeof(BkMap)), o_ids = take(BkIds<T>::ON ? (size_t)L.G * L.subs * BK_T * Geo<T>::KPT * 2 : 0);
+                 o_map = take(BK_MAP_BYTES), o_ids = take(BkIds<T>::ON ? (size_t)L.G * L.subs * BK_T * Geo<T>::KPT * 2 : 0);
     int rc = ensure(ctx, &ctx->bucket, &ctx->bucket_bytes, off, "bucket partition");
     if (rc) return rc;
     char *a = static_cast<char *>(ctx->bucket);
@@ -2335,7 +2352,7 @@ static int first_level(dsort_ctx *ctx, const T *d_in, uint64_t n, uint64_t ioff,
     fault_point(ctx, s, 0);  // first-level partition done
     if (int rc_ = sync_event(ctx, ctx->bucket_ev, "bucket starts")) return rc_;
     if (hb[B] != n) return set_err(ctx, DSORT_EHIP, "bucket partition lost keys");
-    ctx->stats.first_level_map = !Comp<T>::ADAPT && !ad ? 0 : hm->mode == 0 ? 1 : 2;
+    ctx->stats.first_level_map = !Comp<T>::ADAPT && !ad ? (RB && hm->r2s ? 3 : 0) : hm->mode == 0 ? 1 : 2;
     return DSORT_OK;
 }
 

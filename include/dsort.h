@@ -90,7 +90,9 @@ typedef struct dsort_stats {
     int first_level_map;      /* slot map of the last bucketed sort's first partition level: 0 the fixed
                                  top-11-bit map (int32 only), 1 linear over the splitters' key range, 2
                                  logarithmic (bucket_slotmap_kernel; int32 leaves the fixed map when it
-                                 crowds the splitters of several keys into one slot); -1 none */
+                                 crowds the splitters of several keys into one slot); ABI 6: 3 the fixed map
+                                 with one refined slot (a second table over the most crowded slot, when
+                                 no map thins it: small keys mixed with uniform ones); -1 none */
     /* ABI 6 */
     int fence_ranges;         /* DSORT_OPT_TEST_WAVE_FENCE: device ranges the last sample sort's wave
                                  fence found unchanged across its first wave (0: no fence ran) */

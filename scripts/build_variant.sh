@@ -10,6 +10,6 @@ for f in dsort_wave dsort_text dsort_api; do
     -c "$PKG/csrc/$f.hip" -o "$OUT/obj/$f.o" 2>/dev/null &
 done
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 "$OUT/obj/dsort_wave.o" "$OUT/obj/dsort_text.o" "$OUT/obj/dsort_api.o" -shared -L/opt/rocm/lib -lrccl \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 "$OUT/obj/dsort_wave.o" "$OUT/obj/dsort_text.o" "$OUT/obj/dsort_api.o" -shared -L/opt/rocm/lib -lrccl -lrocprofiler-sdk-roctx \
   -Wl,-rpath,/opt/rocm/lib -lamdhip64 -o "$OUT/libdsort.so"
 echo "built $OUT/libdsort.so"

@@ -166,7 +166,8 @@ def main():
         "projection": {
             "label": "PROJECTION: the exchange is not run on one GPU; xGMI at the link peak",
             "exchange_bytes": int(x_bytes), "exchange_ms_at_peak": round(x_ms, 4),
-            "sort_then_merge": proj(t_a), "bucket_exchange": proj(t_b),
+            # (a leg this run skipped -- --only-bx -- has no projection: null, not a figure built on 0 ms)
+            "sort_then_merge": proj(t_a) if not args.only_bx else None, "bucket_exchange": proj(t_b),
         },
     }
     print(json.dumps(res), flush=True)

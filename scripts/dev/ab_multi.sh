@@ -1,12 +1,11 @@
 #!/bin/bash
-# A/B of the default build against several build_variants/<V> with ktime.py in one GPU session,
-# interleaved (default, V1, default, V2, ...) twice.  usage: VARS="v1 v2" scripts/dev/ab_multi.sh [ktime args]
+# Interleaved A/B of the default build and build_variants/$VARS with ktime.py (stage device times of
+# the fastest of --reps sorts), ROUNDS times.   VARS="v1 v2" [ROUNDS=3] scripts/dev/ab_multi.sh [ktime args]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
-R=$PWD; mkdir -p gpurun_out
-sha256sum distributed-sorting-with-fault-tolerance_amd/lib/libdsort.so
-for i in 1 2; do
-  for V in $VARS; do
-    timeout -k 10 90 python3 -u scripts/dev/ktime.py --reps 5 "$@" 2>&1 | grep -v amdgpu.ids || exit $?
-    DSORT_LIB=$R/build_variants/$V/libdsort.so timeout -k 10 90 python3 -u scripts/dev/ktime.py --reps 5 "$@" 2>&1 | grep -v amdgpu.ids || exit $?
+R=$PWD
+for i in $(seq ${ROUNDS:-3}); do
+  timeout -k 10 90 python3 -u scripts/dev/ktime.py --reps 6 "$@" || exit $?
+  for v in $VARS; do
+    DSORT_LIB=$R/build_variants/$v/libdsort.so timeout -k 10 90 python3 -u scripts/dev/ktime.py --reps 6 "$@" || exit $?
   done
 done

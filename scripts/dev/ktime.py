@@ -14,7 +14,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--keys", type=lambda s: int(eval(s, {}, {})), default=1 << 30)
 ap.add_argument("--reps", type=int, default=4)
 ap.add_argument("--dtype", choices=["i32", "i64"], default="i32")
-ap.add_argument("--dist", choices=["uniform", "zipf", "sorted", "reverse", "equal", "few", "byte", "ref100"],
+ap.add_argument("--dist", choices=["uniform", "zipf", "sorted", "reverse", "equal", "few", "byte", "ref100", "mixed"],
                 default="uniform")
 ap.add_argument("--opt", action="append", default=[], help="dsort option name=value (repeatable)")
 a = ap.parse_args()
@@ -43,6 +43,8 @@ else:
         t.copy_(t & 255)
     elif a.dist == "ref100":  # the reference's input.txt shape: keys in [1, 100]
         t.copy_((t & 0x7FFFFFFF) % 100 + 1)
+    elif a.dist == "mixed":  # half the keys in [1, 100] (input.txt's shape), half uniform, interleaved at random
+        t.copy_(torch.where((t & 1) == 1, ((t >> 1) & 0x7FFFFFFF) % 100 + 1, t))
 o = torch.empty_like(t)
 best = None
 for _ in range(a.reps):

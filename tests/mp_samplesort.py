@@ -62,6 +62,8 @@ def run(rank, world, store, n_total, dtype, dist, out_path, transport="rccl", op
             t.copy_(t >> (29 if dtype == "i32" else 61))
         elif dist == "ref100":  # the reference's input.txt shape: keys in [1, 100]
             t.copy_((t & 0x7FFFFFFF) % 100 + 1)
+        elif dist == "mixed":  # half [1, 100], half uniform: the first level's refined slot
+            t.copy_(torch.where((t & 1) == 1, t, (t & 0x7FFFFFFF) % 100 + 1))
     torch.cuda.synchronize()
     step(f"input ready ({sz} keys)")
     if presorted:

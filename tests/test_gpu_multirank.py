@@ -85,7 +85,7 @@ def test_sample_sort_tiny_and_empty_ranks(tmp_path):
 @pytest.mark.parametrize("world,dtype,dist", [(1, "i32", "uniform"), (2, "i32", "uniform"), (3, "i32", "uniform"),
                                               (4, "i32", "uniform"), (3, "i32", "seq"), (2, "i32", "rev"),
                                               (3, "i32", "few"), (2, "i64", "uniform"), (3, "i64", "zipf"),
-                                              (2, "i64", "few"), (3, "i32", "ref100")])
+                                              (2, "i64", "few"), (3, "i32", "ref100"), (2, "i32", "mixed")])
 def test_bucket_exchange_bit_exact(tmp_path, world, dtype, dist):
     """The bucket exchange (dsort_api.hip sample_sort_bx: global splitters from every rank's
     samples, the first partition level before the exchange, the received pieces finished by the

@@ -355,17 +355,24 @@ def _shaped_i32(gpu_ctx, n, dist):
         t.copy_((t & 0xFFFF) - 30000)
     elif dist == "mixed":  # half uniform, half in [1, 100]: no map separates the small keys
         t.copy_(torch.where((t & 1) == 1, t, (t & 0x7FFFFFFF) % 100 + 1))
+    elif dist == "mixed_signed":  # half uniform, half in [-50, 50): the small keys in two fixed slots
+        t.copy_(torch.where((t & 1) == 1, t, (t & 0x7FFFFFFF) % 100 - 50))
+    elif dist == "cluster":  # half uniform, half distinct keys of [0, 2^20): one slot of many distinct keys
+        t.copy_(torch.where((t & 1) == 1, t, (t >> 1) & 0xFFFFF))
     return t
 
 
 @pytest.mark.parametrize("dist,want_map", [("ref100", 1), ("byte", 1), ("signed100", 1), ("narrow16", 1),
-                                           ("mixed", None), ("uniform", 0)])
+                                           ("mixed", 3), ("mixed_signed", 3), ("cluster", 3), ("uniform", 0)])
 def test_small_key_ranges_adaptive_map_bit_exact(gpu_ctx, dist, want_map):
     """int32 keys from a narrow range (the reference's input.txt holds 10 000 keys in [1, 100]): the
     fixed 11-bit slot map of the first partition level puts every splitter into one slot; the slot
     map kernel then switches to the adaptive map (linear over the splitters' range, one-key slots;
-    DESIGN.md §3.3), reported as first_level_map.  2^28 keys (config C2's size) against torch.sort,
-    element for element."""
+    DESIGN.md §3.3), reported as first_level_map.  Round 6: small keys mixed half and half with
+    uniform ones (no map separates them) keep the fixed map with its most crowded slot refined by a
+    second table (first_level_map 3): [1, 100] (one-key sub-slots), [-50, 50) (across two fixed
+    slots, one refined), 2^20 distinct small keys (sub-slots of distinct splitters).  2^28 keys
+    (config C2's size) against torch.sort, element for element."""
     import torch
     n = 1 << 28
     t = _shaped_i32(gpu_ctx, n, dist)
