@@ -458,6 +458,8 @@ struct Gather {
     const void *spl;  // the splitters (Spl<T>, SS per bucket): equal neighbours = a duplicate run
     const void *bspl; // the first level's splitters (bk::Comp<T>::C, B - 1): a bucket's key bounds
     int B;
+    uint32_t tcap;    // tiles the tile and piece tables hold (>= 1): a tile's reads may go out before its
+                      // index is checked against the count on the device
 };
 
 // LOCAL: the chunk histograms are the prefix tables of sb_local_kernel (pref[c][j+1] -

@@ -1155,10 +1155,13 @@ __global__ void __launch_bounds__(64 * W, WG<T>::OCC) bin_sort_kernel(const T *i
         // same 128-byte lines of every chunk: run on one XCD at about the same time, such a line
         // comes from HBM once and from that XCD's L2 the second time.
         j = toff + xcd_block(blockIdx.x, gridDim.x);  // (toff: tiles [toff, toff + grid) of a split launch)
-        if (j >= *ntiles) return;
+        // the tile record and its piece table are read together with the tile count, not after it
+        // (an index past the count reads an entry inside the tables, and returns below)
+        const uint32_t jr = j < ga.tcap ? j : ga.tcap - 1;
         uint2 pe[2];
-        gather_pieces(ga, j, pe);
-        const sb::GTile gt = ga.tiles[j];
+        gather_pieces(ga, jr, pe);
+        const sb::GTile gt = ga.tiles[jr];
+        if (j >= *ntiles) return;
         base = gt.base;
         valid = (int)gt.valid;
         if (valid == 0) return;
@@ -1172,7 +1175,26 @@ __global__ void __launch_bounds__(64 * W, WG<T>::OCC) bin_sort_kernel(const T *i
         const auto *bs = static_cast<const typename bk::Comp<T>::C *>(ga.bspl);
         const bool lk = gt.j0 > 0 || gt.b > 0, hk = gt.j1 < gt.nsub || (int)gt.b + 1 < ga.B;
         known = lk && hk;
-        if (known) {
+        // int32 (DSORT_LATE_BOUNDS): the bounds and the duplicate hint are read after the key loads
+        // are issued -- read here, their round trip sat between the tile record and the key loads
+        // (one of the gather's four dependent round trips); int64 needs them first (one-key tiles)
+#ifndef DSORT_LATE_BOUNDS
+#define DSORT_LATE_BOUNDS 1
+#endif
+        constexpr bool late = DSORT_LATE_BOUNDS && sizeof(T) == 4;
+        const int jl = gt.j0 > 0 ? (int)gt.j0 - 1 : 0, jh = (int)gt.j1 - 1;  // splitters around the tile
+        const int nspl = (int)gt.nsub - 1;
+        const int jj = jl + lane_id();
+        if (late) {
+            gather_tile<T, W>(ga, pe, gt, in, s32 + 128, s32 + 96, x, threadIdx.x);
+            if (known) {
+                klo = gt.j0 > 0 ? sp[gt.j0 - 1].k : bk::Comp<T>::key_of(bs[gt.b - 1]);
+                khi = gt.j1 < gt.nsub ? sp[gt.j1 - 1].k : bk::Comp<T>::key_of(bs[gt.b]);
+            }
+            if (jj < jh && jj + 1 < nspl) hint = sp[jj].k == sp[jj + 1].k;
+            hint = __ballot(hint) != 0;
+        }
+        if (!late && known) {
             klo = gt.j0 > 0 ? sp[gt.j0 - 1].k : bk::Comp<T>::key_of(bs[gt.b - 1]);
             khi = gt.j1 < gt.nsub ? sp[gt.j1 - 1].k : bk::Comp<T>::key_of(bs[gt.b]);
 #ifndef DSORT_ONEKEY_TILES
@@ -1189,13 +1211,12 @@ __global__ void __launch_bounds__(64 * W, WG<T>::OCC) bin_sort_kernel(const T *i
                 return;
             }
         }
-        // a duplicate run inside a gathered tile shows as two equal neighbouring splitters
-        const int jl = gt.j0 > 0 ? (int)gt.j0 - 1 : 0, jh = (int)gt.j1 - 1;  // splitters around the tile
-        const int nspl = (int)gt.nsub - 1;
-        const int jj = jl + lane_id();
-        if (jj < jh && jj + 1 < nspl) hint = sp[jj].k == sp[jj + 1].k;
-        hint = __ballot(hint) != 0;
-        gather_tile<T, W>(ga, pe, gt, in, s32 + 128, s32 + 96, x, threadIdx.x);
+        if (!late) {
+            // a duplicate run inside a gathered tile shows as two equal neighbouring splitters
+            if (jj < jh && jj + 1 < nspl) hint = sp[jj].k == sp[jj + 1].k;
+            hint = __ballot(hint) != 0;
+            gather_tile<T, W>(ga, pe, gt, in, s32 + 128, s32 + 96, x, threadIdx.x);
+        }
     } else {
         j = toff + blockIdx.x;
         if (!load_tile<T, false, W>(in, n, tiles, ntiles, ga, j, nullptr, nullptr, x, base, valid)) return;
@@ -2049,7 +2070,8 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
                            0u, (uint32_t)(2 * (ALIGN - 1)), tt, num, ovf, num + 1, (uint32_t)tmax,
                            static_cast<const Chunk *>(dch), pieces_in_scan ? pcs : nullptr, PS, (uint32_t)tcap, stot);
         DSORT_HIP(ctx, hipGetLastError());
-        const Gather ga{static_cast<const GTile *>(tt), dch, dbi, cnt, pcs, PS, SS, spl, bspl, B};
+        const Gather ga{static_cast<const GTile *>(tt), dch, dbi, cnt, pcs, PS, SS, spl, bspl, B,
+                        (uint32_t)std::max<uint64_t>(tcap, 1)};
         DSORT_HIP(ctx, hipMemcpyAsync(hn, num, 8, hipMemcpyDeviceToHost, s));
         DSORT_HIP(ctx, hipEventRecord(ctx->sub_ev, s));
         // The tile sort of the first `early` tiles goes out behind the count's read-back, before the
