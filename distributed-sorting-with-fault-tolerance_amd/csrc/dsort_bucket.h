@@ -34,7 +34,15 @@ namespace bk {
 constexpr int BK_T = 1024;               // threads of the partition kernels
 constexpr int BK_MAXB = 1024;            // buckets at most (<= threads, one bucket per thread)
 constexpr int BK_OS = 32;                // samples per bucket
-constexpr int BK_CHUNK = 64;             // workgroups per column-sum chunk
+#ifndef DSORT_BK_CHUNK
+#define DSORT_BK_CHUNK 16
+#endif
+// workgroups per column-sum chunk.  (Round 6: 64 -> 16 with the chunk prefixes scanned by
+// bucket_colscan_kernel: at 2^30 keys, 4681 histogram rows made 74 column-sum workgroups of 64
+// serial-ish loads per thread, and the one-workgroup scan walked 74 chunk rows per column --
+// column sums + scan + offsets took 68 us of a 7.6 ms sort.)
+constexpr int BK_CHUNK = DSORT_BK_CHUNK;
+constexpr int BK_CSEG = 16;              // segments of the chunk rows per column (bucket_colscan_kernel)
 
 // Scatter sub-tile per key width: KPT keys per thread, SUB = BK_T * KPT keys staged in LDS
 // (int32: 64 KiB next to the 64 KiB line carry of the line scatter).
@@ -901,18 +909,62 @@ __device__ __forceinline__ uint64_t scan_excl_u64(uint64_t v, uint64_t *wsum, ui
     return off + incl - v;
 }
 
+// Columns [64 blk, 64 blk + 64) of part (nchunk rows of chunk sums): every column's exclusive
+// prefix over the chunks, in place, and its total tot[b].  Thread (column c, segment q) sums its
+// segment's rows (loads in flight together), the 16 segment sums are scanned in LDS, then the
+// segment's rows are rewritten as prefixes.
+static __global__ void __launch_bounds__(BK_MAXB) bucket_colscan_kernel(uint64_t *__restrict__ part, uint32_t nchunk,
+                                                                       int B, uint64_t *__restrict__ tot) {
+    __shared__ uint64_t seg[BK_CSEG][64];
+    const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
+    const int b = (int)blockIdx.x * 64 + c;
+    const uint32_t per = (nchunk + BK_CSEG - 1) / BK_CSEG;
+    const uint32_t r0 = (uint32_t)q * per, r1 = r0 + per < nchunk ? r0 + per : nchunk;
+    constexpr uint32_t U = 8;
+    uint64_t sum = 0;
+    if (b < B)
+        for (uint32_t r = r0; r < r1; r += U) {
+            uint64_t v[U];
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) v[u] = r + u < r1 ? part[(uint64_t)(r + u) * B + b] : 0;
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) sum += v[u];
+        }
+    seg[q][c] = sum;
+    __syncthreads();
+    uint64_t run = 0;
+    for (int i = 0; i < q; ++i) run += seg[i][c];
+    if (b < B) {
+        if (q == BK_CSEG - 1) tot[b] = run + sum;
+        for (uint32_t r = r0; r < r1; r += U) {
+            uint64_t v[U];
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) v[u] = r + u < r1 ? part[(uint64_t)(r + u) * B + b] : 0;
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) {
+                if (r + u < r1) part[(uint64_t)(r + u) * B + b] = run;
+                run += v[u];
+            }
+        }
+    }
+}
+
 // One workgroup: part -> exclusive prefix over chunks (in place); bucket starts bstart[0..B];
 // the tile table of the tile sort (every bucket cut into tiles, bucket_tiles) and its size.
+// ctot (not null): the column totals of bucket_colscan_kernel, which has scanned part already.
 static __global__ void __launch_bounds__(BK_MAXB) bucket_scan_kernel(uint64_t *__restrict__ part,
                                                              uint32_t nchunk, int B, uint32_t tile,
                                                              uint32_t align,
                                                              uint64_t *__restrict__ bstart,
                                                              TileRef *__restrict__ tt,
-                                                             uint32_t *__restrict__ ntiles) {
+                                                             uint32_t *__restrict__ ntiles,
+                                                             const uint64_t *__restrict__ ctot) {
     __shared__ uint64_t wsum[BK_MAXB / 64];
     const int b = threadIdx.x;
     uint64_t tot = 0;
-    if (b < B) {
+    if (ctot) {
+        if (b < B) tot = ctot[b];
+    } else if (b < B) {
         // column b's chunk sums -> exclusive prefixes, 8 loads in flight at a time (a serial chain
         // of dependent round trips took 92 us per sort at 2^30)
         constexpr uint32_t U = 8;

@@ -2249,7 +2249,7 @@ static int bk_layout(dsort_ctx *ctx, uint64_t n, int B, size_t smp_bytes, BkLayo
     size_t off = 0;
     auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
     const size_t o_smp = take(smp_bytes), o_spl = take((size_t)L.BP * sizeof(C)), o_cnt = take((size_t)L.G * B * 4),
-                 o_part = take((size_t)L.nchunk * B * 8), o_offs = take((size_t)L.G * B * 4),
+                 o_part = take((size_t)L.nchunk * B * 8 + (size_t)BK_MAXB * 8), o_offs = take((size_t)L.G * B * 4),
                  o_bst = take((size_t)(B + 1) * 8), o_tt = take((size_t)L.tmax * sizeof(TileRef)), o_nt = take(4),
                  o_map = take(BK_MAP_BYTES), o_ids = take(BkIds<T>::ON ? (size_t)L.G * L.subs * BK_T * Geo<T>::KPT * 2 : 0);
     int rc = ensure(ctx, &ctx->bucket, &ctx->bucket_bytes, off, "bucket partition");
@@ -2330,8 +2330,12 @@ static int first_level(dsort_ctx *ctx, const T *d_in, uint64_t n, uint64_t ioff,
     if ((rc = stage_event(ctx, s, timed, 10))) return rc;
     hipLaunchKernelGGL(bucket_colsum_kernel, dim3((unsigned)L.nchunk), dim3(BK_MAXB), 0, s, L.cnt, (uint32_t)L.G, B,
                        L.part);
+    // (the column totals after the chunk sums: part's slack)
+    uint64_t *ctot = L.part + (size_t)L.nchunk * B;
+    hipLaunchKernelGGL(bucket_colscan_kernel, dim3((unsigned)ceil_div((uint64_t)B, 64)), dim3(BK_MAXB), 0, s, L.part,
+                       (uint32_t)L.nchunk, B, ctot);
     hipLaunchKernelGGL(bucket_scan_kernel, dim3(1), dim3(BK_MAXB), 0, s, L.part, (uint32_t)L.nchunk, B, tile,
-                       (uint32_t)KPC<T>, L.bst, L.tt, L.ntl);
+                       (uint32_t)KPC<T>, L.bst, L.tt, L.ntl, (const uint64_t *)ctot);
     hipLaunchKernelGGL(bucket_offsets_kernel<uint32_t>, dim3((unsigned)L.nchunk), dim3(BK_MAXB), 0, s, L.cnt, L.part,
                        L.bst, (uint32_t)L.G, B, L.offs);
     DSORT_HIP(ctx, hipGetLastError());
