@@ -82,7 +82,7 @@ def parse(argv=None):
                          "timed region, comma-separated from c3,c4,c5 ('all', default; 'none' to skip)")
     ap.add_argument("--no-legs", dest="legs", action="store_const", const="none")
     ap.add_argument("--leg-timeout", type=float, default=180.0,
-                    help="exchange deadline of a sort leg in seconds (the C5 leg gets 4x)")
+                    help="exchange deadline of a sort leg in seconds (the C5 leg gets 2x)")
     ap.add_argument("--launcher-selftest", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
@@ -416,7 +416,7 @@ STAGE_KERNELS = {
 }
 # the generator and runtime copies are not part of the sort
 NOT_SORT = ("gen_uniform", "gen_zipf", "__amd_rocclr", "fingerprint", "descents")
-PMC_FILES = ("r5_pmc_traffic.json", "r4_pmc_traffic.json", "r3_pmc_traffic.json", "r2_pmc_traffic.json")
+PMC_FILES = ("r6_pmc_traffic.json", "r5_pmc_traffic.json", "r4_pmc_traffic.json", "r3_pmc_traffic.json", "r2_pmc_traffic.json")
 
 
 def lib_sha256():
@@ -742,7 +742,19 @@ def leg_summary(name, spec, world, steps, res):
 
 def run_c5_leg(spec, dtype="i32", timeout_s=900):
     """C5 in a child process (bench.py --kill-rank, which runs the C master and its workers): this
-    process may have touched the GPU, so the master is started as a child, never exec'd."""
+    process may have touched the GPU, so the master is started as a child, never exec'd.  The
+    master keeps the chunk replicas in POSIX shared memory (/dev/shm): a node whose /dev/shm cannot
+    hold them skips the leg with that reason instead of failing the workers mid-run."""
+    import shutil
+
+    need = spec["keys"] * (4 if dtype == "i32" else 8)
+    try:
+        free = shutil.disk_usage("/dev/shm").free
+    except OSError:
+        free = None
+    if free is not None and free < need + (need >> 3):
+        return {"config": "C5", "verified": False,
+                "error": f"skipped: /dev/shm has {free} bytes free, the replicas need {need}"}
     cmd = [sys.executable, "-u", os.path.abspath(__file__), "--kill-rank", str(spec["kill_rank"]),
            "--gpus", str(spec["workers"]), "--keys", str(spec["keys"]), "--dtype", dtype, "--kill-after-stage", "0"]
     t0 = time.perf_counter()
@@ -804,7 +816,7 @@ def run_multi(args, rank, world):
     dist.barrier()
     if "c5" in legs_wanted(args) and rank == 0:
         # (the other ranks hold no sort memory now and wait at the barrier below)
-        legs["c5"] = run_c5_leg(plan["c5"], timeout_s=int(args.leg_timeout * 4))
+        legs["c5"] = run_c5_leg(plan["c5"], timeout_s=int(args.leg_timeout * 2))
     dist.barrier()
     dist.destroy_process_group()
     return elapsed, ok, per_rank, w, legs

@@ -5,7 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$PWD; mkdir -p gpurun_out
 bash scripts/dev/rounds/g_r5_full.sh || exit $?
-bash scripts/gpu_profile_r5.sh pmc trace c3 > gpurun_out/r5_profile.log 2>&1 || exit $?
+bash scripts/dev/rounds/gpu_profile_r5.sh pmc trace c3 > gpurun_out/r5_profile.log 2>&1 || exit $?
 TAG=r5c3_ SCRIPT=scripts/c3_rank.py ARGS="--steps 1 --warmup 1 --no-check --only-bx" bash scripts/dev/pmc_sub.sh >> gpurun_out/r5_profile.log 2>&1 || exit $?
 # the PMC table of this build, made on the box so the bench lines below find it matched
 python3 scripts/dev/pmc_json.py gpurun_out/r5_pmc_traffic.json r5i32_ r5i64_ > gpurun_out/r5_pmc_json.log 2>&1 || exit $?
