@@ -59,13 +59,28 @@ template <> struct Geo<int64_t> { static constexpr int KPT = 6; };
 // 1.50 -> 2.08 ms.  int32's packed lookup costs less than the 2 bytes per key would
 // (DSORT_BK_IDS32 builds it for comparison: histogram 0.77 -> 1.23 ms, scatter 2.67 -> 3.25 ms at
 // 2^30, profiles/r4_ab_bucket_ids_int32.log).
+// Round 6: three 10-bit buckets per word (DSORT_BK_IDS3, int64: KPT = 6 keys in two words, B <=
+// 1024) -- 1.33 bytes per key instead of 2: C4's id traffic 4.2 -> 2.8 GB, and the scatter still only
+// unpacks.  (One byte per key, the bucket above its slot's first, took it to 2.1 GB, but the scatter's
+// slot computation and table read cost more than the bytes saved: C4 11.84 -> 11.89 ms,
+// profiles/r6_ab_ids8_dropped.log.)
+#ifndef DSORT_BK_IDS3
+#define DSORT_BK_IDS3 1
+#endif
 template <typename T> struct BkIds {
 #ifdef DSORT_BK_IDS32
     static constexpr bool ON = true;
 #else
     static constexpr bool ON = sizeof(T) == 8;
 #endif
+    static constexpr int PER_WORD = DSORT_BK_IDS3 && sizeof(T) == 8 ? 3 : 2;  // buckets per 32-bit word
+    static constexpr int BITS = PER_WORD == 3 ? 10 : 16;
+    static constexpr uint32_t MASK = (1u << BITS) - 1;
 };
+static_assert(BK_MAXB <= 1024, "10-bit bucket ids");
+// Ids of a sub-tile (SUB keys from key s): thread-major pairs (PER_WORD 2) -- thread t's KPT / 2 words
+// at s / 2 + KPT t / 2 --, or (PER_WORD 3) word w of thread t at (s / SUB) (KPT / 3) BK_T + w BK_T + t:
+// every access of a wave is 64 consecutive words.
 
 struct TileRef {
     uint64_t base;   // first key of the tile
@@ -814,8 +829,11 @@ __global__ void __launch_bounds__(BK_T, 2) bucket_hist_kernel(const T *__restric
 #pragma unroll
         for (int k = 0; k < KPT; ++k) key[k] = nxt[k];
         if (sub + 1 < subs) load_sub<T, KPT, false>(in, b0 + SUB, n, b0 - threadIdx.x + 2 * SUB, nxt);
-        // the buckets of the thread's keys, two per word (bucket ids: BkIds)
-        uint32_t idw[KPT / 2] = {};
+        // the buckets of the thread's keys, BkIds::PER_WORD per word (bucket ids)
+        constexpr int PW = BkIds<T>::PER_WORD;
+        static_assert(!BkIds<T>::ON || KPT % PW == 0, "bucket ids: whole words per thread");
+        uint32_t idw[KPT / PW > 0 ? KPT / PW : 1] = {};
+        const auto idput = [&](int k, int b) { idw[k / PW] |= (uint32_t)b << (BkIds<T>::BITS * (k % PW)); };
         // (the mode branch outside the key loop: a slot array would cost the second workgroup)
         if (m.hot) {  // (runs of one bucket: aggregated increments, bucket_runs_hint)
 #pragma unroll
@@ -824,7 +842,7 @@ __global__ void __launch_bounds__(BK_T, 2) bucket_hist_kernel(const T *__restric
                 const uint32_t sl = m.mode == 0 ? slot_mode<T, BK_SLOTB, 0, ADP>(m, key[k]) : slot_mode<T, BK_SLOTB, 1, ADP>(m, key[k]);
                 const int b = bucket_fast<T, false, true, ADP>(spl, rng, sl, key[k], CT::make(key[k], i + ioff), tab2, &m);
                 bucket_bump<false>(hist, b, i < n);
-                if (i < n) idw[k / 2] |= (uint32_t)b << (16 * (k & 1));
+                if (i < n) idput(k, b);
             }
         } else if (ADP ? m.mode == 0 : !m.one) {
 #pragma unroll
@@ -834,7 +852,7 @@ __global__ void __launch_bounds__(BK_T, 2) bucket_hist_kernel(const T *__restric
                 if (i < n) {
                     const int b = bucket_fast<T, false, ADP, ADP>(spl, rng, sl, key[k], CT::make(key[k], i + ioff));
                     atomicAdd(&hist[b], 1u);
-                    idw[k / 2] |= (uint32_t)b << (16 * (k & 1));
+                    idput(k, b);
                 }
             }
         } else {  // (int64 log map; int32 with one-key slots -- its slot_mode ignores the mode)
@@ -845,7 +863,7 @@ __global__ void __launch_bounds__(BK_T, 2) bucket_hist_kernel(const T *__restric
                 if (i < n) {
                     const int b = bucket_fast<T, false, true, ADP>(spl, rng, sl, key[k], CT::make(key[k], i + ioff), tab2, &m);
                     atomicAdd(&hist[b], 1u);
-                    idw[k / 2] |= (uint32_t)b << (16 * (k & 1));
+                    idput(k, b);
                 }
             }
         }
@@ -853,9 +871,15 @@ __global__ void __launch_bounds__(BK_T, 2) bucket_hist_kernel(const T *__restric
         // i.e. a thread stores (and the scatter's thread loads) KPT / 2 consecutive words -- one
         // 2-byte access per key measured slower than the lookup it replaces (int32)
         if (BkIds<T>::ON && m.ids) {
-            uint32_t *dst = ids + (b0 - threadIdx.x) / 2 + (uint64_t)threadIdx.x * (KPT / 2);
+            if constexpr (PW == 3) {
+                uint32_t *dst = ids + (b0 - threadIdx.x) / SUB * (KPT / 3) * BK_T + threadIdx.x;
 #pragma unroll
-            for (int w = 0; w < KPT / 2; ++w) dst[w] = idw[w];
+                for (int w = 0; w < KPT / 3; ++w) dst[w * BK_T] = idw[w];
+            } else {
+                uint32_t *dst = ids + (b0 - threadIdx.x) / 2 + (uint64_t)threadIdx.x * (KPT / 2);
+#pragma unroll
+                for (int w = 0; w < KPT / 2; ++w) dst[w] = idw[w];
+            }
         }
     }
     __syncthreads();
@@ -1152,11 +1176,22 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
     uint64_t bk_acc[8] = {}, bk_t0 = __builtin_amdgcn_s_memtime();
 #endif
     T nxt[KPT];
-    uint32_t nid[IDS ? KPT / 2 : 1];  // (the histogram's thread-major bucket ids, two per word)
+    constexpr int PW = BkIds<T>::PER_WORD;
+    uint32_t nid[IDS ? KPT / PW : 1];  // (the histogram's bucket ids, PW per word)
+    // the ids of the sub-tile from key s
+    const auto load_ids = [&](uint64_t s) {
+        if constexpr (IDS && PW == 3) {
+            const uint32_t *src = ids + s / SUB * (KPT / 3) * BK_T + tb;
+#pragma unroll
+            for (int w = 0; w < KPT / 3; ++w) nid[w] = src[w * BK_T];
+        } else if constexpr (IDS) {
+#pragma unroll
+            for (int w = 0; w < KPT / 2; ++w) nid[w] = ids[s / 2 + (uint64_t)tb * (KPT / 2) + w];
+        }
+    };
     load_sub<T, KPT>(in, g0 + tb, n, g0 + SUB, nxt);
     if constexpr (IDS) {
-#pragma unroll
-        for (int w = 0; w < KPT / 2; ++w) nid[w] = g0 < n ? ids[g0 / 2 + (uint64_t)tb * (KPT / 2) + w] : 0u;
+        if (g0 < n) load_ids(g0);
     }
 #pragma unroll 1
     for (int sub = 0; sub < subs; ++sub) {
@@ -1170,16 +1205,13 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
         for (int k = 0; k < KPT; ++k) key[k] = nxt[k];
         if constexpr (IDS) {
 #pragma unroll
-            for (int k = 0; k < KPT; ++k) sl[k] = (nid[k / 2] >> (16 * (k & 1))) & 0xFFFFu;
+            for (int k = 0; k < KPT; ++k) sl[k] = (nid[k / PW] >> (BkIds<T>::BITS * (k % PW))) & BkIds<T>::MASK;
         } else {
             slots_at<T, KPT, ADP>(m, key, sl);
         }
         if (!last) {
             load_sub<T, KPT>(in, s0 + SUB + tb, n, s0 + 2 * SUB, nxt);
-            if constexpr (IDS) {
-#pragma unroll
-                for (int w = 0; w < KPT / 2; ++w) nid[w] = ids[(s0 + SUB) / 2 + (uint64_t)tb * (KPT / 2) + w];
-            }
+            if constexpr (IDS) load_ids(s0 + SUB);
         }
         BKST(6);  // (the sub-tile's keys in, their slots)
 #ifndef DSORT_HOT_SCATTER

@@ -2234,7 +2234,7 @@ struct BkLayout {
     uint64_t *part, *bst;
     bk::TileRef *tt;
     bk::BkMap *map;
-    uint32_t *ids;  // every key's bucket (bk::BkIds: two per word, thread-major per sub-tile), else null
+    uint32_t *ids;  // every key's bucket (bk::BkIds: 2 or 3 per word), else null
 };
 template <typename T>
 static int bk_layout(dsort_ctx *ctx, uint64_t n, int B, size_t smp_bytes, BkLayout<T> &L) {
@@ -2251,7 +2251,7 @@ static int bk_layout(dsort_ctx *ctx, uint64_t n, int B, size_t smp_bytes, BkLayo
     const size_t o_smp = take(smp_bytes), o_spl = take((size_t)L.BP * sizeof(C)), o_cnt = take((size_t)L.G * B * 4),
                  o_part = take((size_t)L.nchunk * B * 8 + (size_t)BK_MAXB * 8), o_offs = take((size_t)L.G * B * 4),
                  o_bst = take((size_t)(B + 1) * 8), o_tt = take((size_t)L.tmax * sizeof(TileRef)), o_nt = take(4),
-                 o_map = take(BK_MAP_BYTES), o_ids = take(BkIds<T>::ON ? (size_t)L.G * L.subs * BK_T * Geo<T>::KPT * 2 : 0);
+                 o_map = take(BK_MAP_BYTES), o_ids = take(BkIds<T>::ON ? (size_t)L.G * L.subs * BK_T * Geo<T>::KPT * 4 / BkIds<T>::PER_WORD : 0);
     int rc = ensure(ctx, &ctx->bucket, &ctx->bucket_bytes, off, "bucket partition");
     if (rc) return rc;
     char *a = static_cast<char *>(ctx->bucket);
