@@ -368,9 +368,23 @@ __device__ __forceinline__ int onekey_ab(const typename Comp<T>::C &a, const typ
     const int j = (int)q;
     return lo + 1 + (j < hi - lo - 2 ? j : hi - lo - 2);
 }
+__device__ __forceinline__ int refine_inner(int lo, int hi, uint32_t idx);
+// int64 (round 6, DSORT_ONEKEY_HASH): the copies of K all go to the buckets strictly between K's
+// first and last splitter, spread by a hash of the index (as in the refined slot, refine_pick) --
+// one 8-byte read of K instead of two 16-byte splitter reads: the first level's lookups are bound by
+// LDS bandwidth, and C4 puts ~58 % of its keys in one-key slots.  The outer buckets then hold only
+// keys below / above K (fewer keys than a sample bucket, never more).
+#ifndef DSORT_ONEKEY_HASH
+#define DSORT_ONEKEY_HASH 1
+#endif
 template <typename T>
 __device__ __forceinline__ int bucket_onekey(const typename Comp<T>::C *spl, int lo, int hi, T key,
                                              const typename Comp<T>::C &c) {
+    if constexpr (sizeof(T) == 8 && DSORT_ONEKEY_HASH) {
+        const T K = Comp<T>::key_of(spl[lo]);
+        if (key != K) return key < K ? lo : hi;
+        return refine_inner(lo, hi, Comp<T>::idx_of(c));
+    }
     return onekey_ab<T>(spl[lo], spl[hi - 1], lo, hi, key, c);
 }
 // The refined slot (BkMap.r2s, int32 on the fixed map): the key's sub-slot entry, then

@@ -145,6 +145,10 @@ def test_sub_buckets(gpu_ctx, dtype, kind, sub_keys, os, merged):
         torch.cuda.synchronize()
         passes = gpu_ctx.stats()["merge_passes"]
     assert np.array_equal(out.cpu().numpy(), np.sort(a))
+    if merged and dtype == "i64" and kind == "few":
+        # (int64 one-key slots put every copy of a key in its inner buckets, DSORT_ONEKEY_HASH: with 4
+        # keys of ~4 splitters each every bucket is pure or empty, and none reaches the second level)
+        merged = False
     if merged is not None:
         assert (passes >= 1) == merged
 
@@ -279,8 +283,9 @@ def test_pure_buckets_heavy_keys(gpu_ctx, dtype, mode, n):
 def test_one_key_slots_skewed(gpu_ctx, dtype, mode, n):
     """Skewed small keys (a Zipf head) with the type's extremes: the int64 lookups switch to the
     log slot map, every heavy key gets a one-key slot whose copies are split over its run of
-    buckets by index (the outer two exactly as the composite order), and the tail and the
-    extremes share wide slots (dsort_bucket.h BkMap, bucket_fast)."""
+    buckets -- int32 by index (the outer two exactly as the composite order), int64 by a hash of
+    the index over the inner ones (DSORT_ONEKEY_HASH) -- and the tail and the extremes share wide
+    slots (dsort_bucket.h BkMap, bucket_fast, bucket_onekey)."""
     rng = np.random.default_rng(n + (11 if dtype == np.int64 else 0))
     info = np.iinfo(dtype)
     a = np.minimum(rng.zipf(1.3, n), 1 << 20).astype(dtype)
