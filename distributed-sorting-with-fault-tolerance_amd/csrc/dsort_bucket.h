@@ -341,12 +341,11 @@ __device__ __forceinline__ void build_slots(const typename Comp<T>::C *spl, int 
 
 // Bucket of (key, index).  In a one-key slot the copies of K may go to any bucket from the
 // first of K's splitters to the one after the last (every one of those buckets holds keys <= K
-// before it and >= K after it, and the buckets strictly inside hold only K).  The two outer
-// buckets take exactly the copies the composite order gives them (index <= the first run
-// splitter's, > the last one's), so they stay as full as a sample bucket should; the copies in
-// between are split over the inner buckets by index range, in proportion -- two splitter reads
-// and a division instead of a search over K's run (and a sub-tile's copies, adjacent in the
-// input, land together in one or two buckets).
+// before it and >= K after it, and the buckets strictly inside hold only K).  Since round 6
+// (bucket_onekey, DSORT_ONEKEY_HASH) they all go to the inner buckets, by a hash of the index.
+// (Before: the two outer buckets took exactly the copies the composite order gives them (index <=
+// the first run splitter's, > the last one's) and the copies in between were split over the inner
+// buckets by index range, in proportion -- onekey_ab, kept for DSORT_ONEKEY_HASH=0.)
 // Histogram and scatter use the same map and table, so they agree key for key.  (Which copy of
 // K lands where does not matter to a keys-only sort.)
 // int32: the slot entry carries the slot's first splitter's key down to bit 1 (the slot is the
@@ -369,18 +368,21 @@ __device__ __forceinline__ int onekey_ab(const typename Comp<T>::C &a, const typ
     return lo + 1 + (j < hi - lo - 2 ? j : hi - lo - 2);
 }
 __device__ __forceinline__ int refine_inner(int lo, int hi, uint32_t idx);
-// int64 (round 6, DSORT_ONEKEY_HASH): the copies of K all go to the buckets strictly between K's
-// first and last splitter, spread by a hash of the index (as in the refined slot, refine_pick) --
-// one 8-byte read of K instead of two 16-byte splitter reads: the first level's lookups are bound by
-// LDS bandwidth, and C4 puts ~58 % of its keys in one-key slots.  The outer buckets then hold only
-// keys below / above K (fewer keys than a sample bucket, never more).
+// Round 6 (DSORT_ONEKEY_HASH): the copies of K all go to the buckets strictly between K's first
+// and last splitter, spread by a hash of the index (as in the refined slot, refine_pick) -- one read
+// of K instead of two splitter reads (the int64 lookups are bound by LDS bandwidth, and C4 puts ~58 %
+// of its keys in one-key slots), no run of neighbouring copies piling onto one bucket's counter, and
+// the outer buckets hold only keys below / above K, so every copy of K lands in a pure bucket that
+// the second level skips.  2^30 keys: C4 (int64 Zipf) 11.7 -> 11.2 ms, 16 distinct int32 keys 7.9 ->
+// 5.2 ms, int32 keys of [1, 100] 6.1 -> 4.1 ms, uniform unchanged (profiles/r6_ab_onekey_hash_*.log).
+// (Bit 0: int64, bit 1: int32.)
 #ifndef DSORT_ONEKEY_HASH
-#define DSORT_ONEKEY_HASH 1
+#define DSORT_ONEKEY_HASH 3
 #endif
 template <typename T>
 __device__ __forceinline__ int bucket_onekey(const typename Comp<T>::C *spl, int lo, int hi, T key,
                                              const typename Comp<T>::C &c) {
-    if constexpr (sizeof(T) == 8 && DSORT_ONEKEY_HASH) {
+    if constexpr ((DSORT_ONEKEY_HASH >> (sizeof(T) == 8 ? 0 : 1)) & 1) {
         const T K = Comp<T>::key_of(spl[lo]);
         if (key != K) return key < K ? lo : hi;
         return refine_inner(lo, hi, Comp<T>::idx_of(c));
