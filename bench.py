@@ -832,10 +832,11 @@ def result_header(args, world):
 
 def stage_roofline(k, w, n, dist="uniform", drop_pure=False):
     """Per-stage HIP-event times of the sort's kernels (the average launch of each over the timed
-    steps) against their algorithmic bytes, and the slowest of them.  drop_pure: the one-GPU
-    out-of-place sort, whose first-level scatter writes only the keys outside single-key buckets
-    (round 5: the second level fills those with their key) -- it reads n keys and writes
-    tile_sort_keys; the bucket exchange's scatter writes all n."""
+    steps) against their algorithmic bytes, and the slowest of them.  drop_pure: the first-level
+    scatter writes only the keys outside single-key buckets (round 5: the one-GPU sort, whose second
+    level fills those with their key; round 6: the bucket exchange too, whose owners fill them) --
+    it reads n keys and writes tile_sort_keys (for a rank of the bucket exchange: its received
+    non-pure keys, the same share of its keys in expectation, exact on one GPU)."""
     stages = []
     for kernel, field, per_key, keys_field in STAGE_KERNELS[w]:
         # (int64: the scatter variant that reads the histogram's bucket ids runs on skewed keys --
@@ -969,7 +970,7 @@ def summarize_multi(args, world, elapsed, per_rank, w):
         kr = {"tile_sort_kernel_ms": float(per_rank[r, 0]), "bucket_hist_ms": float(per_rank[r, 6]),
               "bucket_scatter_ms": float(per_rank[r, 7]), "sub_partition_ms": float(per_rank[r, 8]),
               "n": float(per_rank[r, 5]), "tile_sort_keys": float(per_rank[r, 9])}
-        for st in stage_roofline(kr, w, int(kr["n"]), args.dist):
+        for st in stage_roofline(kr, w, int(kr["n"]), args.dist, drop_pure=True):
             if best is None or st["avg_launch_ms"] > best[1]["avg_launch_ms"]:
                 best = (r, st)
     if best is None:  # below 2^25 keys per rank: the tile sort

@@ -595,7 +595,8 @@ static int sample_sort_bx(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, T **d
     //    starts while the scatter runs); kill stage 0
     const uint64_t *hb;
     T *part;
-    rc = bx_partition<T>(ctx, d_in, pl, all, s, true, &hb, &part);
+    std::vector<uint8_t> pure;
+    rc = bx_partition<T>(ctx, d_in, pl, all, s, true, &hb, &part, pure);
     if (rc) return rc;
     // 3. every rank's bucket starts, on the comm stream: they are on the host before the scatter
     //    ends, so the all-gather, the exchange's enqueue and the first wave's tables overlap it (on
@@ -614,15 +615,29 @@ static int sample_sort_bx(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, T **d
     // stream waits for each wave's event).  (The host transport and a single rank run the same waves
     // one after the other: the same layout and second-level calls as the 8-GPU run.)
     const int jb[3] = {0, W == 2 ? Bl / 2 : Bl, Bl};
-    const uint64_t *hme = hb_all.data() + (size_t)me * (Bt + 1);
-    auto hof = [&](int r) { return hb_all.data() + (size_t)r * (Bt + 1); };
+    // Positions in `part` and in the receive buffer follow every rank's compacted starts (a pure
+    // bucket -- its keys dropped by the scatter, bx_partition -- of size 0); the output sizes follow
+    // the real starts.
+    std::vector<uint64_t> hc_all(hb_all.size());
+    for (int r = 0; r < P; ++r) {
+        const uint64_t *h = hb_all.data() + (size_t)r * (Bt + 1);
+        uint64_t *c = hc_all.data() + (size_t)r * (Bt + 1), run = 0;
+        for (int g = 0; g <= Bt; ++g) {
+            c[g] = run;
+            if (g < Bt && !pure[(size_t)g]) run += h[g + 1] - h[g];
+        }
+    }
+    const uint64_t *hme = hc_all.data() + (size_t)me * (Bt + 1);
+    auto hof = [&](int r) { return hc_all.data() + (size_t)r * (Bt + 1); };
     std::vector<uint64_t> rlen(P, 0);
-    uint64_t sent = 0;
+    uint64_t sent = 0, nout = 0;
     for (int q = 0; q < P; ++q) {
         rlen[q] = hof(q)[(size_t)(me + 1) * Bl] - hof(q)[(size_t)me * Bl];
         if (q != me) sent += hme[(size_t)(q + 1) * Bl] - hme[(size_t)q * Bl];
+        const uint64_t *h = hb_all.data() + (size_t)q * (Bt + 1);
+        nout += h[(size_t)(me + 1) * Bl] - h[(size_t)me * Bl];
     }
-    uint64_t nrecv = 0;
+    uint64_t nrecv = 0;  // (keys received: the compacted sizes)
     for (int q = 0; q < P; ++q) nrecv += rlen[q];
     // The other ranks' pieces land behind this rank's partitioned keys when they fit (its own buckets
     // are then read in place: no copy); else everything goes to a receive buffer.
@@ -649,7 +664,7 @@ static int sample_sort_bx(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, T **d
         rc = ensure(ctx, &ctx->recv, &ctx->recv_bytes, (nrecv ? nrecv : 1) * sizeof(T) + 16, "receive buffer");
         if (rc) return rc;
     }
-    rc = ensure(ctx, &ctx->recv2, &ctx->recv2_bytes, (nrecv ? nrecv : 1) * sizeof(T), "sorted slice");
+    rc = ensure(ctx, &ctx->recv2, &ctx->recv2_bytes, (nout ? nout : 1) * sizeof(T), "sorted slice");
     if (rc) return rc;
     T *rb = behind ? part : static_cast<T *>(ctx->recv);  // (the second level's source)
     exchange_fault_point(ctx, 2);
@@ -753,7 +768,7 @@ static int sample_sort_bx(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, T **d
             }
             if (w == 0 && fence.on() && (rc = fence.print(ctx, s, 0))) return rc;
             uint64_t nw = 0;
-            rc = bx_local_sort<T>(ctx, rb, outp, pl, hb_all.data(), base.data() + (size_t)w * P, jb[w], jb[w + 1],
+            rc = bx_local_sort<T>(ctx, rb, outp, pl, hb_all.data(), hc_all.data(), base.data() + (size_t)w * P, jb[w], jb[w + 1],
                                   out_off, w, W, s, true, &nw);
             if (rc) return rc;
             out_off += nw;
@@ -762,11 +777,11 @@ static int sample_sort_bx(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, T **d
         flush_later(ctx);
         ctx->last_stream = s;
         ctx->stats.keys_in = pl.n_local;
-        ctx->stats.keys_out = nrecv;
+        ctx->stats.keys_out = nout;
         ctx->stats.keys_sent = sent;
         ctx->stats.exchange_path = 1;
         *d_out = outp;
-        *n_out = nrecv;
+        *n_out = nout;
         return DSORT_OK;
     }
     // 5. the second level and the tile sort of this rank's buckets, wave by wave, each queued behind
@@ -788,7 +803,7 @@ static int sample_sort_bx(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, T **d
         if (w == 0 && fence.on()) rc = fence.print(ctx, s, 0);
         uint64_t nw = 0;
         if (!rc)
-            rc = bx_local_sort<T>(ctx, rb, outp, pl, hb_all.data(), base.data() + (size_t)w * P, jb[w], jb[w + 1],
+            rc = bx_local_sort<T>(ctx, rb, outp, pl, hb_all.data(), hc_all.data(), base.data() + (size_t)w * P, jb[w], jb[w + 1],
                                   out_off, w, W, s, true, &nw);
         out_off += nw;
         if (!rc && w == 0 && fence.on()) rc = fence.check(ctx, s, deadline);
@@ -817,11 +832,11 @@ static int sample_sort_bx(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, T **d
     flush_later(ctx);  // (the buffers the second level replaced while the keys were in flight)
     ctx->last_stream = s;
     ctx->stats.keys_in = pl.n_local;
-    ctx->stats.keys_out = nrecv;
+    ctx->stats.keys_out = nout;
     ctx->stats.keys_sent = sent;
     ctx->stats.exchange_path = 1;
     *d_out = outp;
-    *n_out = nrecv;
+    *n_out = nout;
     return DSORT_OK;
 }
 

@@ -992,13 +992,20 @@ static __global__ void __launch_bounds__(BK_MAXB) bucket_colscan_kernel(uint64_t
 // One workgroup: part -> exclusive prefix over chunks (in place); bucket starts bstart[0..B];
 // the tile table of the tile sort (every bucket cut into tiles, bucket_tiles) and its size.
 // ctot (not null): the column totals of bucket_colscan_kernel, which has scanned part already.
-static __global__ void __launch_bounds__(BK_MAXB) bucket_scan_kernel(uint64_t *__restrict__ part,
+// cspl (not null, the bucket exchange, round 6): the compacted starts cstart[0..B] too -- the
+// starts with every pure bucket (between two splitters of one key, whose keys the scatter drops)
+// of size 0: the scatter's layout of `part`, so the keys a rank ships are contiguous per peer and
+// a pure bucket ships none.
+template <typename T>
+__global__ void __launch_bounds__(BK_MAXB) bucket_scan_kernel(uint64_t *__restrict__ part,
                                                              uint32_t nchunk, int B, uint32_t tile,
                                                              uint32_t align,
                                                              uint64_t *__restrict__ bstart,
                                                              TileRef *__restrict__ tt,
                                                              uint32_t *__restrict__ ntiles,
-                                                             const uint64_t *__restrict__ ctot) {
+                                                             const uint64_t *__restrict__ ctot,
+                                                             const typename Comp<T>::C *__restrict__ cspl,
+                                                             uint64_t *__restrict__ cstart) {
     __shared__ uint64_t wsum[BK_MAXB / 64];
     const int b = threadIdx.x;
     uint64_t tot = 0;
@@ -1037,6 +1044,13 @@ static __global__ void __launch_bounds__(BK_MAXB) bucket_scan_kernel(uint64_t *_
     if (b == 0) {
         bstart[B] = allk;
         *ntiles = (uint32_t)allt;
+    }
+    if (cspl) {  // (workgroup-uniform)
+        const bool pure = b > 0 && b + 1 < B && Comp<T>::key_of(cspl[b - 1]) == Comp<T>::key_of(cspl[b]);
+        uint64_t allc;
+        const uint64_t sc = scan_excl_u64(b < B && !pure ? tot : 0, wsum, allc);
+        if (b < B) cstart[b] = sc;
+        if (b == 0) cstart[B] = allc;
     }
 }
 

@@ -286,16 +286,21 @@ int bx_sample(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, BxSample *d_smp, 
 //    level of d_in into ctx->scratch (bucket-major, Btot buckets; recv_room more keys fit behind
 //    them).  *hb = this rank's bucket starts (host, Btot + 1), *part = the partitioned keys.  Kill
 //    stage 0 fires here.
+//    pure[g] (Btot): global bucket g lies between two splitters of one key.  Its keys are dropped
+//    (DSORT_BX_DROP_PURE, round 6): part holds the others at the compacted starts -- every pure
+//    bucket of size 0 -- and the owner fills a pure bucket with its key, so its keys never cross
+//    the links.
 template <typename T>
 int bx_partition(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, const BxSample *d_all, hipStream_t s, bool timed,
-                 const uint64_t **hb, T **part);
+                 const uint64_t **hb, T **part, std::vector<uint8_t> &pure);
 // 3. after the exchange: src holds the pieces of this rank's buckets from every source r, source
 //    r's in bucket order from src[base[r]] on (base: of the wave's first bucket);
-//    hb_all[r * (Btot + 1) + g] = source r's bucket starts.  Sorts them into out (nrecv keys; src holds at least nrecv keys: the second level's
-//    scratch).  Kill stages 1 and 2 fire here.
+//    hb_all[r * (Btot + 1) + g] = source r's bucket starts, hc_all its compacted starts (the pieces'
+//    positions: a pure bucket has none).  Sorts them into out (nrecv keys; src holds at least nrecv
+//    keys: the second level's scratch).  Kill stages 1 and 2 fire here.
 //    The buckets [j_lo, j_hi) of this rank (wave w of W) into out + out_off; *n_out = their keys.
 template <typename T>
-int bx_local_sort(dsort_ctx *ctx, T *src, T *out, const BxPlan &pl, const uint64_t *hb_all,
+int bx_local_sort(dsort_ctx *ctx, T *src, T *out, const BxPlan &pl, const uint64_t *hb_all, const uint64_t *hc_all,
                   const uint64_t *base, int j_lo, int j_hi, uint64_t out_off, int w, int W, hipStream_t s,
                   bool timed, uint64_t *n_out);
 

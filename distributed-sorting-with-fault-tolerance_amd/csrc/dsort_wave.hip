@@ -2232,6 +2232,7 @@ struct BkLayout {
     C *spl;
     uint32_t *cnt, *offs, *ntl;
     uint64_t *part, *bst;
+    uint64_t *cst;  // the bucket exchange's compacted starts (pure buckets of size 0, bucket_scan_kernel)
     bk::TileRef *tt;
     bk::BkMap *map;
     uint32_t *ids;  // every key's bucket (bk::BkIds: 2 or 3 per word), else null
@@ -2250,7 +2251,7 @@ static int bk_layout(dsort_ctx *ctx, uint64_t n, int B, size_t smp_bytes, BkLayo
     auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
     const size_t o_smp = take(smp_bytes), o_spl = take((size_t)L.BP * sizeof(C)), o_cnt = take((size_t)L.G * B * 4),
                  o_part = take((size_t)L.nchunk * B * 8 + (size_t)BK_MAXB * 8), o_offs = take((size_t)L.G * B * 4),
-                 o_bst = take((size_t)(B + 1) * 8), o_tt = take((size_t)L.tmax * sizeof(TileRef)), o_nt = take(4),
+                 o_bst = take((size_t)(B + 1) * 8), o_cst = take((size_t)(B + 1) * 8), o_tt = take((size_t)L.tmax * sizeof(TileRef)), o_nt = take(4),
                  o_map = take(BK_MAP_BYTES), o_ids = take(BkIds<T>::ON ? (size_t)L.G * L.subs * BK_T * Geo<T>::KPT * 4 / BkIds<T>::PER_WORD : 0);
     int rc = ensure(ctx, &ctx->bucket, &ctx->bucket_bytes, off, "bucket partition");
     if (rc) return rc;
@@ -2261,6 +2262,7 @@ static int bk_layout(dsort_ctx *ctx, uint64_t n, int B, size_t smp_bytes, BkLayo
     L.part = reinterpret_cast<uint64_t *>(a + o_part);
     L.offs = reinterpret_cast<uint32_t *>(a + o_offs);  // (positions mod 2^32: the scatter's index width)
     L.bst = reinterpret_cast<uint64_t *>(a + o_bst);
+    L.cst = reinterpret_cast<uint64_t *>(a + o_cst);
     L.tt = reinterpret_cast<TileRef *>(a + o_tt);
     L.ntl = reinterpret_cast<uint32_t *>(a + o_nt);
     L.map = reinterpret_cast<BkMap *>(a + o_map);
@@ -2283,10 +2285,12 @@ static int bk_layout(dsort_ctx *ctx, uint64_t n, int B, size_t smp_bytes, BkLayo
 // d_in into part_out (pure buckets into `direct` when not null).  On return the host holds the
 // bucket starts hb[0..B] and the splitters hspl[0..B-2] (it waits for them while the scatter runs).
 // ioff = the composite index of d_in[0].  `tile` != 0: also the merge path's tile table.
+// compact (the bucket exchange): the keys of pure buckets are dropped and part_out holds the others
+// at the compacted starts (bucket_scan_kernel); hb stays the real starts.
 template <typename T>
 static int first_level(dsort_ctx *ctx, const T *d_in, uint64_t n, uint64_t ioff, T *part_out, T *direct,
                        const BkLayout<T> &L, uint32_t tile, hipStream_t s, bool timed, uint64_t *&hb,
-                       typename bk::Comp<T>::C *&hspl) {
+                       typename bk::Comp<T>::C *&hspl, bool compact = false) {
     using namespace bk;
     using C = typename Comp<T>::C;
     const int B = L.B, BP = L.BP;
@@ -2334,10 +2338,11 @@ static int first_level(dsort_ctx *ctx, const T *d_in, uint64_t n, uint64_t ioff,
     uint64_t *ctot = L.part + (size_t)L.nchunk * B;
     hipLaunchKernelGGL(bucket_colscan_kernel, dim3((unsigned)ceil_div((uint64_t)B, 64)), dim3(BK_MAXB), 0, s, L.part,
                        (uint32_t)L.nchunk, B, ctot);
-    hipLaunchKernelGGL(bucket_scan_kernel, dim3(1), dim3(BK_MAXB), 0, s, L.part, (uint32_t)L.nchunk, B, tile,
-                       (uint32_t)KPC<T>, L.bst, L.tt, L.ntl, (const uint64_t *)ctot);
+    hipLaunchKernelGGL(bucket_scan_kernel<T>, dim3(1), dim3(BK_MAXB), 0, s, L.part, (uint32_t)L.nchunk, B, tile,
+                       (uint32_t)KPC<T>, L.bst, L.tt, L.ntl, (const uint64_t *)ctot, compact ? L.spl : nullptr, L.cst);
     hipLaunchKernelGGL(bucket_offsets_kernel<uint32_t>, dim3((unsigned)L.nchunk), dim3(BK_MAXB), 0, s, L.cnt, L.part,
-                       L.bst, (uint32_t)L.G, B, L.offs);
+                       compact ? L.cst : L.bst, (uint32_t)L.G, B, L.offs);
+    if (compact) direct = part_out;  // (a pure bucket's keys are dropped by the scatter: nothing goes there)
     DSORT_HIP(ctx, hipGetLastError());
     // bucket starts to the host (the second level is planned from the bucket sizes); the host
     // waits for them while the scatter runs.  (The copies run on the side stream once the offsets
@@ -2720,9 +2725,12 @@ int bx_sample(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, BxSample *d_smp, 
     return DSORT_OK;
 }
 
+#ifndef DSORT_BX_DROP_PURE
+#define DSORT_BX_DROP_PURE 1
+#endif
 template <typename T>
 int bx_partition(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, const BxSample *d_all, hipStream_t s, bool timed,
-                 const uint64_t **hb_out, T **part) {
+                 const uint64_t **hb_out, T **part, std::vector<uint8_t> &pure) {
     using namespace wv;
     using C = typename bk::Comp<T>::C;
     ctx->stages_done = 0;
@@ -2760,7 +2768,8 @@ int bx_partition(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, const BxSample
     uint64_t *hb;
     C *hspl;
     if (pl.n_local) {
-        rc = first_level<T>(ctx, d_in, pl.n_local, pl.ioff[pl.me], scratch, nullptr, L, 0u, s, timed, hb, hspl);
+        rc = first_level<T>(ctx, d_in, pl.n_local, pl.ioff[pl.me], scratch, nullptr, L, 0u, s, timed, hb, hspl,
+                            DSORT_BX_DROP_PURE != 0);
         if (rc) return rc;
     } else {
         // no keys here: empty buckets (the splitters still go to the host for the second level)
@@ -2772,14 +2781,20 @@ int bx_partition(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, const BxSample
         fault_point(ctx, s, 0);
     }
     if ((rc = stage_event(ctx, s, timed, 2))) return rc;  // the local part done: the exchange starts
+    // (the scatter's rule, bucket_scatter_lines_kernel / bucket_scan_kernel: the same splitters on
+    // every rank, which derive every rank's compacted starts from its bucket starts)
+    pure.assign((size_t)pl.Btot, 0);
+    for (int g = 1; DSORT_BX_DROP_PURE && g + 1 < pl.Btot; ++g)
+        pure[(size_t)g] = bk::Comp<T>::key_of(hspl[g - 1]) == bk::Comp<T>::key_of(hspl[g]) ? 1 : 0;
     *hb_out = hb;
     *part = scratch;
     return DSORT_OK;
 }
 
 template <typename T>
-int bx_local_sort(dsort_ctx *ctx, T *recv, T *out, const BxPlan &pl, const uint64_t *hb_all, const uint64_t *base,
-                  int j_lo, int j_hi, uint64_t out_off, int w, int W, hipStream_t s, bool timed, uint64_t *n_out) {
+int bx_local_sort(dsort_ctx *ctx, T *recv, T *out, const BxPlan &pl, const uint64_t *hb_all, const uint64_t *hc_all,
+                  const uint64_t *base, int j_lo, int j_hi, uint64_t out_off, int w, int W, hipStream_t s, bool timed,
+                  uint64_t *n_out) {
     using namespace wv;
     using C = typename bk::Comp<T>::C;
     const int P = pl.P, me = pl.me, Bt = pl.Btot, Bl = j_hi - j_lo;  // (Bl: this wave's buckets)
@@ -2796,10 +2811,10 @@ int bx_local_sort(dsort_ctx *ctx, T *recv, T *out, const BxPlan &pl, const uint6
         pm.first[j] = (uint32_t)pm.p.size();
         uint64_t tot = 0;
         for (int r = 0; r < P; ++r) {
-            const uint64_t *h = hb_all + (size_t)r * (Bt + 1);
-            const uint64_t len = h[g + 1] - h[g];
-            if (len) pm.p.push_back(SrcPiece{base[r] + (h[g] - h[g0]), len});
-            tot += len;
+            const uint64_t *h = hb_all + (size_t)r * (Bt + 1), *hc = hc_all + (size_t)r * (Bt + 1);
+            const uint64_t len = hc[g + 1] - hc[g];  // (0 for a pure bucket whose keys stayed home)
+            if (len) pm.p.push_back(SrcPiece{base[r] + (hc[g] - hc[g0]), len});
+            tot += h[g + 1] - h[g];
         }
         hbo[j + 1] = hbo[j] + tot;
         // a global bucket between two splitters of one key holds only that key
@@ -2864,13 +2879,15 @@ int bx_local_sort(dsort_ctx *ctx, T *recv, T *out, const BxPlan &pl, const uint6
 template int bx_sample<int32_t>(dsort_ctx *, const int32_t *, const BxPlan &, BxSample *, hipStream_t);
 template int bx_sample<int64_t>(dsort_ctx *, const int64_t *, const BxPlan &, BxSample *, hipStream_t);
 template int bx_partition<int32_t>(dsort_ctx *, const int32_t *, const BxPlan &, const BxSample *, hipStream_t, bool,
-                                   const uint64_t **, int32_t **);
+                                   const uint64_t **, int32_t **, std::vector<uint8_t> &);
 template int bx_partition<int64_t>(dsort_ctx *, const int64_t *, const BxPlan &, const BxSample *, hipStream_t, bool,
-                                   const uint64_t **, int64_t **);
+                                   const uint64_t **, int64_t **, std::vector<uint8_t> &);
 template int bx_local_sort<int32_t>(dsort_ctx *, int32_t *, int32_t *, const BxPlan &, const uint64_t *,
-                                    const uint64_t *, int, int, uint64_t, int, int, hipStream_t, bool, uint64_t *);
+                                    const uint64_t *, const uint64_t *, int, int, uint64_t, int, int, hipStream_t, bool,
+                                    uint64_t *);
 template int bx_local_sort<int64_t>(dsort_ctx *, int64_t *, int64_t *, const BxPlan &, const uint64_t *,
-                                    const uint64_t *, int, int, uint64_t, int, int, hipStream_t, bool, uint64_t *);
+                                    const uint64_t *, const uint64_t *, int, int, uint64_t, int, int, hipStream_t, bool,
+                                    uint64_t *);
 
 namespace wv {
 
