@@ -111,6 +111,21 @@ def test_bucket_exchange_bit_exact(tmp_path, world, dtype, dist):
         assert max(sizes) <= 1.1 * n / world, sizes
 
 
+def test_bucket_exchange_pure_buckets_stay_home(tmp_path):
+    """Round 6: a global bucket between two splitters of one key (pure) is filled with that key by
+    its owner; the first level drops its keys and writes the others at compacted starts, so they
+    never cross to another rank.  8 distinct keys over 192 global buckets: every key has ~24
+    splitters, nearly every key lies in a pure bucket, and almost nothing is shipped -- against
+    about 2/3 of the keys when everything crossed."""
+    world = 3
+    n = world * (1 << 22) + 12_345
+    ins, outs, meta = run_ranks(tmp_path, world, n, "i32", "few", opts={"all": {"buckets": 192, "test_wave_fence": 1}})
+    assert all(m["stats"]["exchange_path"] == 1 for m in meta), [m["stats"]["exchange_path"] for m in meta]
+    assert np.array_equal(np.concatenate(outs), np.sort(ins))
+    sent = sum(m["stats"]["keys_sent"] for m in meta)
+    assert sent <= 0.05 * n, sent
+
+
 def test_small_sample_sort_takes_the_merge_path(tmp_path):
     """Below 2^22 keys per rank the sample sort sorts locally and merges the received runs."""
     ins, outs, meta = run_ranks(tmp_path, 2, 1_000_003)
