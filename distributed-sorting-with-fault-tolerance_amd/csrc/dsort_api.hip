@@ -72,13 +72,21 @@ int ensure(dsort_ctx *ctx, void **buf, size_t *have, size_t need, const char *wh
 
 void release_dev(dsort_ctx *ctx, void *p) {
     if (!p) return;
-    if (ctx->poll_waits) ctx->dev_later.push_back(p);
-    else (void)hipFree(p);
+    if (ctx->poll_waits) {
+        ctx->dev_later.push_back(p);
+        ++ctx->deferred_n;
+    } else {
+        (void)hipFree(p);
+    }
 }
 void release_host(dsort_ctx *ctx, void *p) {
     if (!p) return;
-    if (ctx->poll_waits) ctx->host_later.push_back(p);
-    else (void)hipHostFree(p);
+    if (ctx->poll_waits) {
+        ctx->host_later.push_back(p);
+        ++ctx->deferred_n;
+    } else {
+        (void)hipHostFree(p);
+    }
 }
 void flush_later(dsort_ctx *ctx) {
     for (void *p : ctx->dev_later) (void)hipFree(p);
@@ -828,7 +836,13 @@ static int sample_sort_bx(dsort_ctx *ctx, const T *d_in, const BxPlan &pl, T **d
     }
     // the receives have landed (and the test hold, DSORT_OPT_TEST_HOLD_EXCHANGE, is released)
     rc = exch_wait(ctx, cs, true, deadline, "key all-to-all", ctx->opt.test_hold_exchange != 0);
-    if (rc) return rc;
+    if (rc) {
+        // (a failed final wait has aborted the communicator, or met a HIP error: the arenas the
+        // second level replaced go once the sort stream is idle, as on the failures above --
+        // tests/test_gpu_faults.py::test_faulted_exchanges_release_replaced_arenas)
+        if (hipStreamSynchronize(s) == hipSuccess) flush_later(ctx);
+        return rc;
+    }
     flush_later(ctx);  // (the buffers the second level replaced while the keys were in flight)
     ctx->last_stream = s;
     ctx->stats.keys_in = pl.n_local;
@@ -1100,6 +1114,17 @@ static int sample_sort(dsort_ctx *ctx, const T *d_in, size_t n_local, T **d_out,
 using namespace dsort;
 
 // ======================================================================== C ABI =========
+// (stats.deferred_frees / pending_frees of the call, whatever it returns)
+template <typename T>
+static int sample_sort_entry(dsort_ctx *ctx, const T *d, size_t n, T **o, size_t *no, void *st, bool presorted) {
+    if (!ctx) return DSORT_EINVAL;
+    const uint64_t d0 = ctx->deferred_n;
+    const int rc = sample_sort<T>(ctx, d, n, o, no, st, presorted);
+    ctx->stats.deferred_frees = (int)(ctx->deferred_n - d0);
+    ctx->stats.pending_frees = (int)(ctx->dev_later.size() + ctx->host_later.size());
+    return rc;
+}
+
 extern "C" {
 
 const char *dsort_version(void) { return DSORT_VERSION_STRING; }
@@ -1483,16 +1508,16 @@ int dsort_comm_destroy(dsort_ctx *ctx) {
 }
 
 int dsort_sample_sort_dev_i32(dsort_ctx *ctx, const int32_t *d, size_t n, int32_t **o, size_t *no, void *st) {
-    return sample_sort<int32_t>(ctx, d, n, o, no, st, false);
+    return sample_sort_entry<int32_t>(ctx, d, n, o, no, st, false);
 }
 int dsort_sample_sort_dev_i64(dsort_ctx *ctx, const int64_t *d, size_t n, int64_t **o, size_t *no, void *st) {
-    return sample_sort<int64_t>(ctx, d, n, o, no, st, false);
+    return sample_sort_entry<int64_t>(ctx, d, n, o, no, st, false);
 }
 int dsort_sample_merge_dev_i32(dsort_ctx *ctx, const int32_t *d, size_t n, int32_t **o, size_t *no, void *st) {
-    return sample_sort<int32_t>(ctx, d, n, o, no, st, true);
+    return sample_sort_entry<int32_t>(ctx, d, n, o, no, st, true);
 }
 int dsort_sample_merge_dev_i64(dsort_ctx *ctx, const int64_t *d, size_t n, int64_t **o, size_t *no, void *st) {
-    return sample_sort<int64_t>(ctx, d, n, o, no, st, true);
+    return sample_sort_entry<int64_t>(ctx, d, n, o, no, st, true);
 }
 
 int dsort_plan_sample_positions(size_t n, int s, uint64_t *idx) {

@@ -172,6 +172,7 @@ struct dsort_ctx {
     // buffers replaced while poll_waits is set: hipFree / hipHostFree synchronize the device, which
     // would wait for the comm stream, so they are released once the exchange is over (flush_later)
     std::vector<void *> dev_later, host_later;
+    uint64_t deferred_n = 0;  // arenas whose release was deferred so far (stats.deferred_frees)
     // stage timing
     hipEvent_t ev[30] = {};  // 0 start, 1 tile sort done, 2 local sort done, 3 exchange done,
                              // 4 final merge done, 5/6 around the key all-to-all, 7/8 around the

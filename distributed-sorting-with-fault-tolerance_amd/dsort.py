@@ -72,7 +72,8 @@ class Stats(ctypes.Structure):
                 ("sub_partition_ms", ctypes.c_double), ("sub_split_subbuckets", ctypes.c_int),
                 ("sub_scatter_fallback", ctypes.c_int), ("exchange_path", ctypes.c_int),
                 ("first_level_map", ctypes.c_int),
-                ("fence_ranges", ctypes.c_int)]  # ABI 6
+                ("fence_ranges", ctypes.c_int),  # ABI 6
+                ("deferred_frees", ctypes.c_int), ("pending_frees", ctypes.c_int)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -96,6 +96,9 @@ typedef struct dsort_stats {
     /* ABI 6 */
     int fence_ranges;         /* DSORT_OPT_TEST_WAVE_FENCE: device ranges the last sample sort's wave
                                  fence found unchanged across its first wave (0: no fence ran) */
+    int deferred_frees;       /* the last sample sort: arenas it replaced while keys were in flight,
+                                 whose release waited for the exchange's end */
+    int pending_frees;        /* ... of those, still held when it returned (0, failed or not) */
 } dsort_stats;
 
 /* ---------------------------------------------------------------- lifecycle ---------- */

@@ -195,6 +195,48 @@ def test_held_exchange_times_out_at_the_deadline(gpu_ctx):
     ctx.comm_destroy()
 
 
+def test_faulted_exchanges_release_replaced_arenas(gpu_ctx):
+    """the arenas the second level replaces while the keys are in flight (their release
+    deferred: a device-wide synchronize could hang on a dead peer's stream) are freed once no kernel
+    can touch them -- also when the exchange fails (dsort_api.hip sample_sort_bx: the abort, the
+    sort stream's drain, then flush_later).  Three bucket exchanges of growing size, each ending in
+    DSORT_ETIMEOUT at the held final wait for the all-to-all, after the second level has grown its
+    arenas (a failure inside the waves takes the same release, round 5): every one
+    returns with nothing pending (dsort_stats.pending_frees), the larger ones having deferred some
+    (deferred_frees: the path is exercised), and a good sort follows."""
+    import torch
+
+    import dsort
+    ctx = gpu_ctx
+    sizes = [(1 << 24) + 11, (1 << 26) + 13, (1 << 27) + 17]
+    t = torch.empty(sizes[-1], dtype=torch.int32, device="cuda")
+    ctx.gen_uniform(t, SEED, 5)
+    fp = ctx.fingerprint(t)
+    deferred = []
+    for n in sizes:
+        ctx.comm_init(1, 0, dsort.Context.unique_id())
+        # (a deadline the second level meets: the sort times out in the held final wait, after both
+        # waves ran and grew their arenas)
+        with ctx.options(test_hold_exchange=1, comm_timeout_ms=3000):
+            with pytest.raises(dsort.DsortError, match="ETIMEOUT.*key all-to-all"):
+                ctx.sample_sort_dev(t[:n])
+        st = ctx.stats()
+        assert st["pending_frees"] == 0, st
+        deferred.append(st["deferred_frees"])
+        ctx.comm_destroy()
+    assert sum(deferred[1:]) > 0, deferred  # (the grown second-level arenas)
+    ctx.comm_init(1, 0, dsort.Context.unique_id())
+    try:
+        ptr, nout = ctx.sample_sort_dev(t)
+        ctx.synchronize()
+        assert nout == sizes[-1] and _sorted_slice_ok(ctx, ptr, nout, fp)
+        assert ctx.stats()["pending_frees"] == 0
+    finally:
+        ctx.comm_destroy()
+    del t
+    torch.cuda.empty_cache()
+
+
 def test_c_master_rccl_one_gpu_with_comm_deadline():
     """dsort_master --mode samplesort over RCCL on this box's one GPU with an exchange deadline
     (DSORT_OPT_COMM_TIMEOUT_MS: every polled wait of the exchange and the communicator set-up)."""
