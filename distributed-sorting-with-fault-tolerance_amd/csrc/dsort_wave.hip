@@ -957,7 +957,11 @@ __device__ __forceinline__ void gather_pieces(const sb::Gather &ga, uint32_t jt,
         pe[q] = k < ga.PS ? ga.pieces[(uint64_t)jt * ga.PS + k] : make_uint2(0u, 0u);
     }
 }
-// ptab: 3 kMaxPieces + 1 words of LDS for the piece table; wsum: one word per wave.
+// ptab: 3 kMaxPieces + 1 words of LDS for the piece table, then (DSORT_GATHER_VPC) TILE / N 16-bit
+// piece indices of the vector slots; wsum: one word per wave.
+#ifndef DSORT_GATHER_VPC
+#define DSORT_GATHER_VPC 1
+#endif
 template <typename T, int W>
 __device__ __forceinline__ void gather_tile(const sb::Gather &ga, const uint2 (&pe)[2], const sb::GTile &gt,
                                             const T *in, uint32_t *ptab, uint32_t *wsum, T (&x)[R],
@@ -993,6 +997,16 @@ __device__ __forceinline__ void gather_tile(const sb::Gather &ga, const uint2 (&
         ex += i < w ? v : 0;
         tot += v;
     }
+    // DSORT_GATHER_VPC (round 6): with small pieces (under 20 vectors on average: a C3 rank's tiles
+    // gather 273 pieces of ~60 int32 keys) the piece of every vector slot (16-bit, behind the piece
+    // table), written by the piece's thread -- a lane's loads then look their piece up with one read
+    // each, independently, where the walk up the pieces (a binary search for the first, then a step
+    // per piece boundary crossed, each an LDS round trip the next load's address waited for) chained
+    // up to ~25 round trips in front of the last load.  C3 rank: tile sort 1.51 -> 1.38 ms; with the
+    // one-GPU sort's ~30-vector pieces the fill cost more than the walk (+0.04 ms), so those walk
+    // (profiles/r6_ab_gather_vpc.log).  Workgroup-uniform.
+    const bool vp = DSORT_GATHER_VPC && !keyw && tot < 20u * (uint32_t)np;
+    uint16_t *vpc = reinterpret_cast<uint16_t *>(phi + KP);
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
         const int k = 2 * tid + q;
@@ -1000,6 +1014,8 @@ __device__ __forceinline__ void gather_tile(const sb::Gather &ga, const uint2 (&
             voff[k] = ex;
             plo[k] = lo[q];
             phi[k] = hi[q];
+            if (vp)
+                for (uint32_t v = ex; v < ex + nv[q]; ++v) vpc[v] = (uint16_t)k;
         }
         ex += nv[q];
     }
@@ -1032,6 +1048,23 @@ __device__ __forceinline__ void gather_tile(const sb::Gather &ga, const uint2 (&
         return;
     }
     const uint32_t e0 = (uint32_t)(w * (WK / N) + lane);
+    if (vp) {
+        uint32_t keep = 0;  // bit N i + j: key j of vector i belongs to the tile
+#pragma unroll
+        for (int i = 0; i < R / N; ++i) {
+            const uint32_t e = e0 + 64 * i;
+            if (e < tot) {
+                const uint32_t k = vpc[e], pl = plo[k], ph = phi[k];
+                const uint32_t g = (pl / N - voff[k] + e) * N;  // first key of the vector
+                V16<T>::get(*reinterpret_cast<const V *>(in + g), x + N * i);
+#pragma unroll
+                for (int j = 0; j < N; ++j) keep |= (uint32_t)(g + j >= pl && g + j < ph) << (N * i + j);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < R; ++i) x[i] = (keep >> i) & 1 ? x[i] : key_max<T>();
+        return;
+    }
     // piece of vector slot e0: the last k with voff[k] <= e0
     int a = 0, b = np;
     while (b - a > 1) {
@@ -1135,7 +1168,8 @@ __global__ void __launch_bounds__(64 * W, WG<T>::OCC) bin_sort_kernel(const T *i
                                                                      sb::Gather ga, uint32_t *fb, uint32_t *nfb,
                                                                      uint32_t toff) {
     constexpr int TILE = TILE_W<W>;
-    static_assert(128 + 3 * kMaxPieces<T> + 1 <= TILE * (int)sizeof(T) / 4, "the piece table fits in the tile");
+    static_assert(128 + 3 * kMaxPieces<T> + 1 + (TILE / KPC<T> + 1) / 2 <= TILE * (int)sizeof(T) / 4,
+                  "the piece table and the vector slots' pieces fit in the tile");
     __shared__ __attribute__((aligned(16))) T s[TILE];
     __shared__ __attribute__((aligned(16))) uint32_t cw[BIN_NB<W> / 2];
     // the counters are zeroed before the gather's barriers; the piece table of a gathered tile and
