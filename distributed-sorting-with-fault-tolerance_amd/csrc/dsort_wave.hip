@@ -2106,20 +2106,34 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
         DSORT_HIP(ctx, hipGetLastError());
         const Gather ga{static_cast<const GTile *>(tt), dch, dbi, cnt, pcs, PS, SS, spl, bspl, B,
                         (uint32_t)std::max<uint64_t>(tcap, 1)};
+        // (few buckets, round 6: the piece tables' kernel goes out before the tile count is read
+        // back, on a grid for the tile tables' capacity -- its workgroups past the count return at
+        // once -- so the early tile sort can follow it and the host's wait for the count runs under
+        // both: a C3 rank's two waves each idled the GPU ~40 us between the scan and the tile sort)
+#ifndef DSORT_PIECES_EARLY
+#define DSORT_PIECES_EARLY 1
+#endif
+        const bool pieces_early = DSORT_PIECES_EARLY && !pieces_in_scan && pcs && tcap > 0;
+        if (pieces_early) {
+            hipLaunchKernelGGL(sb_pieces_kernel, dim3((unsigned)ceil_div(tcap, 4)), dim3(256), 0, s,
+                               static_cast<const GTile *>(tt), num, static_cast<const Chunk *>(dch), cnt, SS, pcs, PS,
+                               (uint32_t)tcap);
+            DSORT_HIP(ctx, hipGetLastError());
+        }
         DSORT_HIP(ctx, hipMemcpyAsync(hn, num, 8, hipMemcpyDeviceToHost, s));
         DSORT_HIP(ctx, hipEventRecord(ctx->sub_ev, s));
         // The tile sort of the first `early` tiles goes out behind the count's read-back, before the
         // host waits for it: every tile holds at most TILE keys, so there are at least (keys in
         // tiles) / TILE of them.  The rest follow the count (at 2^30 int32 ~15 % of the tiles), and
         // the wait -- the read-back, then the launch -- runs under the first part instead of idling
-        // the GPU (about 35 us per sort).  (With the piece tables made by the scan only: a kernel of
-        // their own needs the count for its grid.  Not under a stage-1 kill point, which must see
+        // the GPU (about 35 us per sort).  (With the piece tables made by the scan, or by their own
+        // kernel on a grid for the tables' capacity, pieces_early.  Not under a stage-1 kill point, which must see
         // the second level finished and nothing after it.)
 #ifndef DSORT_TILE_EARLY
 #define DSORT_TILE_EARLY 1
 #endif
         const uint64_t ebound = (n - npure) / (uint64_t)TILE;
-        const uint32_t early = DSORT_TILE_EARLY && pieces_in_scan && ctx->opt.kill_after_pass != 1
+        const uint32_t early = DSORT_TILE_EARLY && (pieces_in_scan || pieces_early) && ctx->opt.kill_after_pass != 1
                                    ? (uint32_t)std::min<uint64_t>(ebound, tcap)
                                    : 0u;
         if (early) {
@@ -2149,7 +2163,7 @@ static int sub_sort(dsort_ctx *ctx, T *src, T *d_keys, uint64_t n, const uint64_
                                fill_keys);
         }
         // every tile's piece table
-        if (ntiles && !pieces_in_scan) {
+        if (ntiles && !pieces_in_scan && !pieces_early) {
             hipLaunchKernelGGL(sb_pieces_kernel, dim3((unsigned)ceil_div(ntiles, 4)), dim3(256), 0, s,
                                static_cast<const GTile *>(tt), num, static_cast<const Chunk *>(dch), cnt, SS, pcs, PS,
                                (uint32_t)tcap);
