@@ -836,8 +836,12 @@ __device__ __forceinline__ uint32_t sb_chunk_order(uint32_t bid, uint32_t G) {
 
 // int32: 1024 threads of 15 keys, 8 waves per SIMD at two workgroups per CU: twice the waves of
 // round 2's 512 threads of 31 keys to hide the lookups' LDS round trips (2.33 -> 2.02 ms at 2^30).
-// (int64 at 1024 threads of 6 keys: round 4 C4 -0.24 ms, 2^30 uniform int64 +0.4 ms; round 5, with the
-// one-key slots, C4 +0.9 ms (profiles/r5_ab_c4_local_1024x6.log): kept at 512 x 13)
+// int64 (round 6): 1024 threads of 6 keys, lookups in pairs (DSORT_SB_G64) -- round 5 measured this
+// geometry with 8-key batches, which spilled 22 VGPRs at 8 waves per SIMD (C4 +0.9 ms,
+// profiles/r5_ab_c4_local_1024x6.log); in pairs nothing spills, and since the first level's one-key
+// hash (dsort_bucket.h bucket_onekey) C4's buckets hold hardly any duplicate run: C4 second level
+// 2.21 -> 1.82 ms, uniform int64 3.78 -> 3.48 ms (profiles/r6_ab_local_partition_i64_1024x6.log;
+// 512 x 13 with 8-key batches before)
 #ifndef DSORT_SB_LT32
 #define DSORT_SB_LT32 1024
 #endif
@@ -847,9 +851,15 @@ __device__ __forceinline__ uint32_t sb_chunk_order(uint32_t bid, uint32_t G) {
 #ifndef DSORT_SB_G32
 #define DSORT_SB_G32 1  // int32 keys per batch of the classify (G below)
 #endif
-template <typename T> constexpr int SB_LT = sizeof(T) == 4 ? DSORT_SB_LT32 : 512;
-// keys per thread: the chunk (int32 60 KiB, int64 52 KiB) + tables fit two workgroups per CU
-template <typename T> constexpr int SB_LKPT = sizeof(T) == 4 ? DSORT_SB_KPT32 : 13;
+#ifndef DSORT_SB_LT64
+#define DSORT_SB_LT64 1024
+#endif
+#ifndef DSORT_SB_KPT64
+#define DSORT_SB_KPT64 6
+#endif
+template <typename T> constexpr int SB_LT = sizeof(T) == 4 ? DSORT_SB_LT32 : DSORT_SB_LT64;
+// keys per thread: the chunk (int32 60 KiB, int64 48 KiB) + tables fit two workgroups per CU
+template <typename T> constexpr int SB_LKPT = sizeof(T) == 4 ? DSORT_SB_KPT32 : DSORT_SB_KPT64;
 
 template <typename T> constexpr int SB_LCH = SB_LT<T> * SB_LKPT<T>;
 
@@ -921,7 +931,10 @@ __global__ void __launch_bounds__(SB_LT<T>, SB_LT<T> / 128) sb_local_kernel(T *_
     // In groups of G keys: the slot-table reads, then the splitter reads, then the atomics, so a
     // key's LDS round trips do not wait for the previous key's.  A key past the chunk adds 0.
     // (int32: 31 keys and their ranks are already live; batching spills and measured slower)
-    constexpr int G = sizeof(T) == 4 ? DSORT_SB_G32 : 8;
+#ifndef DSORT_SB_G64
+#define DSORT_SB_G64 2
+#endif
+    constexpr int G = sizeof(T) == 4 ? DSORT_SB_G32 : DSORT_SB_G64;
     // a whole chunk: only the first and last slot rows can fall outside it
     const bool whole = c.len == (uint32_t)CHL;
     if constexpr (G == 1) {
