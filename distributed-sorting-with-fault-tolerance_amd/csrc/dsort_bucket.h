@@ -50,7 +50,10 @@ template <typename T> struct Geo;
 template <> struct Geo<int32_t> { static constexpr int KPT = 16; };  // (14: +0.09 ms; 12, 13 slower still)
 // int64: 48 KiB next to the 64 KiB carry (8 keys with the splitters read from global memory on
 // the lookups: C4 scatter 6.47 -> 7.09 ms)
-template <> struct Geo<int64_t> { static constexpr int KPT = 6; };
+#ifndef DSORT_BK_KPT64
+#define DSORT_BK_KPT64 6
+#endif
+template <> struct Geo<int64_t> { static constexpr int KPT = DSORT_BK_KPT64; };
 // Bucket ids (int64, skewed keys): the histogram stores every key's bucket (2 bytes) and the
 // scatter reads it instead of repeating the lookup, when the lookup is the expensive one -- the log
 // slot map or one-key slots (BkMap.ids, set by bucket_slotmap_kernel): at 2^30 Zipf (C4) scatter
@@ -819,7 +822,7 @@ __global__ void __launch_bounds__(BK_T, 2) bucket_hist_kernel(const T *__restric
     using CT = Comp<T>;
     constexpr bool ADP = CT::ADAPT || AD;
     constexpr int KPT = Geo<T>::KPT, SUB = BK_T * KPT;
-    static_assert(!BkIds<T>::ON || KPT % 2 == 0, "bucket ids two per word");
+    static_assert(!BkIds<T>::ON || KPT % BkIds<T>::PER_WORD == 0, "bucket ids: whole words per thread");
     __shared__ typename CT::C spl[BK_MAXB + 1];
     __shared__ uint32_t rng[BK_SLOTS];
     const BkMap m = *map;
