@@ -70,6 +70,19 @@ template <> struct Geo<int64_t> { static constexpr int KPT = DSORT_BK_KPT64; };
 #ifndef DSORT_BK_IDS3
 #define DSORT_BK_IDS3 1
 #endif
+// Non-temporal stores (round 6) for the histogram's bucket ids and the int32 scatter's whole lines:
+// written once and read by a later kernel after gigabytes of other traffic, they gain nothing from
+// the caches.  2^30 int32 7.52 -> 7.46 ms of device time (4 of 4 interleaved runs), C4 10.81 ->
+// 10.75 ms (profiles/r6_ab_nontemporal_lines_ids.log); the int64 scatter's lines measured neutral to
+// worse, and the fill of the pure buckets +0.25 ms (profiles/r6_ab_fill_nontemporal_dropped.log).
+#ifndef DSORT_IDS_NT
+#define DSORT_IDS_NT 1
+#endif
+#ifndef DSORT_LINES_NT
+#define DSORT_LINES_NT 1  // (bit 0: int32, bit 1: int64)
+#endif
+typedef int bk_v4i __attribute__((ext_vector_type(4)));
+typedef long long bk_v2l __attribute__((ext_vector_type(2)));
 template <typename T> struct BkIds {
 #ifdef DSORT_BK_IDS32
     static constexpr bool ON = true;
@@ -893,7 +906,13 @@ __global__ void __launch_bounds__(BK_T, 2) bucket_hist_kernel(const T *__restric
             if constexpr (PW == 3) {
                 uint32_t *dst = ids + (b0 - threadIdx.x) / SUB * (KPT / 3) * BK_T + threadIdx.x;
 #pragma unroll
-                for (int w = 0; w < KPT / 3; ++w) dst[w * BK_T] = idw[w];
+                for (int w = 0; w < KPT / 3; ++w) {
+#if DSORT_IDS_NT
+                    __builtin_nontemporal_store(idw[w], dst + w * BK_T);
+#else
+                    dst[w * BK_T] = idw[w];
+#endif
+                }
             } else {
                 uint32_t *dst = ids + (b0 - threadIdx.x) / 2 + (uint64_t)threadIdx.x * (KPT / 2);
 #pragma unroll
@@ -1394,9 +1413,16 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
             const uint32_t gi = sgb[b] + e0;  // mod 2^32
             T *tgt = (sb.y >> 10) & 1 ? out2 : out;
             if (full) {
-                V vv;
-                __builtin_memcpy(&vv, v, sizeof(V));
-                *reinterpret_cast<V *>(tgt + gi) = vv;
+                if constexpr ((DSORT_LINES_NT >> (sizeof(T) == 8 ? 1 : 0)) & 1) {
+                    using NV = typename std::conditional<sizeof(T) == 4, bk_v4i, bk_v2l>::type;
+                    NV vv;
+                    __builtin_memcpy(&vv, v, sizeof(NV));
+                    __builtin_nontemporal_store(vv, reinterpret_cast<NV *>(tgt + gi));
+                } else {
+                    V vv;
+                    __builtin_memcpy(&vv, v, sizeof(V));
+                    *reinterpret_cast<V *>(tgt + gi) = vv;
+                }
             } else {
 #pragma unroll
                 for (int t = 0; t < KPL; ++t)
