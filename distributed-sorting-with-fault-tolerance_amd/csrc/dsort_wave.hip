@@ -741,6 +741,12 @@ __device__ __forceinline__ void window_pass(T *s, int P, int tid) {
     for (int q = 0; q < 16 / N; ++q) *p[q] = V16<T>::make(v + N * q);
 }
 
+// The tile sort's output as non-temporal stores (round 6, int32: bit 0; int64 bit 1): 2^30 int32
+// 7.56 -> 7.50 ms of device time over 3 of 3 interleaved runs, C4 neutral; the local partition's
+// in-place write-back the same way measured neutral (profiles/r6_ab_nontemporal_tile_out.log).
+#ifndef DSORT_TILE_OUT_NT
+#define DSORT_TILE_OUT_NT 1
+#endif
 // Bin sort of one tile held in x (slots past `valid` are key_max) into out[0, valid).
 //   1. range [mn, mx] of the keys below key_max (they and the padding are not binned: the output
 //      ends with valid - M of them, M = the binned keys);
@@ -908,7 +914,14 @@ __device__ __forceinline__ bool bin_sort_tile(const T (&x)[R], int valid, T *s, 
             const int p0 = N * q;
             const V v = *reinterpret_cast<const V *>(s + bsw<T>((uint32_t)p0));
             if (p0 >= sh && p0 + N <= E) {
-                *reinterpret_cast<V *>(ob + p0) = v;
+                if constexpr ((DSORT_TILE_OUT_NT >> (sizeof(T) == 8 ? 1 : 0)) & 1) {
+                    using NV = typename std::conditional<sizeof(T) == 4, bk::bk_v4i, bk::bk_v2l>::type;
+                    NV nv;
+                    __builtin_memcpy(&nv, &v, sizeof(NV));
+                    __builtin_nontemporal_store(nv, reinterpret_cast<NV *>(ob + p0));
+                } else {
+                    *reinterpret_cast<V *>(ob + p0) = v;
+                }
             } else {
                 T k[N];
                 V16<T>::get(v, k);
