@@ -742,10 +742,11 @@ __device__ __forceinline__ void window_pass(T *s, int P, int tid) {
 }
 
 // The tile sort's output as non-temporal stores (round 6, int32: bit 0; int64 bit 1): 2^30 int32
-// 7.56 -> 7.50 ms of device time over 3 of 3 interleaved runs, C4 neutral; the local partition's
-// in-place write-back the same way measured neutral (profiles/r6_ab_nontemporal_tile_out.log).
+// 7.56 -> 7.50 ms of device time over 3 of 3 interleaved runs; 2^30 uniform int64 16.43 -> 16.21 ms
+// (3 of 3), C4 neutral; the local partition's in-place write-back the same way measured neutral
+// (profiles/r6_ab_nontemporal_tile_out.log, r6_ab_nontemporal_i64.log).
 #ifndef DSORT_TILE_OUT_NT
-#define DSORT_TILE_OUT_NT 1
+#define DSORT_TILE_OUT_NT 3
 #endif
 // Bin sort of one tile held in x (slots past `valid` are key_max) into out[0, valid).
 //   1. range [mn, mx] of the keys below key_max (they and the padding are not binned: the output
