@@ -178,6 +178,11 @@ __global__ void __launch_bounds__(NT) format_count_kernel(const int32_t *__restr
     if (threadIdx.x == 0) cnt[blockIdx.x] = agg;
 }
 
+// (round 6) the formatted text's whole 16-byte chunks as non-temporal stores: format 1.27-1.30 ->
+// 1.23-1.25 ms at 2^28 keys, 3 of 3 interleaved runs (profiles/r6_ab_text_format_nontemporal.log)
+#ifndef DSORT_TEXT_NT
+#define DSORT_TEXT_NT 1
+#endif
 __global__ void __launch_bounds__(NT) format_kernel(const int32_t *__restrict__ keys, uint64_t n,
                                                     char *__restrict__ text, uint64_t cap,
                                                     const uint64_t *__restrict__ pref) {
@@ -215,7 +220,13 @@ __global__ void __launch_bounds__(NT) format_kernel(const int32_t *__restrict__ 
     for (int c = threadIdx.x; c < nch; c += NT) {
         const int lo_b = c * 16, hi_b = lo_b + 16;
         if (lo_b >= sh && hi_b <= hi) {
+#if DSORT_TEXT_NT
+            typedef int text_v4i __attribute__((ext_vector_type(4)));
+            __builtin_nontemporal_store(*reinterpret_cast<const text_v4i *>(sb + lo_b),
+                                        reinterpret_cast<text_v4i *>(ga + lo_b));
+#else
             *reinterpret_cast<int4 *>(ga + lo_b) = *reinterpret_cast<const int4 *>(sb + lo_b);
+#endif
         } else {
             const int b0 = lo_b > sh ? lo_b : sh, b1 = hi_b < hi ? hi_b : hi;
             for (int b = b0; b < b1; ++b) ga[b] = sb[b];
