@@ -74,7 +74,9 @@ template <> struct Geo<int64_t> { static constexpr int KPT = DSORT_BK_KPT64; };
 // written once and read by a later kernel after gigabytes of other traffic, they gain nothing from
 // the caches.  2^30 int32 7.52 -> 7.46 ms of device time (4 of 4 interleaved runs), C4 10.81 ->
 // 10.75 ms (profiles/r6_ab_nontemporal_lines_ids.log); the int64 scatter's lines measured neutral to
-// worse, and the fill of the pure buckets +0.25 ms (profiles/r6_ab_fill_nontemporal_dropped.log).
+// worse, and the fill of the pure buckets +0.25 ms (profiles/r6_ab_fill_nontemporal_dropped.log);
+// the sorted-runs instance (HT) keeps cached stores: its long streams of one bucket lost 0.05 ms
+// (sorted and reversed input, profiles/r6_ab_nt_other_inputs.log).
 #ifndef DSORT_IDS_NT
 #define DSORT_IDS_NT 1
 #endif
@@ -1413,7 +1415,7 @@ __global__ void __launch_bounds__(BK_T) bucket_scatter_lines_kernel(const T *__r
             const uint32_t gi = sgb[b] + e0;  // mod 2^32
             T *tgt = (sb.y >> 10) & 1 ? out2 : out;
             if (full) {
-                if constexpr ((DSORT_LINES_NT >> (sizeof(T) == 8 ? 1 : 0)) & 1) {
+                if constexpr (((DSORT_LINES_NT >> (sizeof(T) == 8 ? 1 : 0)) & 1) && !HT) {
                     using NV = typename std::conditional<sizeof(T) == 4, bk_v4i, bk_v2l>::type;
                     NV vv;
                     __builtin_memcpy(&vv, v, sizeof(NV));
